@@ -1,0 +1,212 @@
+"""bench.py — device-resident RLNC encode+repair throughput on MI355X (BASELINE.json metric).
+
+Step = one pass of the hot path over one batch: encode the rank's chunksets (10 -> 16,
+chunkset.rs:43-52) and repair every chunkset from exactly 10 random surviving coded chunks
+(plan + decode, chunkset.rs:173-208), all resident in HBM. Default workload = BASELINE config 2:
+a 1 GiB random blob = 103 chunksets per GPU, all in one batch. For N > 1 each rank owns its own
+1 GiB slice of an N GiB blob (contiguous chunkset-index shard, no collective on the data path);
+value = blob bytes of all ranks / max-over-ranks time ("scaling": "weak").
+
+Launched with torchrun for N > 1 (RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* from the environment).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+GIB = float(1 << 30)
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+CONFIGS = {
+    # name: (blob bytes per GPU, description)
+    "cfg2": (1 << 30, "1 GiB random blob (103 x 10 MiB chunksets) encode + repair from 10 random survivors, one batch"),
+    "cfg3": (16 << 30, "16 GiB random blob (1639 chunksets) encode + repair from 10 random survivors, one batch"),
+}
+
+
+def shard_range(n_total, world, rank):
+    """contiguous chunkset-index shard of rank"""
+    per = -(-n_total // world)
+    lo = min(rank * per, n_total)
+    return lo, min(lo + per, n_total)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--config", default="cfg2", choices=sorted(CONFIGS))
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-sample", type=int, default=0, help="chunksets in the CPU sample (0 = auto)")
+    p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
+    return p.parse_args()
+
+
+def cpu_baseline(n_sample, seed):
+    """The CPU restatement (oracle/, "port") on the host cores: rayon-style chunkset-parallel encode
+    (blob.rs:256-264) + per-chunkset incremental decode (chunkset.rs:173-208)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import numpy as np
+    import oracle as o
+    threads = max(1, min(16, os.cpu_count() or 1))
+    if n_sample <= 0:
+        n_sample = threads
+    blob = o.fill_random(seed, n_sample * o.CS)
+    coeffs = o.fill_random(seed + 1, n_sample * o.N * o.K)
+    rng = np.random.default_rng(seed)
+    cand = np.full((n_sample, o.N), 0xFF, np.uint8)
+    for c in range(n_sample):
+        cand[c, :o.K] = rng.permutation(o.N)[:o.K]
+    t0 = time.perf_counter()
+    coded = o.blob_encode(blob, coeffs, nthreads=threads)
+    t1 = time.perf_counter()
+    out, status = o.blob_repair(coded, cand, blob.size, nthreads=threads)
+    t2 = time.perf_counter()
+    ok = status == 0
+    assert np.array_equal(out.reshape(n_sample, o.CS)[ok], blob.reshape(n_sample, o.CS)[ok])
+    return {"value": n_sample * o.CS / GIB / (t2 - t0), "unit": "GiB/s", "cores": threads, "kind": "port",
+            "sample": "%d chunksets (%.0f MiB) encode+repair, %d threads; encode %.2f s, repair %.2f s"
+                      % (n_sample, n_sample * o.CS / 2 ** 20, threads, t1 - t0, t2 - t1),
+            "encode_gib_s": n_sample * o.CS / GIB / (t1 - t0), "repair_gib_s": n_sample * o.CS / GIB / (t2 - t1)}
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    import decds_amd
+    from decds_amd import codec
+    from decds_amd._capi import CHUNKSET_BYTES as CS, CODED_PIECE_BYTES as F, K, N
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit("--gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    blob_per_gpu, desc = CONFIGS[args.config]
+    n_total = -(-(blob_per_gpu * world) // CS)
+    lo, hi = shard_range(n_total, world, rank)
+    n = hi - lo
+    blob_len_rank = min(blob_per_gpu * world, hi * CS) - lo * CS
+
+    ctx = decds_amd.Context(local)
+    stream = torch.cuda.Stream()
+    dev = torch.device("cuda", local)
+    with torch.cuda.stream(stream):
+        src = torch.zeros(n * CS, dtype=torch.uint8, device=dev)
+        codec.fill_random_device(ctx, 0xDEC05002, src, nbytes=blob_len_rank, byte_offset=lo * CS, stream=stream)
+        coeffs_h = codec.fill_random_host(0xC0EF0002, n * N * K, byte_offset=lo * N * K)
+        rng = np.random.default_rng(0x5EED0002 + rank)
+        cand_h = np.full((n, N), 0xFF, np.uint8)
+        for c in range(n):
+            cand_h[c, :K] = rng.permutation(N)[:K]
+        coeffs = torch.from_numpy(coeffs_h).to(dev)
+        cand = torch.from_numpy(cand_h).to(dev)
+        coded = torch.empty(n * N * F, dtype=torch.uint8, device=dev)
+        plan = torch.empty(n * 128, dtype=torch.uint8, device=dev)
+        verd = torch.empty(n * N, dtype=torch.int8, device=dev)
+        status = torch.empty(n, dtype=torch.int32, device=dev)
+        out = torch.empty(n * CS, dtype=torch.uint8, device=dev)
+    stream.synchronize()
+
+    def step(ev=None):
+        if ev is not None:
+            ev[0].record(stream)
+        codec.encode_batch(ctx, src, n, coeffs, coded, stream=stream)
+        if ev is not None:
+            ev[1].record(stream)
+        codec.repair_plan_batch(ctx, coded, n, cand, plan, verd, status, stream=stream)
+        if ev is not None:
+            ev[2].record(stream)
+        codec.decode_batch(ctx, coded, n, plan, out, status, stream=stream)
+        if ev is not None:
+            ev[3].record(stream)
+
+    for _ in range(args.warmup):
+        step()
+    stream.synchronize()
+    events = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for s in range(args.steps):
+        step(events[s])
+    stream.synchronize()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    enc_ms = sum(e[0].elapsed_time(e[1]) for e in events) / args.steps
+    plan_ms = sum(e[1].elapsed_time(e[2]) for e in events) / args.steps
+    dec_ms = sum(e[2].elapsed_time(e[3]) for e in events) / args.steps
+
+    # correctness of the timed work: every repaired chunkset equals its source
+    st = status.cpu().numpy()
+    ready = torch.from_numpy(st == 0).to(dev)
+    assert set(np.unique(st).tolist()) <= {0, 5}, "unexpected repair status"
+    same = torch.equal(out.view(n, CS)[ready], src.view(n, CS)[ready])
+    assert same, "repaired data differs from the source"
+    n_ready = int((st == 0).sum())
+
+    enc_bytes = n * (CS + N * F)            # algorithmic HBM bytes of one encode launch
+    dec_bytes = n_ready * (K * F + CS)      # ... of one decode launch (ready chunksets only)
+    enc_gbs = enc_bytes / (enc_ms * 1e-3) / 1e9
+    dec_gbs = dec_bytes / (dec_ms * 1e-3) / 1e9
+    dominant = "rlnc_encode_kernel" if enc_ms >= dec_ms else "rlnc_decode_kernel"
+    achieved = enc_gbs if dominant == "rlnc_encode_kernel" else dec_gbs
+    traffic = None
+    try:
+        with open(args.traffic_json) as f:
+            tj = json.load(f)
+        if tj.get("config") == args.config and dominant in tj.get("kernels", {}):
+            traffic = tj["kernels"][dominant]["hbm_bytes_per_launch"]
+    except (OSError, ValueError):
+        pass
+
+    if rank == 0:
+        total_bytes = blob_per_gpu * world * args.steps
+        value = total_bytes / GIB / elapsed
+        line = {
+            "metric": "RLNC encode+repair GiB/s device-resident, 10MB chunksets; % HBM roofline",
+            "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(elapsed * 1e3 / args.steps, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+            "data": "synthetic (SplitMix64 random blob + coding vectors, seeded)",
+            "config": {"workload": args.config + ": " + desc, "chunksets_per_gpu": n,
+                       "blob_bytes_per_gpu": blob_per_gpu, "survivors_per_chunkset": K,
+                       "parallelism": "chunkset-index shards x%d, no collective" % world},
+            "roofline": {"bound": "hbm", "kernel": dominant, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic},
+            "breakdown": {"encode_ms": round(enc_ms, 4), "plan_ms": round(plan_ms, 4), "decode_ms": round(dec_ms, 4),
+                          "encode_GBps": round(enc_gbs, 1), "decode_GBps": round(dec_gbs, 1),
+                          "encode_blob_GiBps": round(n * CS / GIB / (enc_ms * 1e-3), 1),
+                          "repair_blob_GiBps": round(n * CS / GIB / ((plan_ms + dec_ms) * 1e-3), 1),
+                          "ready_chunksets": n_ready, "not_ready_chunksets": n - n_ready},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(args.cpu_sample, 0xDEC05002)
+        else:
+            line["cpu_baseline"] = None
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

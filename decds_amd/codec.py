@@ -1,0 +1,107 @@
+"""Batch codec over device-resident chunksets (torch CUDA tensors as HBM plumbing).
+
+encode_batch / repair_plan_batch / decode_batch are thin wrappers of the C-ABI *_batch entry
+points: they pass raw device pointers and the caller's HIP stream, so the kernels run on the
+stream the caller times with events. blob_encode_host / blob_repair_host mirror Blob::new's
+chunkset loop (blob.rs:244-264) and RepairingBlob's repair driver (blob.rs:373-473) over host
+buffers with overlapped pinned copies.
+"""
+import ctypes
+
+import numpy as np
+
+from ._capi import (CHUNKSET_BYTES, CODED_PIECE_BYTES, K, N, NO_CANDIDATE, REPAIR_PLAN_BYTES, check, lib)
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def _stream(stream):
+    if stream is None:
+        import torch
+        stream = torch.cuda.current_stream()
+    return ctypes.c_void_p(stream.cuda_stream)
+
+
+def _need(t, nbytes, what):
+    if not t.is_cuda:
+        raise TypeError("%s must be a CUDA tensor (device-resident batch API)" % what)
+    if not t.is_contiguous():
+        raise ValueError("%s must be contiguous" % what)
+    if t.numel() * t.element_size() < nbytes:
+        raise ValueError("%s too small: %d < %d bytes" % (what, t.numel() * t.element_size(), nbytes))
+
+
+def encode_batch(ctx, src, n, coeffs, dst, pitch=CODED_PIECE_BYTES, stream=None):
+    """chunkset.rs:43-52 for n chunksets: src n*CS bytes, coeffs n*16*10, dst n*16 rows of `pitch`."""
+    _need(src, n * CHUNKSET_BYTES, "src")
+    _need(coeffs, n * N * K, "coeffs")
+    _need(dst, (n * N - 1) * pitch + CODED_PIECE_BYTES, "dst")
+    check(lib().decds_encode_batch(ctx.handle, _ptr(src), n, _ptr(coeffs), _ptr(dst), pitch, _stream(stream)))
+
+
+def repair_plan_batch(ctx, coded, n, cand, plan, verdicts, status, pitch=CODED_PIECE_BYTES, stream=None):
+    _need(coded, (n * N - 1) * pitch + CODED_PIECE_BYTES, "coded")
+    _need(cand, n * N, "cand")
+    _need(plan, n * REPAIR_PLAN_BYTES, "plan")
+    _need(verdicts, n * N, "verdicts")
+    _need(status, n * 4, "status")
+    check(lib().decds_repair_plan_batch(ctx.handle, _ptr(coded), pitch, n, _ptr(cand), _ptr(plan),
+                                        _ptr(verdicts), _ptr(status), _stream(stream)))
+
+
+def decode_batch(ctx, coded, n, plan, dst, status, pitch=CODED_PIECE_BYTES, stream=None):
+    _need(coded, (n * N - 1) * pitch + CODED_PIECE_BYTES, "coded")
+    _need(plan, n * REPAIR_PLAN_BYTES, "plan")
+    _need(dst, n * CHUNKSET_BYTES, "dst")
+    _need(status, n * 4, "status")
+    check(lib().decds_decode_batch(ctx.handle, _ptr(coded), pitch, n, _ptr(plan), _ptr(dst), _ptr(status),
+                                   _stream(stream)))
+
+
+def repair_batch(ctx, coded, n, cand, plan, verdicts, dst, status, pitch=CODED_PIECE_BYTES, stream=None):
+    repair_plan_batch(ctx, coded, n, cand, plan, verdicts, status, pitch, stream)
+    decode_batch(ctx, coded, n, plan, dst, status, pitch, stream)
+
+
+def fill_random_device(ctx, seed, dst, nbytes=None, byte_offset=0, stream=None):
+    nbytes = dst.numel() * dst.element_size() if nbytes is None else nbytes
+    check(lib().decds_fill_random_device(ctx.handle, seed, byte_offset, _ptr(dst), nbytes, _stream(stream)))
+
+
+def fill_random_host(seed, nbytes, byte_offset=0):
+    out = np.empty(nbytes, dtype=np.uint8)
+    lib().decds_fill_random_host(seed, byte_offset, out.ctypes.data_as(ctypes.c_void_p), nbytes)
+    return out
+
+
+def blob_encode_host(ctx, blob, coeffs, batch=64):
+    """Blob::new's chunkset loop (blob.rs:252-264) on host buffers. Returns (n*16, F) uint8."""
+    blob = np.ascontiguousarray(np.frombuffer(blob, dtype=np.uint8) if isinstance(blob, (bytes, bytearray)) else blob)
+    n = -(-blob.size // CHUNKSET_BYTES)
+    coeffs = np.ascontiguousarray(coeffs, dtype=np.uint8)
+    if coeffs.size != n * N * K:
+        raise ValueError("coeffs must hold n*16*10 bytes")
+    out = np.empty((n * N, CODED_PIECE_BYTES), dtype=np.uint8)
+    vp = ctypes.c_void_p
+    check(lib().decds_blob_encode_host(ctx.handle, vp(blob.ctypes.data), blob.size, vp(coeffs.ctypes.data),
+                                       vp(out.ctypes.data), batch))
+    return out
+
+
+def blob_repair_host(ctx, coded, cand, blob_len, batch=64):
+    """RepairingBlob add_chunk/get_repaired_chunkset (blob.rs:373-473). Returns (blob, status)."""
+    coded = np.ascontiguousarray(coded, dtype=np.uint8)
+    n = coded.shape[0] // N
+    cand = np.ascontiguousarray(cand, dtype=np.uint8).reshape(n, N)
+    out = np.empty(blob_len, dtype=np.uint8)
+    status = np.empty(n, dtype=np.int32)
+    vp = ctypes.c_void_p
+    check(lib().decds_blob_repair_host(ctx.handle, vp(coded.ctypes.data), n, vp(cand.ctypes.data), blob_len,
+                                       vp(out.ctypes.data), vp(status.ctypes.data), batch))
+    return out, status
+
+
+__all__ = ["encode_batch", "repair_plan_batch", "decode_batch", "repair_batch", "fill_random_device",
+           "fill_random_host", "blob_encode_host", "blob_repair_host", "NO_CANDIDATE"]

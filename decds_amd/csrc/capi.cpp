@@ -1,0 +1,181 @@
+// capi.cpp — the extern "C" boundary declared in include/decds_rlnc.h: context management,
+// argument checking, status mapping onto DecdsError (decds-lib/src/errors.rs) and the batch
+// launchers. Every compute entry point runs the gfx950 kernels; there is no host fallback.
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "../../include/decds_rlnc.h"
+#include "capi_internal.h"
+#include "rlnc_kernels.h"
+#include "rlnc_layout.h"
+
+using namespace decds;
+
+static thread_local std::string g_last_error;
+
+int decds_set_error(int code, const char *fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_last_error = buf;
+    return code;
+}
+
+int decds_hip_error(hipError_t e, const char *what) {
+    return decds_set_error(DECDS_ERR_HIP, "%s: %s (%d)", what, hipGetErrorString(e), (int)e);
+}
+
+int decds_ctx_bind(const decds_ctx *ctx) {
+    if (!ctx) return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "null context");
+    hipError_t e = hipSetDevice(ctx->device);
+    return e == hipSuccess ? DECDS_OK : decds_hip_error(e, "hipSetDevice");
+}
+
+extern "C" {
+
+const char *decds_last_error(void) { return g_last_error.c_str(); }
+
+const char *decds_status_string(int s) {
+    switch (s) {
+        case DECDS_OK: return "ok";
+        case DECDS_ERR_INVALID_CHUNKSET_SIZE: return "invalid chunkset size";
+        case DECDS_ERR_INVALID_CHUNK_METADATA: return "invalid chunk metadata";
+        case DECDS_ERR_CHUNKSET_READY_TO_REPAIR: return "chunkset ready to repair";
+        case DECDS_ERR_CHUNK_DECODING_FAILED: return "chunk decoding failed";
+        case DECDS_ERR_CHUNKSET_NOT_YET_READY: return "chunkset not yet ready to repair";
+        case DECDS_ERR_CHUNKSET_REPAIRING_FAILED: return "chunkset repairing failed";
+        case DECDS_ERR_INVALID_SHARE_ID: return "invalid erasure coded share id";
+        case DECDS_ERR_EMPTY_DATA_FOR_BLOB: return "empty data for blob";
+        case DECDS_ERR_INVALID_CHUNKSET_ID: return "invalid chunkset id";
+        case DECDS_ERR_CHUNKSET_ALREADY_REPAIRED: return "chunkset already repaired";
+        case DECDS_ERR_HIP: return "HIP runtime error";
+        case DECDS_ERR_INVALID_ARGUMENT: return "invalid argument";
+        case DECDS_ERR_NO_DEVICE: return "no gfx950 device";
+        default: return "unknown status";
+    }
+}
+
+int decds_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+int decds_ctx_create(int device, decds_ctx **out) {
+    if (!out) return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "null out pointer");
+    *out = nullptr;
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess || n == 0)
+        return decds_set_error(DECDS_ERR_NO_DEVICE, "no HIP device visible (%s)",
+                               e == hipSuccess ? "count 0" : hipGetErrorString(e));
+    if (device < 0 || device >= n)
+        return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "device %d out of range [0,%d)", device, n);
+    hipDeviceProp_t prop;
+    if ((e = hipGetDeviceProperties(&prop, device)) != hipSuccess) return decds_hip_error(e, "hipGetDeviceProperties");
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return decds_set_error(DECDS_ERR_NO_DEVICE, "device %d is %s; these kernels are built for gfx950 only",
+                               device, prop.gcnArchName);
+    if ((e = hipSetDevice(device)) != hipSuccess) return decds_hip_error(e, "hipSetDevice");
+    if ((e = configure_kernels()) != hipSuccess) return decds_hip_error(e, "hipFuncSetAttribute");
+    decds_ctx *c = new decds_ctx;
+    c->device = device;
+    c->poly = POLY_DEFAULT;
+    c->marker = (uint8_t)MARKER_DEFAULT;
+    c->geom.num_cus = prop.multiProcessorCount;
+    c->geom.wgs_per_cu = 2;
+    *out = c;
+    return DECDS_OK;
+}
+
+int decds_ctx_destroy(decds_ctx *ctx) {
+    delete ctx;
+    return DECDS_OK;
+}
+
+int decds_ctx_set_field(decds_ctx *ctx, uint32_t poly, uint8_t marker) {
+    if (!ctx) return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "null context");
+    if (poly < 0x100 || poly > 0x1FF) return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "poly must be degree 8");
+    if (marker == 0) return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "marker must be non-zero");
+    ctx->poly = poly;
+    ctx->marker = marker;
+    return DECDS_OK;
+}
+
+int decds_ctx_get_field(const decds_ctx *ctx, uint32_t *poly, uint8_t *marker) {
+    if (!ctx) return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "null context");
+    if (poly) *poly = ctx->poly;
+    if (marker) *marker = ctx->marker;
+    return DECDS_OK;
+}
+
+static int check_pitch(size_t pitch) {
+    if (pitch < F)
+        return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "coded pitch %zu < %llu", pitch, (unsigned long long)F);
+    if ((N - 1) * (uint64_t)pitch + F >= (1ull << 32))
+        return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "coded pitch %zu too large", pitch);
+    return DECDS_OK;
+}
+
+static int check_n(size_t n) {
+    if (n == 0 || n > (1u << 24))
+        return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "chunkset count %zu outside [1, 2^24]", n);
+    return DECDS_OK;
+}
+
+int decds_encode_batch(decds_ctx *ctx, const uint8_t *src, size_t n, const uint8_t *coeffs,
+                       uint8_t *dst, size_t dst_pitch, void *stream) {
+    int s;
+    if ((s = decds_ctx_bind(ctx)) || (s = check_n(n)) || (s = check_pitch(dst_pitch))) return s;
+    if (!src || !coeffs || !dst) return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "null buffer");
+    hipError_t e = launch_encode(ctx->geom, src, n, coeffs, dst, dst_pitch, ctx->poly, ctx->marker,
+                                 (hipStream_t)stream);
+    return e == hipSuccess ? DECDS_OK : decds_hip_error(e, "rlnc_encode_kernel launch");
+}
+
+int decds_repair_plan_batch(decds_ctx *ctx, const uint8_t *coded, size_t coded_pitch, size_t n,
+                            const uint8_t *cand, uint8_t *plan, int8_t *verdicts, int32_t *status,
+                            void *stream) {
+    int s;
+    if ((s = decds_ctx_bind(ctx)) || (s = check_n(n)) || (s = check_pitch(coded_pitch))) return s;
+    if (!coded || !cand || !plan || !verdicts || !status)
+        return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "null buffer");
+    hipError_t e = launch_repair_plan(coded, coded_pitch, n, cand, plan, verdicts, status, ctx->poly,
+                                      (hipStream_t)stream);
+    return e == hipSuccess ? DECDS_OK : decds_hip_error(e, "rlnc_plan_kernel launch");
+}
+
+int decds_decode_batch(decds_ctx *ctx, const uint8_t *coded, size_t coded_pitch, size_t n,
+                       const uint8_t *plan, uint8_t *dst, int32_t *status, void *stream) {
+    int s;
+    if ((s = decds_ctx_bind(ctx)) || (s = check_n(n)) || (s = check_pitch(coded_pitch))) return s;
+    if (!coded || !plan || !dst || !status) return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "null buffer");
+    hipError_t e = launch_decode(ctx->geom, coded, coded_pitch, n, plan, dst, status, ctx->poly,
+                                 ctx->marker, (hipStream_t)stream);
+    return e == hipSuccess ? DECDS_OK : decds_hip_error(e, "rlnc_decode_kernel launch");
+}
+
+int decds_repair_batch(decds_ctx *ctx, const uint8_t *coded, size_t coded_pitch, size_t n,
+                       const uint8_t *cand, uint8_t *plan, int8_t *verdicts, uint8_t *dst,
+                       int32_t *status, void *stream) {
+    int s = decds_repair_plan_batch(ctx, coded, coded_pitch, n, cand, plan, verdicts, status, stream);
+    if (s) return s;
+    return decds_decode_batch(ctx, coded, coded_pitch, n, plan, dst, status, stream);
+}
+
+int decds_fill_random_device(decds_ctx *ctx, uint64_t seed, uint64_t byte_offset, uint8_t *dst,
+                             size_t nbytes, void *stream) {
+    int s;
+    if ((s = decds_ctx_bind(ctx))) return s;
+    if (!dst && nbytes) return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "null buffer");
+    hipError_t e = launch_fill_random(seed, byte_offset, dst, nbytes, (hipStream_t)stream);
+    return e == hipSuccess ? DECDS_OK : decds_hip_error(e, "fill_random launch");
+}
+
+}  // extern "C"

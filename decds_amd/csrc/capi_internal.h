@@ -1,0 +1,23 @@
+// capi_internal.h — state shared by the C-ABI translation units (not part of the public ABI).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "rlnc_kernels.h"
+
+struct decds_ctx {
+    int device;
+    uint32_t poly;     // GF(2^8) polynomial incl. x^8 (rlnc 0.4.0: 0x11D [recalled])
+    uint8_t marker;    // boundary marker appended by rlnc Encoder::new (0x81 [recalled])
+    decds::LaunchGeom geom;
+};
+
+int decds_set_error(int code, const char *fmt, ...);
+int decds_hip_error(hipError_t e, const char *what);
+int decds_ctx_bind(const decds_ctx *ctx);  // hipSetDevice(ctx->device)
+
+namespace decds {
+// host-side GF(2^8) helpers for the 10-byte coding vectors (control path, not the hot path)
+uint8_t host_gf_mul(uint8_t a, uint8_t b, uint32_t poly);
+uint8_t host_gf_inv(uint8_t a, uint32_t poly);
+}  // namespace decds

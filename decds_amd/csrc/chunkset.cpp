@@ -1,0 +1,348 @@
+// chunkset.cpp — host-side mirror of decds-lib's chunkset API (chunkset.rs) and of the blob-level
+// chunkset iteration (blob.rs) over the gfx950 batch kernels. Same names, argument meaning and
+// error behaviour as the reference; the Merkle/BLAKE3 commitment layer is out of scope.
+//
+//   decds_chunkset_new                 ChunkSet::new                    chunkset.rs:37-69
+//   decds_chunkset_get_chunk           ChunkSet::get_chunk              chunkset.rs:87-89
+//   decds_repairing_chunkset_*         RepairingChunkSet                chunkset.rs:107-208
+//   decds_blob_encode_host             Blob::new chunkset loop          blob.rs:244-264
+//   decds_blob_repair_host             RepairingBlob add/get_repaired   blob.rs:373-394, 451-473
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <mutex>
+#include <random>
+#include <vector>
+
+#include "../../include/decds_rlnc.h"
+#include "capi_internal.h"
+#include "rlnc_layout.h"
+
+using namespace decds;
+
+namespace {
+
+// RAII device buffer
+struct DevBuf {
+    uint8_t *p = nullptr;
+    hipError_t alloc(size_t n) { return hipMalloc(reinterpret_cast<void **>(&p), n); }
+    ~DevBuf() {
+        if (p) (void)hipFree(p);
+    }
+};
+
+std::mutex g_rng_mu;
+std::mt19937_64 &rng() {
+    // the reference draws coding vectors from rand::rng() (chunkset.rs:42): OS-seeded, not
+    // reproducible; the same holds here when the caller passes coeffs == NULL
+    static std::mt19937_64 g{std::random_device{}()};
+    return g;
+}
+
+
+}  // namespace
+
+struct decds_chunkset {
+    size_t id;
+    std::vector<uint8_t> coded;  // 16 x F, rlnc full coded pieces
+};
+
+struct decds_repairing_chunkset {
+    decds_ctx *ctx;
+    size_t id;
+    uint8_t basis[K * K];
+    uint8_t pivots[K];
+    uint32_t rank;
+    bool repaired;
+    std::vector<uint8_t> rows;  // accepted full coded pieces, acceptance order
+};
+
+extern "C" {
+
+int decds_chunkset_new(decds_ctx *ctx, size_t chunkset_id, const uint8_t *data, size_t len,
+                       const uint8_t *coeffs, decds_chunkset **out) {
+    if (!out) return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "null out pointer");
+    *out = nullptr;
+    if (len != CS) return decds_set_error(DECDS_ERR_INVALID_CHUNKSET_SIZE, "invalid chunkset size: %zuB, expected: %lluB",
+                                          len, (unsigned long long)CS);
+    if (!data) return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "null data");
+    int s = decds_ctx_bind(ctx);
+    if (s) return s;
+    uint8_t cv[N * K];
+    if (coeffs) {
+        std::memcpy(cv, coeffs, sizeof cv);
+    } else {
+        std::lock_guard<std::mutex> g(g_rng_mu);
+        for (auto &b : cv) b = (uint8_t)rng()();
+    }
+    DevBuf dsrc, dcv, ddst;
+    hipError_t e;
+    if ((e = dsrc.alloc(CS)) || (e = dcv.alloc(sizeof cv)) || (e = ddst.alloc(N * F))) return decds_hip_error(e, "hipMalloc");
+    if ((e = hipMemcpy(dsrc.p, data, CS, hipMemcpyHostToDevice)) || (e = hipMemcpy(dcv.p, cv, sizeof cv, hipMemcpyHostToDevice)))
+        return decds_hip_error(e, "hipMemcpy H2D");
+    if ((s = decds_encode_batch(ctx, dsrc.p, 1, dcv.p, ddst.p, F, nullptr))) return s;
+    auto *c = new decds_chunkset{chunkset_id, std::vector<uint8_t>(N * F)};
+    if ((e = hipMemcpy(c->coded.data(), ddst.p, N * F, hipMemcpyDeviceToHost))) {
+        delete c;
+        return decds_hip_error(e, "hipMemcpy D2H");
+    }
+    *out = c;
+    return DECDS_OK;
+}
+
+int decds_chunkset_get_chunk(const decds_chunkset *cs, size_t chunk_id, uint8_t *out, size_t out_len,
+                             size_t *global_chunk_id) {
+    if (!cs) return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "null chunkset");
+    if (chunk_id >= N) return decds_set_error(DECDS_ERR_INVALID_SHARE_ID, "invalid erasure coded share id: %zu (num_shares: %u)",
+                                              chunk_id, N);
+    if (out) {
+        if (out_len < F) return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "out buffer < %llu", (unsigned long long)F);
+        std::memcpy(out, cs->coded.data() + chunk_id * F, F);
+    }
+    if (global_chunk_id) *global_chunk_id = cs->id * N + chunk_id;  // chunkset.rs:47
+    return DECDS_OK;
+}
+
+size_t decds_chunkset_id(const decds_chunkset *cs) { return cs ? cs->id : 0; }
+void decds_chunkset_free(decds_chunkset *cs) { delete cs; }
+
+int decds_repairing_chunkset_new(decds_ctx *ctx, size_t chunkset_id, decds_repairing_chunkset **out) {
+    if (!ctx || !out) return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "null argument");
+    auto *r = new decds_repairing_chunkset;
+    r->ctx = ctx;
+    r->id = chunkset_id;
+    std::memset(r->basis, 0, sizeof r->basis);
+    std::memset(r->pivots, 0, sizeof r->pivots);
+    r->rank = 0;
+    r->repaired = false;
+    r->rows.reserve(K * F);
+    *out = r;
+    return DECDS_OK;
+}
+
+int decds_repairing_chunkset_add_chunk_unvalidated(decds_repairing_chunkset *r, size_t chunk_chunkset_id,
+                                                   const uint8_t *data, size_t len) {
+    if (!r) return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "null repairing chunkset");
+    if (r->repaired) return decds_set_error(DECDS_ERR_CHUNKSET_ALREADY_REPAIRED, "chunkset %zu is already repaired", r->id);
+    // chunkset.rs:174-176
+    if (chunk_chunkset_id != r->id)
+        return decds_set_error(DECDS_ERR_INVALID_CHUNK_METADATA, "invalid chunk for chunkset %zu", chunk_chunkset_id);
+    // chunkset.rs:177-179
+    if (r->rank == K) return decds_set_error(DECDS_ERR_CHUNKSET_READY_TO_REPAIR, "chunkset %zu is ready to repair", r->id);
+    // chunkset.rs:181-183 -> rlnc Decoder::decode: wrong length or a piece that does not raise the
+    // rank is an error mapped to ChunkDecodingFailed(chunkset_id, msg)
+    if (!data || len != F)
+        return decds_set_error(DECDS_ERR_CHUNK_DECODING_FAILED, "decoding chunk for chunkset %zu failed: invalid piece length %zu",
+                               chunk_chunkset_id, len);
+    if (!decds_rank_push(r->basis, r->pivots, &r->rank, data, r->ctx->poly))
+        return decds_set_error(DECDS_ERR_CHUNK_DECODING_FAILED, "decoding chunk for chunkset %zu failed: received piece is not useful",
+                               chunk_chunkset_id);
+    r->rows.insert(r->rows.end(), data, data + F);
+    return DECDS_OK;
+}
+
+int decds_repairing_chunkset_is_ready_to_repair(const decds_repairing_chunkset *r) {
+    return r && !r->repaired && r->rank == K;
+}
+
+int decds_repairing_chunkset_repair(decds_repairing_chunkset *r, uint8_t *out, size_t out_len) {
+    if (!r) return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "null repairing chunkset");
+    if (r->repaired) return decds_set_error(DECDS_ERR_CHUNKSET_ALREADY_REPAIRED, "chunkset %zu is already repaired", r->id);
+    // chunkset.rs:201,206
+    if (r->rank != K) return decds_set_error(DECDS_ERR_CHUNKSET_NOT_YET_READY, "chunkset %zu is not ready to repair", r->id);
+    if (!out || out_len < CS) return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "out buffer < %llu", (unsigned long long)CS);
+    int s = decds_ctx_bind(r->ctx);
+    if (s) return s;
+    DevBuf dcoded, dcand, dplan, dverd, dstat, ddst;
+    hipError_t e;
+    if ((e = dcoded.alloc(N * F)) || (e = dcand.alloc(N)) || (e = dplan.alloc(DECDS_REPAIR_PLAN_BYTES)) ||
+        (e = dverd.alloc(N)) || (e = dstat.alloc(sizeof(int32_t))) || (e = ddst.alloc(CS)))
+        return decds_hip_error(e, "hipMalloc");
+    uint8_t cand[N];
+    for (uint32_t i = 0; i < N; i++) cand[i] = i < K ? (uint8_t)i : (uint8_t)DECDS_NO_CANDIDATE;
+    if ((e = hipMemcpy(dcoded.p, r->rows.data(), K * F, hipMemcpyHostToDevice)) ||
+        (e = hipMemcpy(dcand.p, cand, N, hipMemcpyHostToDevice)))
+        return decds_hip_error(e, "hipMemcpy H2D");
+    if ((s = decds_repair_batch(r->ctx, dcoded.p, F, 1, dcand.p, dplan.p, reinterpret_cast<int8_t *>(dverd.p), ddst.p,
+                                reinterpret_cast<int32_t *>(dstat.p), nullptr)))
+        return s;
+    int32_t st = 0;
+    if ((e = hipMemcpy(&st, dstat.p, sizeof st, hipMemcpyDeviceToHost)) || (e = hipMemcpy(out, ddst.p, CS, hipMemcpyDeviceToHost)))
+        return decds_hip_error(e, "hipMemcpy D2H");
+    if (st != DECDS_OK)
+        return decds_set_error(DECDS_ERR_CHUNKSET_REPAIRING_FAILED, "chunkset %zu repairing failed: RLNC Decoding error: %s",
+                               r->id, st == DECDS_ERR_CHUNKSET_REPAIRING_FAILED ? "invalid decoded data format" : decds_status_string(st));
+    r->repaired = true;  // repair(self) consumes the decoder (chunkset.rs:200)
+    r->rows.clear();
+    r->rows.shrink_to_fit();
+    return DECDS_OK;
+}
+
+void decds_repairing_chunkset_free(decds_repairing_chunkset *r) { delete r; }
+
+// ------------------------------------------------------------------ blob-level batching ------
+// Two streams alternate over batches: while batch b runs its kernel, batch b+1's H2D and batch
+// b-1's D2H proceed on the copy engines. Caller buffers are page-locked with hipHostRegister for
+// the duration of the call so the copies DMA directly from/to them.
+namespace {
+struct HostReg {
+    void *p = nullptr;
+    bool ok = false;
+    HostReg(const void *ptr, size_t n) : p(const_cast<void *>(ptr)) {
+        ok = n && hipHostRegister(p, n, hipHostRegisterDefault) == hipSuccess;
+        if (!ok) (void)hipGetLastError();
+    }
+    ~HostReg() {
+        if (ok) (void)hipHostUnregister(p);
+    }
+};
+}  // namespace
+
+int decds_blob_encode_host(decds_ctx *ctx, const uint8_t *blob, size_t blob_len, const uint8_t *coeffs_host,
+                           uint8_t *coded_host, size_t batch) {
+    if (blob_len == 0) return decds_set_error(DECDS_ERR_EMPTY_DATA_FOR_BLOB, "empty data for blob");  // blob.rs:245-247
+    if (!blob || !coeffs_host || !coded_host) return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "null buffer");
+    int s = decds_ctx_bind(ctx);
+    if (s) return s;
+    const size_t n = (blob_len + CS - 1) / CS;  // blob.rs:252
+    if (batch == 0) batch = 64;
+    batch = std::min(batch, n);
+    HostReg rin(blob, blob_len), rout(coded_host, n * N * F), rcv(coeffs_host, n * N * K);
+    hipStream_t st[2];
+    DevBuf din[2], dout[2], dcv[2];
+    hipError_t e;
+    for (int i = 0; i < 2; i++) {
+        if ((e = hipStreamCreateWithFlags(&st[i], hipStreamNonBlocking))) return decds_hip_error(e, "hipStreamCreate");
+        if ((e = din[i].alloc(batch * CS)) || (e = dout[i].alloc(batch * N * F)) || (e = dcv[i].alloc(batch * N * K)))
+            return decds_hip_error(e, "hipMalloc");
+    }
+    int rc = DECDS_OK;
+    for (size_t b0 = 0, it = 0; b0 < n && rc == DECDS_OK; b0 += batch, it++) {
+        const int k = (int)(it & 1);
+        const size_t nb = std::min(batch, n - b0);
+        const size_t off = b0 * CS, have = std::min(blob_len - off, nb * CS);
+        if ((e = hipMemcpyAsync(din[k].p, blob + off, have, hipMemcpyHostToDevice, st[k]))) { rc = decds_hip_error(e, "H2D"); break; }
+        if (have < nb * CS && (e = hipMemsetAsync(din[k].p + have, 0, nb * CS - have, st[k]))) {  // blob.rs:254 zero pad
+            rc = decds_hip_error(e, "memset");
+            break;
+        }
+        if ((e = hipMemcpyAsync(dcv[k].p, coeffs_host + b0 * N * K, nb * N * K, hipMemcpyHostToDevice, st[k]))) {
+            rc = decds_hip_error(e, "H2D");
+            break;
+        }
+        if ((rc = decds_encode_batch(ctx, din[k].p, nb, dcv[k].p, dout[k].p, F, st[k]))) break;
+        if ((e = hipMemcpyAsync(coded_host + b0 * N * F, dout[k].p, nb * N * F, hipMemcpyDeviceToHost, st[k]))) {
+            rc = decds_hip_error(e, "D2H");
+            break;
+        }
+    }
+    for (int i = 0; i < 2; i++) {
+        e = hipStreamSynchronize(st[i]);
+        if (e && rc == DECDS_OK) rc = decds_hip_error(e, "hipStreamSynchronize");
+        (void)hipStreamDestroy(st[i]);
+    }
+    return rc;
+}
+
+int decds_blob_repair_host(decds_ctx *ctx, const uint8_t *coded_host, size_t n, const uint8_t *cand_host,
+                           size_t blob_len, uint8_t *out, int32_t *status_host, size_t batch) {
+    if (!coded_host || !cand_host || !out || !status_host || n == 0)
+        return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "null buffer or no chunksets");
+    if (blob_len > n * CS || blob_len <= (n - 1) * CS)
+        return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "blob length %zu inconsistent with %zu chunksets", blob_len, n);
+    int s = decds_ctx_bind(ctx);
+    if (s) return s;
+    if (batch == 0) batch = 64;
+    batch = std::min(batch, n);
+    // RepairingBlob::add_chunk over the arrival order (blob.rs:373-394): the rank test runs on the
+    // 10-byte coding vectors on the host, so only the 10 accepted rows of each chunkset cross PCIe
+    std::vector<uint8_t> sel(n * K, 0);
+    for (size_t c = 0; c < n; c++) {
+        uint8_t basis[K * K], piv[K];
+        uint32_t rank = 0;
+        for (uint32_t a = 0; a < N && rank < K; a++) {
+            const uint8_t row = cand_host[c * N + a];
+            if (row >= N) break;
+            if (decds_rank_push(basis, piv, &rank, coded_host + (c * N + row) * F, ctx->poly)) sel[c * K + rank - 1] = row;
+        }
+        status_host[c] = rank == K ? DECDS_OK : DECDS_ERR_CHUNKSET_NOT_YET_READY;
+    }
+    hipStream_t st[2];
+    DevBuf dcoded[2], dcand[2], dplan[2], dverd[2], dstat[2], ddst[2];
+    std::vector<std::vector<uint8_t>> cand_h(2, std::vector<uint8_t>(batch * N));
+    hipError_t e;
+    for (int i = 0; i < 2; i++) {
+        if ((e = hipStreamCreateWithFlags(&st[i], hipStreamNonBlocking))) return decds_hip_error(e, "hipStreamCreate");
+        if ((e = dcoded[i].alloc(batch * N * F)) || (e = dplan[i].alloc(batch * DECDS_REPAIR_PLAN_BYTES)) ||
+            (e = dverd[i].alloc(batch * N)) || (e = dstat[i].alloc(batch * sizeof(int32_t))) ||
+            (e = ddst[i].alloc(batch * CS)) || (e = dcand[i].alloc(batch * N)))
+            return decds_hip_error(e, "hipMalloc");
+    }
+    HostReg rout(out, blob_len);
+    int rc = DECDS_OK;
+    std::vector<std::vector<int32_t>> stat_h(2, std::vector<int32_t>(batch));
+    size_t pending_b0[2] = {(size_t)-1, (size_t)-1}, pending_nb[2] = {0, 0};
+    auto finish = [&](int k) -> int {
+        if (pending_b0[k] == (size_t)-1) return DECDS_OK;
+        hipError_t ee = hipStreamSynchronize(st[k]);
+        if (ee) return decds_hip_error(ee, "hipStreamSynchronize");
+        for (size_t c = 0; c < pending_nb[k]; c++) {
+            const size_t cs = pending_b0[k] + c;
+            int32_t &hs = status_host[cs];
+            if (hs == DECDS_OK && stat_h[k][c] != DECDS_OK) hs = DECDS_ERR_CHUNKSET_REPAIRING_FAILED;
+            if (hs != DECDS_OK) {  // no data for a chunkset that could not be repaired
+                const size_t off = cs * CS;
+                std::memset(out + off, 0, std::min(blob_len - off, (size_t)CS));
+            }
+        }
+        pending_b0[k] = (size_t)-1;
+        return DECDS_OK;
+    };
+    for (size_t b0 = 0, it = 0; b0 < n && rc == DECDS_OK; b0 += batch, it++) {
+        const int k = (int)(it & 1);
+        if ((rc = finish(k))) break;
+        const size_t nb = std::min(batch, n - b0);
+        for (size_t c = 0; c < nb; c++) {
+            const bool ready = status_host[b0 + c] == DECDS_OK;
+            for (uint32_t a = 0; a < N; a++) cand_h[k][c * N + a] = ready && a < K ? (uint8_t)a : (uint8_t)DECDS_NO_CANDIDATE;
+            if (!ready) continue;
+            for (uint32_t r = 0; r < K; r++) {
+                const uint8_t row = sel[(b0 + c) * K + r];
+                if ((e = hipMemcpyAsync(dcoded[k].p + (c * N + r) * F, coded_host + ((b0 + c) * N + row) * F, F,
+                                        hipMemcpyHostToDevice, st[k]))) {
+                    rc = decds_hip_error(e, "H2D");
+                    break;
+                }
+            }
+        }
+        if (rc) break;
+        if ((e = hipMemcpyAsync(dcand[k].p, cand_h[k].data(), nb * N, hipMemcpyHostToDevice, st[k]))) {
+            rc = decds_hip_error(e, "H2D");
+            break;
+        }
+        if ((rc = decds_repair_batch(ctx, dcoded[k].p, F, nb, dcand[k].p, dplan[k].p, reinterpret_cast<int8_t *>(dverd[k].p),
+                                     ddst[k].p, reinterpret_cast<int32_t *>(dstat[k].p), st[k])))
+            break;
+        if ((e = hipMemcpyAsync(stat_h[k].data(), dstat[k].p, nb * sizeof(int32_t), hipMemcpyDeviceToHost, st[k]))) {
+            rc = decds_hip_error(e, "D2H");
+            break;
+        }
+        // blob.rs:464: truncate the last chunkset to its real size
+        const size_t off = b0 * CS, keep = std::min(blob_len - off, nb * CS);
+        if ((e = hipMemcpyAsync(out + off, ddst[k].p, keep, hipMemcpyDeviceToHost, st[k]))) {
+            rc = decds_hip_error(e, "D2H");
+            break;
+        }
+        pending_b0[k] = b0;
+        pending_nb[k] = nb;
+    }
+    for (int i = 0; i < 2; i++) {
+        int r2 = finish(i);
+        if (r2 && rc == DECDS_OK) rc = r2;
+        (void)hipStreamDestroy(st[i]);
+    }
+    return rc;
+}
+
+}  // extern "C"

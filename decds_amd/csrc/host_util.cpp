@@ -1,0 +1,76 @@
+// host_util.cpp — host-side control-path helpers of the C-ABI: the rank step over 10-byte coding
+// vectors (rlnc Decoder's "piece useful?" test, chunkset.rs:181-183) and the seeded byte stream.
+// These never touch chunk payloads; the payload arithmetic runs only in rlnc_kernels.hip.
+#include <cstring>
+
+#include "../../include/decds_rlnc.h"
+#include "capi_internal.h"
+#include "rlnc_layout.h"
+
+namespace decds {
+
+uint8_t host_gf_mul(uint8_t a, uint8_t b, uint32_t poly) {
+    uint32_t acc = 0, x = a;
+    for (int i = 0; i < 8; i++) {
+        if (b & (1u << i)) acc ^= x;
+        x <<= 1;
+        if (x & 0x100u) x ^= poly;
+    }
+    return (uint8_t)acc;
+}
+
+uint8_t host_gf_inv(uint8_t a, uint32_t poly) {
+    uint8_t r = 1, b = a;
+    for (unsigned e = 254; e; e >>= 1) {
+        if (e & 1u) r = host_gf_mul(r, b, poly);
+        b = host_gf_mul(b, b, poly);
+    }
+    return a ? r : 0;
+}
+
+}  // namespace decds
+
+using namespace decds;
+
+extern "C" {
+
+int decds_rank_push(uint8_t *basis, uint8_t *pivots, uint32_t *rank, const uint8_t *coeff, uint32_t poly) {
+    if (!basis || !pivots || !rank || !coeff || *rank > K)
+        return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "bad rank_push arguments");
+    if (*rank == K) return 0;
+    uint8_t r[K];
+    std::memcpy(r, coeff, K);
+    for (uint32_t e = 0; e < *rank; e++) {
+        const uint8_t f = r[pivots[e]];
+        if (f)
+            for (uint32_t c = 0; c < K; c++) r[c] ^= host_gf_mul(f, basis[e * K + c], poly);
+    }
+    uint32_t p = K;
+    for (uint32_t c = 0; c < K; c++)
+        if (r[c]) { p = c; break; }
+    if (p == K) return 0;
+    const uint8_t inv = host_gf_inv(r[p], poly);
+    for (uint32_t c = 0; c < K; c++) r[c] = host_gf_mul(r[c], inv, poly);
+    for (uint32_t e = 0; e < *rank; e++) {
+        const uint8_t f = basis[e * K + p];
+        if (f)
+            for (uint32_t c = 0; c < K; c++) basis[e * K + c] ^= host_gf_mul(f, r[c], poly);
+    }
+    std::memcpy(basis + *rank * K, r, K);
+    pivots[*rank] = (uint8_t)p;
+    (*rank)++;
+    return 1;
+}
+
+void decds_fill_random_host(uint64_t seed, uint64_t off, uint8_t *dst, size_t nbytes) {
+    for (size_t i = 0; i < nbytes; i++) {
+        const uint64_t p = off + i;
+        uint64_t z = seed + ((p >> 3) + 1) * 0x9E3779B97F4A7C15ull;
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        z ^= z >> 31;
+        dst[i] = (uint8_t)(z >> (8 * (p & 7)));
+    }
+}
+
+}  // extern "C"

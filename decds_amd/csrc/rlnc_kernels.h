@@ -1,0 +1,27 @@
+// rlnc_kernels.h — host-side launchers for the gfx950 RLNC kernels (rlnc_kernels.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace decds {
+
+struct LaunchGeom {
+    int num_cus;          // CUs on the device (256 on MI355X)
+    int wgs_per_cu;       // resident workgroups per CU the streaming kernels are sized for
+};
+
+hipError_t launch_encode(const LaunchGeom &g, const uint8_t *src, size_t n, const uint8_t *coeffs,
+                         uint8_t *dst, size_t pitch, uint32_t poly, uint32_t marker,
+                         hipStream_t stream);
+hipError_t launch_repair_plan(const uint8_t *coded, size_t pitch, size_t n, const uint8_t *cand,
+                              uint8_t *plan, int8_t *verdicts, int32_t *status, uint32_t poly,
+                              hipStream_t stream);
+hipError_t launch_decode(const LaunchGeom &g, const uint8_t *coded, size_t pitch, size_t n,
+                         const uint8_t *plan, uint8_t *dst, int32_t *status, uint32_t poly,
+                         uint32_t marker, hipStream_t stream);
+hipError_t launch_fill_random(uint64_t seed, uint64_t byte_offset, uint8_t *dst, size_t nbytes,
+                              hipStream_t stream);
+hipError_t configure_kernels();  // raise the dynamic-LDS limit once per process
+
+}  // namespace decds

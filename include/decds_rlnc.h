@@ -1,0 +1,162 @@
+/*
+ * decds_rlnc.h — C-ABI of the MI355X-native RLNC chunkset codec (libdecds_rlnc.so, gfx950).
+ *
+ * Drop-in seam. decds-lib reaches its arithmetic through crate rlnc =0.4.0 from
+ * decds-lib/src/chunkset.rs; these entry points replace those call sites and the chunkset
+ * iteration around them in decds-lib/src/blob.rs. Each declaration names the reference interface
+ * it replaces (file:line under /root/reference). Plain pointers and sizes only: no Rust, torch or
+ * HIP types cross the boundary; a hipStream_t travels as `void *` (NULL = default stream).
+ *
+ * Memory ownership: the caller owns every buffer. The library borrows pointers for the duration
+ * of the call (device calls: until the enqueued work on `stream` completes) and never frees
+ * caller memory. A context owns only its device selection, field parameters and error text.
+ *
+ * Pointer kinds: *_batch functions take DEVICE pointers (hipMalloc'd or torch CUDA storage) and
+ * are asynchronous on `stream`; decds_chunkset_* / decds_repairing_chunkset_* / decds_blob_*_host
+ * take HOST pointers and are synchronous.
+ *
+ * Status codes map 1:1 onto decds-lib/src/errors.rs (DecdsError); negative codes are runtime
+ * failures that the Rust side surfaces as ChunksetRepairingFailed — there is never a silent CPU
+ * fallback: without a usable gfx950 device every compute entry point returns DECDS_ERR_NO_DEVICE.
+ */
+#ifndef DECDS_RLNC_H
+#define DECDS_RLNC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DECDS_NUM_ORIGINAL_CHUNKS 10u        /* chunkset.rs:19 */
+#define DECDS_NUM_ERASURE_CODED_CHUNKS 16u   /* chunkset.rs:21, consts.rs:5 */
+#define DECDS_CHUNKSET_BYTES 10485760ull     /* chunkset.rs:20 */
+#define DECDS_PIECE_BYTES 1048577ull         /* chunkset.rs:117 */
+#define DECDS_CODED_PIECE_BYTES 1048587ull   /* rlnc full coded piece: coding vector || payload */
+#define DECDS_REPAIR_PLAN_BYTES 128u
+#define DECDS_NO_CANDIDATE 0xFFu
+
+/* ---- status codes (decds-lib/src/errors.rs:3-48) ------------------------------------------- */
+#define DECDS_OK 0
+#define DECDS_ERR_INVALID_CHUNKSET_SIZE 1          /* InvalidChunksetSize(len)        errors.rs:36 */
+#define DECDS_ERR_INVALID_CHUNK_METADATA 2         /* InvalidChunkMetadata(id)        errors.rs:38 */
+#define DECDS_ERR_CHUNKSET_READY_TO_REPAIR 3       /* ChunksetReadyToRepair(id)       errors.rs:23 */
+#define DECDS_ERR_CHUNK_DECODING_FAILED 4          /* ChunkDecodingFailed(id, msg)    errors.rs:42 */
+#define DECDS_ERR_CHUNKSET_NOT_YET_READY 5         /* ChunksetNotYetReadyToRepair(id) errors.rs:25 */
+#define DECDS_ERR_CHUNKSET_REPAIRING_FAILED 6      /* ChunksetRepairingFailed(id,msg) errors.rs:29 */
+#define DECDS_ERR_INVALID_SHARE_ID 7               /* InvalidErasureCodedShareId(id)  errors.rs:32 */
+#define DECDS_ERR_EMPTY_DATA_FOR_BLOB 8            /* EmptyDataForBlob                errors.rs:6  */
+#define DECDS_ERR_INVALID_CHUNKSET_ID 9            /* InvalidChunksetId(id, n)        errors.rs:34 */
+#define DECDS_ERR_CHUNKSET_ALREADY_REPAIRED 10     /* ChunksetAlreadyRepaired(id)     errors.rs:27 */
+#define DECDS_ERR_HIP (-1)                         /* HIP runtime failure (text: decds_last_error) */
+#define DECDS_ERR_INVALID_ARGUMENT (-2)
+#define DECDS_ERR_NO_DEVICE (-3)
+
+typedef struct decds_ctx decds_ctx;
+
+/* ---- context ---------------------------------------------------------------------------- */
+int decds_ctx_create(int device, decds_ctx **out);
+int decds_ctx_destroy(decds_ctx *ctx);
+/* GF(2^8) polynomial (with the x^8 bit, e.g. 0x11D) and boundary marker used by rlnc 0.4.0.
+ * Defaults 0x11D / 0x81. Exposed so an identification run can re-pin them. */
+int decds_ctx_set_field(decds_ctx *ctx, uint32_t poly, uint8_t marker);
+int decds_ctx_get_field(const decds_ctx *ctx, uint32_t *poly, uint8_t *marker);
+const char *decds_status_string(int status);
+const char *decds_last_error(void); /* thread-local text of the last failure */
+int decds_device_count(void);
+
+/* ---- batch codec over device-resident chunksets (the hot path) ---------------------------- */
+/* Replaces ChunkSet::new's RLNC part for a batch of chunksets: Encoder::new(data, 10)
+ * (chunkset.rs:43) + 16 x Encoder::code(&mut rng) (chunkset.rs:45-52), as driven by the rayon
+ * loop in Blob::new (blob.rs:256-264).
+ *   src    : n x DECDS_CHUNKSET_BYTES (chunkset c at src + c*CS)
+ *   coeffs : n x 16 x 10 coding vectors (row j of chunkset c at coeffs + (c*16+j)*10)
+ *   dst    : n*16 coded rows; row r = c*16+j at dst + r*dst_pitch, laid out exactly like rlnc's
+ *            full coded piece: coding vector (10 B) || payload (L B). dst_pitch >= 1,048,587. */
+int decds_encode_batch(decds_ctx *ctx, const uint8_t *src, size_t n_chunksets,
+                       const uint8_t *coeffs, uint8_t *dst, size_t dst_pitch, void *stream);
+
+/* Replaces the incremental rank logic of RepairingChunkSet::add_chunk_unvalidated ->
+ * Decoder::decode (chunkset.rs:173-184) and is_ready_to_repair (chunkset.rs:187-189) for a batch:
+ *   cand     : n x 16 coded-row indices in arrival order, DECDS_NO_CANDIDATE-terminated
+ *   plan     : n x DECDS_REPAIR_PLAN_BYTES (accepted rows + inverse coding matrix)
+ *   verdicts : n x 16 per-candidate results: DECDS_OK (useful), DECDS_ERR_CHUNK_DECODING_FAILED
+ *              (did not raise the rank), DECDS_ERR_CHUNKSET_READY_TO_REPAIR (arrived after rank 10),
+ *              -1 (no candidate)
+ *   status   : n x int32: DECDS_OK (rank 10) or DECDS_ERR_CHUNKSET_NOT_YET_READY */
+int decds_repair_plan_batch(decds_ctx *ctx, const uint8_t *coded, size_t coded_pitch,
+                            size_t n_chunksets, const uint8_t *cand, uint8_t *plan,
+                            int8_t *verdicts, int32_t *status, void *stream);
+
+/* Replaces RepairingChunkSet::repair -> Decoder::get_decoded_data (chunkset.rs:200-208):
+ * dst = n x DECDS_CHUNKSET_BYTES; chunksets whose status is not DECDS_OK are skipped; a decoded
+ * tail that is not marker || zeros sets DECDS_ERR_CHUNKSET_REPAIRING_FAILED. */
+int decds_decode_batch(decds_ctx *ctx, const uint8_t *coded, size_t coded_pitch,
+                       size_t n_chunksets, const uint8_t *plan, uint8_t *dst, int32_t *status,
+                       void *stream);
+
+/* plan + decode in one call (the RepairingBlob::add_chunk loop + get_repaired_chunkset,
+ * blob.rs:373-394, 451-473, for candidates already resident on the device) */
+int decds_repair_batch(decds_ctx *ctx, const uint8_t *coded, size_t coded_pitch,
+                       size_t n_chunksets, const uint8_t *cand, uint8_t *plan, int8_t *verdicts,
+                       uint8_t *dst, int32_t *status, void *stream);
+
+/* Counter-based SplitMix64 byte stream (seeded, reproducible on host and device) for synthetic
+ * blobs and coding vectors; byte p = byte (p%8) of mix64(seed + (p/8 + 1) * 0x9E3779B97F4A7C15). */
+int decds_fill_random_device(decds_ctx *ctx, uint64_t seed, uint64_t byte_offset, uint8_t *dst,
+                             size_t nbytes, void *stream);
+void decds_fill_random_host(uint64_t seed, uint64_t byte_offset, uint8_t *dst, size_t nbytes);
+
+/* Host-side rank step over a 10-byte coding vector (rlnc Decoder's "is this piece useful").
+ * basis: 10x10 RREF rows, pivots: 10, *rank in/out. Returns 1 useful (basis updated), 0 not. */
+int decds_rank_push(uint8_t *basis, uint8_t *pivots, uint32_t *rank, const uint8_t *coeff,
+                    uint32_t poly);
+
+/* ---- chunkset-level mirror (decds-lib/src/chunkset.rs), host buffers ----------------------- */
+typedef struct decds_chunkset decds_chunkset;
+/* ChunkSet::new(chunkset_id, data) (chunkset.rs:37-69, minus the BLAKE3/Merkle commitment which
+ * is out of scope): len != 10 MiB -> DECDS_ERR_INVALID_CHUNKSET_SIZE. coeffs: 16 x 10 coding
+ * vectors, or NULL to draw them from the library's RNG (the reference draws from rand::rng(),
+ * chunkset.rs:42). */
+int decds_chunkset_new(decds_ctx *ctx, size_t chunkset_id, const uint8_t *data, size_t len,
+                       const uint8_t *coeffs, decds_chunkset **out);
+/* ChunkSet::get_chunk (chunkset.rs:87-89): copies the 1,048,587-byte erasure-coded data of local
+ * chunk `chunk_id`; *global_chunk_id = chunkset_id*16 + chunk_id (chunkset.rs:47) */
+int decds_chunkset_get_chunk(const decds_chunkset *cs, size_t chunk_id, uint8_t *out,
+                             size_t out_len, size_t *global_chunk_id);
+size_t decds_chunkset_id(const decds_chunkset *cs);
+void decds_chunkset_free(decds_chunkset *cs);
+
+typedef struct decds_repairing_chunkset decds_repairing_chunkset;
+/* RepairingChunkSet::new (chunkset.rs:129-135) */
+int decds_repairing_chunkset_new(decds_ctx *ctx, size_t chunkset_id, decds_repairing_chunkset **out);
+/* RepairingChunkSet::add_chunk_unvalidated (chunkset.rs:173-184): chunk_chunkset_id is the
+ * chunk's get_chunkset_id(); data/len its get_erasure_coded_data() */
+int decds_repairing_chunkset_add_chunk_unvalidated(decds_repairing_chunkset *rcs,
+                                                   size_t chunk_chunkset_id, const uint8_t *data,
+                                                   size_t len);
+/* RepairingChunkSet::is_ready_to_repair (chunkset.rs:187-189) */
+int decds_repairing_chunkset_is_ready_to_repair(const decds_repairing_chunkset *rcs);
+/* RepairingChunkSet::repair (chunkset.rs:200-208): out receives 10 MiB. Consumes the decoder
+ * state on success (a second call returns DECDS_ERR_CHUNKSET_ALREADY_REPAIRED). */
+int decds_repairing_chunkset_repair(decds_repairing_chunkset *rcs, uint8_t *out, size_t out_len);
+void decds_repairing_chunkset_free(decds_repairing_chunkset *rcs);
+
+/* ---- blob-level batching (decds-lib/src/blob.rs), host buffers, pinned-staged -------------- */
+/* Blob::new's chunkset loop (blob.rs:252-264): zero-pads blob to n = ceil(len/CS) chunksets and
+ * encodes them in device batches of `batch` chunksets with H2D / kernel / D2H overlapped on two
+ * streams. coded_host: n*16 rows of 1,048,587 bytes. coeffs_host: n x 16 x 10. */
+int decds_blob_encode_host(decds_ctx *ctx, const uint8_t *blob, size_t blob_len,
+                           const uint8_t *coeffs_host, uint8_t *coded_host, size_t batch);
+/* RepairingBlob add_chunk/get_repaired_chunkset over all chunksets (blob.rs:373-394, 451-473):
+ * coded_host: n*16 rows; cand_host: n x 16 arrival order; out: blob_len bytes (last chunkset
+ * truncated as blob.rs:464); status_host: n per-chunkset status. */
+int decds_blob_repair_host(decds_ctx *ctx, const uint8_t *coded_host, size_t n_chunksets,
+                           const uint8_t *cand_host, size_t blob_len, uint8_t *out,
+                           int32_t *status_host, size_t batch);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DECDS_RLNC_H */

@@ -1,0 +1,92 @@
+"""CPU-side tests of the C-ABI library: it loads, exports every symbol include/decds_rlnc.h
+declares, and its host-only control-path helpers agree with the oracle. No compute call is made
+here (no GPU in this container); without a device every compute entry point must refuse loudly."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+import decds_amd
+from decds_amd import _capi
+import oracle as o
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_functions():
+    src = open(os.path.join(ROOT, "include", "decds_rlnc.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(decds_[a-z_0-9]+)\s*\(", src)))
+
+
+def test_library_exports_every_declared_symbol():
+    lib = _capi.lib()
+    declared = header_functions()
+    assert len(declared) >= 20
+    missing = [f for f in declared if not hasattr(lib, f)]
+    assert not missing, missing
+    assert sorted(_capi.EXPORTED) == declared
+
+
+def test_status_codes_match_header():
+    src = open(os.path.join(ROOT, "include", "decds_rlnc.h")).read()
+    codes = {int(v.strip("()")) for v in re.findall(r"#define DECDS_(?:OK|ERR_[A-Z_]+)\s+(\(?-?\d+\)?)", src)}
+    assert codes == set(_capi.STATUS_NAMES)
+    lib = _capi.lib()
+    for code in _capi.STATUS_NAMES:
+        assert lib.decds_status_string(code) not in (None, b"unknown status")
+
+
+def test_no_device_refuses_loudly():
+    lib = _capi.lib()
+    if lib.decds_device_count() > 0:
+        pytest.skip("a device is visible")
+    h = ctypes.c_void_p()
+    assert lib.decds_ctx_create(0, ctypes.byref(h)) == _capi.STATUS["NoDevice"]
+    assert b"device" in lib.decds_last_error()
+    with pytest.raises(decds_amd.DecdsError) as e:
+        decds_amd.Context(0)
+    assert e.value.kind == "NoDevice"
+    # a null context is refused by every batch entry point
+    assert lib.decds_encode_batch(None, None, 1, None, None, _capi.CODED_PIECE_BYTES, None) == _capi.STATUS["InvalidArgument"]
+
+
+def test_chunkset_new_invalid_size_before_device():
+    # chunkset.rs:285-298 — the size check precedes any device work
+    lib = _capi.lib()
+    h = ctypes.c_void_p()
+    for n in (_capi.CHUNKSET_BYTES - 1, _capi.CHUNKSET_BYTES + 1):
+        buf = bytes(n)
+        assert lib.decds_chunkset_new(None, 0, buf, n, None, ctypes.byref(h)) == _capi.STATUS["InvalidChunksetSize"]
+        assert str(n) in lib.decds_last_error().decode()
+
+
+def test_fill_random_host_matches_oracle():
+    for seed, off, n in [(1, 0, 100), (0xDEC05001, 12345, 4097), (7, 3, 17)]:
+        a = decds_amd.codec.fill_random_host(seed, n, off) if hasattr(decds_amd, "codec") else None
+        from decds_amd import codec
+        a = codec.fill_random_host(seed, n, off)
+        assert np.array_equal(a, o.fill_random(seed, n, off))
+
+
+def test_rank_push_matches_oracle():
+    lib = _capi.lib()
+    rng = np.random.default_rng(11)
+    for _ in range(300):
+        b1, p1, r1 = np.zeros(100, np.uint8), np.zeros(10, np.uint8), ctypes.c_uint32(0)
+        b2, p2, r2 = np.zeros(100, np.uint8), np.zeros(10, np.uint8), ctypes.c_size_t(0)
+        for _ in range(13):
+            cv = (rng.integers(0, 4, 10) * rng.integers(0, 2, 10)).astype(np.uint8)
+            u1 = lib.decds_rank_push(b1.ctypes.data, p1.ctypes.data, ctypes.byref(r1), cv.ctypes.data, 0x11D)
+            u2 = o.lib().orc_rank_push(o._p(b2), o._p(p2), ctypes.byref(r2), o._p(cv), 10, 0x11D)
+            assert u1 == u2
+        assert r1.value == r2.value
+        assert np.array_equal(b1[: 10 * r1.value], b2[: 10 * r2.value])
+
+
+def test_layout_constants():
+    assert _capi.PIECE_BYTES == o.L == 1048577
+    assert _capi.CODED_PIECE_BYTES == o.F
+    assert _capi.CHUNKSET_BYTES == o.CS

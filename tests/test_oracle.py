@@ -1,0 +1,169 @@
+"""CPU tests of the restatement (oracle/) against the committed known-answer vectors and the
+reference's own round-trip properties (chunkset.rs:257-283, 438-480; tests.rs:4-57)."""
+import hashlib
+
+import numpy as np
+import pytest
+
+import oracle as o
+
+
+def sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def test_field_known_answers(kat):
+    t = o.mul_table()
+    assert sha(t) == kat["mul_table_sha256"]
+    assert sha(o.mul_table(0x11B)) == kat["mul_table_sha256_poly_0x11b"]
+    for a, b, p in kat["products"]:
+        assert t[a, b] == p
+    for a, inv in kat["inverses"]:
+        assert o.gf_inv(a) == inv and t[a, inv] == 1
+
+
+def test_field_axioms():
+    t = o.mul_table().astype(np.int64)
+    rng = np.random.default_rng(1)
+    a, b, c = rng.integers(0, 256, (3, 2000))
+    assert np.array_equal(t[a, b], t[b, a])
+    assert np.array_equal(t[t[a, b], c], t[a, t[b, c]])
+    assert np.array_equal(t[a, b ^ c], t[a, b] ^ t[a, c])          # distributive over XOR (add)
+    assert all(t[x, o.gf_inv(x)] == 1 for x in range(1, 256))
+    assert len(set(t[2 ** 0 if False else 2, :].tolist())) == 256  # 2 is a unit; the map is a bijection
+
+
+def test_small_encode_vectors(kat):
+    for v in kat["small_encode"]:
+        data = np.frombuffer(bytes.fromhex(v["data"]), dtype=np.uint8)
+        cv = np.frombuffer(bytes.fromhex(v["coding_vector"]), dtype=np.uint8)
+        piece = o.code_with_coding_vector(data, cv)
+        assert piece.tobytes().hex() == v["full_coded_piece"]
+        # structure: cv prefix, then L = ceil((len+1)/k) payload bytes (chunkset.rs:117)
+        assert piece[:10].tobytes() == cv.tobytes()
+        assert piece.size == 10 + (data.size + 1 + 9) // 10
+
+
+def test_encoder_padding_layout():
+    data = o.fill_random(5, o.CS)
+    padded = o.encoder_pad(data)
+    assert padded.size == o.K * o.L
+    assert np.array_equal(padded[: o.CS], data)
+    assert padded[o.CS] == o.MARKER and not padded[o.CS + 1:].any()
+
+
+def test_cfg1_full_chunkset_golden(kat):
+    c = kat["cfg1"]
+    data = o.fill_random(c["data_seed"], o.CS)
+    assert sha(data) == c["data_sha256"]
+    coeffs = np.frombuffer(bytes.fromhex(c["coeffs"]), dtype=np.uint8)
+    coded = o.chunkset_encode(data, coeffs, nthreads=8)
+    assert [sha(coded[j]) for j in range(16)] == c["coded_sha256"]
+
+
+def test_chunkset_encode_invalid_size():
+    # chunkset.rs:285-298: InvalidChunksetSize for CS-1 and CS+1
+    for n in (o.CS - 1, o.CS + 1):
+        with pytest.raises(ValueError):
+            o.chunkset_encode(np.zeros(n, np.uint8), np.ones(160, np.uint8))
+
+
+def _roundtrip(data_len, seed, k=10):
+    data = o.fill_random(seed, data_len)
+    L = o.piece_len(data_len, k)
+    rng = np.random.default_rng(seed)
+    dec = o.Decoder(L, k)
+    pieces = 0
+    while not dec.is_already_decoded():
+        cv = rng.integers(0, 256, k, dtype=np.uint8)
+        st = dec.decode(o.code_with_coding_vector(data, cv, k))
+        assert st in (o.OK, o.NOT_USEFUL)
+        pieces += 1
+    st, out = dec.get_decoded_data()
+    assert st == o.OK
+    assert np.array_equal(out, data)
+    assert dec.decode(o.code_with_coding_vector(data, np.ones(k, np.uint8), k)) == o.RECEIVED_ALL
+
+
+@pytest.mark.parametrize("n", [1, 9, 10, 11, 1000, 4097])
+def test_decoder_roundtrip_small(n):
+    _roundtrip(n, 100 + n)
+
+
+def test_decoder_not_useful_and_state_unchanged():
+    data = o.fill_random(9, 500)
+    dec = o.Decoder(o.piece_len(500), 10)
+    cv1 = np.arange(1, 11, dtype=np.uint8)
+    assert dec.decode(o.code_with_coding_vector(data, cv1)) == o.OK
+    # a multiple of an accepted vector does not raise the rank (rlnc: piece not useful)
+    cv2 = np.array([o.gf_mul(7, int(x)) for x in cv1], dtype=np.uint8)
+    assert dec.decode(o.code_with_coding_vector(data, cv2)) == o.NOT_USEFUL
+    assert dec.rank() == 1
+    assert dec.decode(np.zeros(10 + o.piece_len(500), np.uint8)) == o.NOT_USEFUL
+    assert dec.decode(np.zeros(5, np.uint8)) == o.INVALID_LEN
+    assert dec.get_decoded_data()[0] == o.NOT_ALL
+
+
+def test_full_chunkset_roundtrip_shuffled():
+    # chunkset.rs:257-283 with a fixed seed: encode, shuffle the 16 chunks, add until ready
+    data = o.fill_random(77, o.CS)
+    coeffs = o.fill_random(78, 160)
+    coded = o.chunkset_encode(data, coeffs, nthreads=8)
+    order = np.random.default_rng(3).permutation(16)
+    dec = o.Decoder()
+    for j in order:
+        if dec.is_already_decoded():
+            break
+        assert dec.decode(coded[j]) in (o.OK, o.NOT_USEFUL)
+    st, out = dec.get_decoded_data()
+    assert st == o.OK and out.size == o.CS and np.array_equal(out, data)
+
+
+def test_rank_push_matches_decoder():
+    rng = np.random.default_rng(5)
+    for trial in range(200):
+        basis = np.zeros(100, np.uint8)
+        piv = np.zeros(10, np.uint8)
+        import ctypes
+        rank = ctypes.c_size_t(0)
+        dec = o.Decoder(3, 10)
+        for _ in range(14):
+            # low-entropy vectors so dependent ones actually occur
+            cv = (rng.integers(0, 3, 10) * rng.integers(0, 2, 10)).astype(np.uint8)
+            useful = o.lib().orc_rank_push(o._p(basis), o._p(piv), ctypes.byref(rank), o._p(cv), 10, o.POLY)
+            if dec.is_already_decoded():
+                assert not useful
+                continue
+            st = dec.decode(np.concatenate([cv, np.zeros(3, np.uint8)]))
+            assert (st == o.OK) == bool(useful)
+        assert rank.value == dec.rank()
+
+
+def test_matrix_inverse():
+    rng = np.random.default_rng(6)
+    t = o.mul_table()
+    for _ in range(20):
+        m = rng.integers(0, 256, (10, 10), dtype=np.uint8)
+        inv = o.matrix_inverse(m)
+        if inv is None:
+            continue
+        prod = np.zeros((10, 10), np.uint8)
+        for i in range(10):
+            for j in range(10):
+                acc = 0
+                for kk in range(10):
+                    acc ^= int(t[m[i, kk], inv[kk, j]])
+                prod[i, j] = acc
+        assert np.array_equal(prod, np.eye(10, dtype=np.uint8))
+
+
+def test_blob_encode_repair_partial_last_chunkset():
+    # blob.rs:767-837: a blob of 2.5 chunksets; the last one is zero-padded and truncated on repair
+    blob_len = 2 * o.CS + o.CS // 2
+    blob = o.fill_random(21, blob_len)
+    n = 3
+    coeffs = o.fill_random(22, n * 160)
+    coded = o.blob_encode(blob, coeffs, nthreads=4)
+    cand = np.array([np.random.default_rng(c).permutation(16) for c in range(n)], np.uint8)
+    out, status = o.blob_repair(coded, cand, blob_len, nthreads=4)
+    assert (status == 0).all() and np.array_equal(out, blob)
