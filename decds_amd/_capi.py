@@ -9,6 +9,8 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libdecds_rlnc.so")
+# tuning runs load an alternative build of the same sources (tools/kbench.py); default: in-tree lib
+LIB_PATH = os.environ.get("DECDS_LIB", LIB_PATH)
 
 K = 10                  # ChunkSet::NUM_ORIGINAL_CHUNKS (chunkset.rs:19)
 N = 16                  # ChunkSet::NUM_ERASURE_CODED_CHUNKS (chunkset.rs:21)

@@ -24,16 +24,19 @@ def _stale():
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force=False, verbose=True):
-    if not force and not _stale():
+def build(force=False, verbose=True, defines=(), out=None):
+    """Compile the library; `defines` (e.g. ["DECDS_WG=512"]) and `out` build a tuning variant."""
+    lib = out or LIB
+    if not force and out is None and not _stale():
         return LIB
-    objdir = os.path.join(HERE, "..", "build", "obj")
+    tag = "_".join(d.replace("=", "") for d in defines) or "default"
+    objdir = os.path.join(HERE, "..", "build", "obj", tag)
     os.makedirs(objdir, exist_ok=True)
     objs, procs = [], []
     for s in SOURCES:
         o = os.path.join(objdir, s + ".o")
         objs.append(o)
-        cmd = [HIPCC] + FLAGS + ["-c", os.path.join(CSRC, s), "-o", o]
+        cmd = [HIPCC] + FLAGS + ["-D" + d for d in defines] + ["-c", os.path.join(CSRC, s), "-o", o]
         if s.endswith(".cpp"):
             cmd[1:1] = ["-x", "hip"]
         procs.append((cmd, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)))
@@ -43,14 +46,23 @@ def build(force=False, verbose=True):
             raise RuntimeError("hipcc failed: %s\n%s" % (" ".join(cmd), out.decode()))
         if verbose and out.strip():
             sys.stderr.write(out.decode())
-    tmp = LIB + ".tmp"
+    tmp = lib + ".tmp"
     cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", tmp] + objs
     r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
     if r.returncode != 0:
         raise RuntimeError("link failed: %s\n%s" % (" ".join(cmd), r.stdout.decode()))
-    os.replace(tmp, LIB)
-    return LIB
+    os.replace(tmp, lib)
+    return lib
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv))
+    # python -m decds_amd.build [--force] [--variant NAME -DX=1 ...]
+    args = sys.argv[1:]
+    defs = [a[2:] for a in args if a.startswith("-D")]
+    if "--variant" in args:
+        name = args[args.index("--variant") + 1]
+        vdir = os.path.join(HERE, "..", "build", "variants")
+        os.makedirs(vdir, exist_ok=True)
+        print(build(force=True, defines=defs, out=os.path.join(vdir, "lib_%s.so" % name)))
+    else:
+        print(build(force="--force" in args, defines=defs))

@@ -89,7 +89,6 @@ int decds_ctx_create(int device, decds_ctx **out) {
     c->poly = POLY_DEFAULT;
     c->marker = (uint8_t)MARKER_DEFAULT;
     c->geom.num_cus = prop.multiProcessorCount;
-    c->geom.wgs_per_cu = 2;
     *out = c;
     return DECDS_OK;
 }

@@ -8,7 +8,6 @@ namespace decds {
 
 struct LaunchGeom {
     int num_cus;          // CUs on the device (256 on MI355X)
-    int wgs_per_cu;       // resident workgroups per CU the streaming kernels are sized for
 };
 
 hipError_t launch_encode(const LaunchGeom &g, const uint8_t *src, size_t n, const uint8_t *coeffs,

@@ -10,24 +10,50 @@
 // is replicated 16x across the 64 LDS banks and lane l reads copy (l & 15): the 16 lanes of every
 // ds_read_b128 lane group {0-3,12-15,20-27}, {4-11,16-19,28-31}, ... hit 16 distinct 4-bank slots,
 // so the data-dependent lookups are bank-conflict-free by construction (MI355X_MICROARCH.md §LDS).
-// Per 16-column lane block: 10 unaligned 16-B loads, 320 conflict-free ds_read_b128, XOR3
+// Per 16-column lane block: 10 unaligned 16-B loads, 320 conflict-free ds_read_b128, v_bitop3 XOR3
 // accumulation into a 16x16 byte block (columns x outputs), a v_perm byte transpose, 16 (or 10)
-// 16-B stores. No MFMA: this is byte-wise finite-field work, bounded by HBM and LDS bandwidth.
+// 16-B stores. No MFMA: this is byte-wise finite-field work, bounded by HBM (and LDS) bandwidth.
 #include <hip/hip_runtime.h>
+
+#include <utility>
 
 #include "rlnc_kernels.h"
 #include "rlnc_layout.h"
 
 namespace decds {
 
+// ---- geometry ---------------------------------------------------------------------------------
 constexpr uint32_t WG = 256;                                  // 4 waves
+constexpr uint32_t WGS_PER_CU = 2;                            // 2 x 80 KiB LDS = the CU's 160 KiB
+constexpr uint32_t WAVES_PER_SIMD = WGS_PER_CU * WG / 256;    // 2 -> up to 256 VGPRs per lane
 constexpr uint32_t TILE_BLOCKS = WG;                          // one 16-col block per lane per tile
 constexpr uint32_t TILES_PER_CS = (MAIN_BLOCKS + TILE_BLOCKS - 1) / TILE_BLOCKS;  // 256
 constexpr uint32_t ROW_BYTES = 256;                           // 16 replicas x 16 B
 constexpr uint32_t TABLE_BYTES = 16 * ROW_BYTES;              // 16 nibble rows
-constexpr uint32_t LDS_BYTES = K * 2 * TABLE_BYTES;           // 80 KiB -> 2 workgroups per CU
+constexpr uint32_t LDS_BYTES = K * 2 * TABLE_BYTES;           // 80 KiB
 static_assert(TILES_PER_CS == 256, "tile geometry");
 
+// ---- per-kernel tuning (measured in one process by tools/abbench.py; DESIGN.md "Tuning log") --
+//   ASM  : hand-pipelined LDS lookups (8-16 ds_read_b128 in flight per wave) instead of hipcc's
+//          schedule (which waits after every column: ~4 in flight)
+//   ROLL : the next block's input i is loaded as soon as this block has consumed input i
+//   LAUX / SAUX : cache-policy word of the streaming loads / stores (buffer instructions; gfx950:
+//          sc0 = 1, nt = 2, sc1 = 16); -1 = plain global_load / global_store
+template <bool ASM_, bool ROLL_, int LAUX_, int SAUX_>
+struct Tune {
+    static constexpr bool ASM = ASM_, ROLL = ROLL_;
+    static constexpr int LAUX = LAUX_, SAUX = SAUX_;
+};
+#ifndef DECDS_ENC_TUNE
+#define DECDS_ENC_TUNE false, false, -1, -1
+#endif
+#ifndef DECDS_DEC_TUNE
+#define DECDS_DEC_TUNE true, true, -1, 2
+#endif
+using EncTune = Tune<DECDS_ENC_TUNE>;
+using DecTune = Tune<DECDS_DEC_TUNE>;
+
+// ---- GF(2^8) ----------------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t gf_mul(uint32_t a, uint32_t b, uint32_t poly) {
     uint32_t acc = 0;
 #pragma unroll
@@ -39,11 +65,20 @@ __device__ __forceinline__ uint32_t gf_mul(uint32_t a, uint32_t b, uint32_t poly
     return acc & 0xFFu;
 }
 
+__device__ __forceinline__ uint32_t gf_inv(uint32_t a, uint32_t poly) {  // a^254
+    uint32_t r = 1;
+#pragma unroll
+    for (int e = 0; e < 8; e++) {
+        if (254u & (1u << e)) r = gf_mul(r, a, poly);
+        a = gf_mul(a, a, poly);
+    }
+    return r;
+}
+
 // Build the 2*NIN replicated nibble tables for a NOUT x NIN coefficient matrix M (row-major in
 // global memory, row stride ldm). Caller brackets with __syncthreads().
 template <int NIN, int NOUT>
-__device__ __forceinline__ void build_tables(uint8_t *lds, const uint8_t *M, uint32_t ldm,
-                                             uint32_t poly) {
+__device__ __forceinline__ void build_tables(uint8_t *lds, const uint8_t *M, uint32_t ldm, uint32_t poly) {
     for (uint32_t r = threadIdx.x; r < NIN * 32; r += WG) {
         const uint32_t i = r >> 5, h = (r >> 4) & 1u, n = r & 15u;
         const uint32_t m = n << (4 * h);
@@ -63,16 +98,48 @@ __device__ __forceinline__ uint32_t tbl_mul(const uint8_t *lds, uint32_t i, uint
            lds[(i * 2 + 1) * TABLE_BYTES + (x >> 4) * ROW_BYTES + j];
 }
 
-__device__ __forceinline__ uint4 ld16(const uint8_t *p) {
-    // piece rows start at i*L (L = 2^20 + 1) / r*pitch + 10: byte-misaligned by design of the
-    // rlnc layout; gfx9 global loads accept unaligned addresses (unaligned access mode).
-    return *reinterpret_cast<const uint4 *>(p);
+// ---- streaming row access ---------------------------------------------------------------------
+// Rows are addressed as a wave-uniform 64-bit base plus a 32-bit row offset (a chunkset's rows
+// lie within 16 * pitch < 4 GiB of its base): global_load/store's SGPR-base + VGPR-offset form,
+// or a buffer descriptor on that base when a cache-policy word is requested. Piece rows start at
+// i*L (L = 2^20 + 1) and coded payloads at r*pitch + 10, so most rows are byte-misaligned by the
+// rlnc layout itself; gfx9 vector memory accepts unaligned 16-B accesses.
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+template <int AUX>
+__device__ __forceinline__ uint4 ldrow(const uint8_t *base, uint32_t off) {
+    u32x4 v;
+    if constexpr (AUX >= 0) {
+        const __amdgpu_buffer_rsrc_t r =
+            __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(base), 0, 0xFFFFFFFFu, 0x00020000);
+        v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, AUX);
+    } else {
+        v = *reinterpret_cast<const u32x4 *>(base + off);
+    }
+    return make_uint4(v.x, v.y, v.z, v.w);
 }
-__device__ __forceinline__ void st16(uint8_t *p, uint4 v) { *reinterpret_cast<uint4 *>(p) = v; }
+
+template <int AUX>
+__device__ __forceinline__ void strow(uint8_t *base, uint32_t off, uint4 v) {
+    const u32x4 w = {v.x, v.y, v.z, v.w};
+    if constexpr (AUX >= 0) {
+        const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, 0, 0xFFFFFFFFu, 0x00020000);
+        __builtin_amdgcn_raw_buffer_store_b128(w, r, off, 0, AUX);
+    } else {
+        *reinterpret_cast<u32x4 *>(base + off) = w;
+    }
+}
+
+template <class T, int NIN>
+__device__ __forceinline__ void load_block(uint4 (&x)[NIN], const uint8_t *ibase, const uint32_t (&ioff)[NIN],
+                                           uint32_t col0) {
+#pragma unroll
+    for (int i = 0; i < NIN; i++) x[i] = ldrow<T::LAUX>(ibase, ioff[i] + col0);
+}
 
 // 4x4 byte transpose: out[b].byte[p] = in[p].byte[b]
-__device__ __forceinline__ void transpose4x4(uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3,
-                                             uint32_t &b0, uint32_t &b1, uint32_t &b2, uint32_t &b3) {
+__device__ __forceinline__ void transpose4x4(uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3, uint32_t &b0,
+                                             uint32_t &b1, uint32_t &b2, uint32_t &b3) {
     const uint32_t u0 = __builtin_amdgcn_perm(a1, a0, 0x05010400u);  // a0.0 a1.0 a0.1 a1.1
     const uint32_t u1 = __builtin_amdgcn_perm(a1, a0, 0x07030602u);  // a0.2 a1.2 a0.3 a1.3
     const uint32_t u2 = __builtin_amdgcn_perm(a3, a2, 0x05010400u);  // a2.0 a3.0 a2.1 a3.1
@@ -83,53 +150,126 @@ __device__ __forceinline__ void transpose4x4(uint32_t a0, uint32_t a1, uint32_t 
     b3 = __builtin_amdgcn_perm(u3, u1, 0x07060302u);
 }
 
-// One 16-column lane block: out_j[col0 .. col0+16) = sum_i M[j][i] * in_i[col0 .. col0+16)
-// Rows are addressed as a wave-uniform 64-bit base plus a 32-bit row offset (every row of a
-// chunkset lies within 16 * pitch < 4 GiB of its base), which maps onto global_load/store's
-// SGPR-base + VGPR-offset form and keeps the per-row state to one SGPR.
-template <int NIN, int NOUT>
-__device__ __forceinline__ void combine_block(const uint8_t *lds, uint32_t laneoff,
-                                              const uint8_t *ibase, const uint32_t (&ioff)[NIN],
-                                              uint8_t *obase, const uint32_t (&ooff)[NOUT],
-                                              uint32_t col0) {
-    uint4 x[NIN];
-#pragma unroll
-    for (int i = 0; i < NIN; i++) x[i] = ld16(ibase + (ioff[i] + col0));
+__device__ __forceinline__ uint32_t word_of(const uint4 &v, int w) {
+    return w == 0 ? v.x : w == 1 ? v.y : w == 2 ? v.z : v.w;
+}
 
+__device__ __forceinline__ void xor3_into(uint32_t (&acc)[4], const u32x4 &a, const u32x4 &b) {
+    // v_bitop3_b32 (gfx950): acc ^ a ^ b in one VALU op (truth table 0x96)
+    acc[0] = __builtin_amdgcn_bitop3_b32(acc[0], a.x, b.x, 0x96);
+    acc[1] = __builtin_amdgcn_bitop3_b32(acc[1], a.y, b.y, 0x96);
+    acc[2] = __builtin_amdgcn_bitop3_b32(acc[2], a.z, b.z, 0x96);
+    acc[3] = __builtin_amdgcn_bitop3_b32(acc[3], a.w, b.w, 0x96);
+}
+
+// ---- lookups, compiler-scheduled ----------------------------------------------------------------
+// address = nibble * 256 + laneoff, assembled by one v_perm: byte0 <- laneoff, byte1 <- the nibble
+// of byte p, bytes 2,3 <- 0 (tables >= 64 KiB take byte 2 from laneoff_hi = laneoff | 0x10000)
+template <class T, int NIN>
+__device__ __forceinline__ void lookups_compiled(uint32_t (&acc)[16][4], uint4 (&x)[NIN], const uint8_t *lds,
+                                                 uint32_t laneoff, const uint8_t *ibase, const uint32_t (&ioff)[NIN],
+                                                 uint32_t ncol0) {
+#pragma unroll
+    for (int i = 0; i < NIN; i++) {
+        const uint8_t *tlo = lds + (i * 2 + 0) * TABLE_BYTES;
+        const uint8_t *thi = lds + (i * 2 + 1) * TABLE_BYTES;
+#pragma unroll
+        for (int w = 0; w < 4; w++) {
+            const uint32_t xw = word_of(x[i], w);
+            const uint32_t lo = xw & 0x0F0F0F0Fu, hi = (xw >> 4) & 0x0F0F0F0Fu;
+#pragma unroll
+            for (int p = 0; p < 4; p++) {
+                const uint32_t sel = 0x0C0C0000u | ((4u + p) << 8);
+                const uint32_t alo = __builtin_amdgcn_perm(lo, laneoff, sel);
+                const uint32_t ahi = __builtin_amdgcn_perm(hi, laneoff, sel);
+                const u32x4 a = *reinterpret_cast<const u32x4 *>(tlo + alo);
+                const u32x4 b = *reinterpret_cast<const u32x4 *>(thi + ahi);
+                xor3_into(acc[4 * w + p], a, b);
+            }
+        }
+        if constexpr (T::ROLL) x[i] = ldrow<T::LAUX>(ibase, ioff[i] + ncol0);
+    }
+}
+
+// ---- lookups, hand-pipelined --------------------------------------------------------------------
+// The lookups of one lane block are cut into 4*NIN groups (input i, dword w: 4 columns x {lo, hi}
+// = 8 reads); group g+1 is issued before group g is consumed, so 8-16 reads are in flight per wave.
+// Reads are inline asm with immediate table offsets and explicit counted waits
+// (cdna_hip_programming.md §5.7 form (ii)): nothing else in this region issues LGKM operations and
+// one wave's LDS reads return in order.
+template <int G>
+__device__ __forceinline__ void lds_issue(u32x4 (&r)[8], uint32_t xw, uint32_t laneoff, uint32_t laneoff_hi) {
+    constexpr int i = G >> 2;
+    constexpr uint32_t tlo = (2 * i) * TABLE_BYTES, thi = (2 * i + 1) * TABLE_BYTES;
+    constexpr bool flo = tlo >= 65536, fhi = thi >= 65536;  // ds offsets are 16-bit
+    const uint32_t lo = xw & 0x0F0F0F0Fu;
+    const uint32_t hi = (xw >> 4) & 0x0F0F0F0Fu;
+#pragma unroll
+    for (int p = 0; p < 4; p++) {
+        const uint32_t sel_lo = (flo ? 0x0C020000u : 0x0C0C0000u) | ((4u + p) << 8);
+        const uint32_t sel_hi = (fhi ? 0x0C020000u : 0x0C0C0000u) | ((4u + p) << 8);
+        const uint32_t alo = __builtin_amdgcn_perm(lo, flo ? laneoff_hi : laneoff, sel_lo);
+        const uint32_t ahi = __builtin_amdgcn_perm(hi, fhi ? laneoff_hi : laneoff, sel_hi);
+        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r[2 * p]) : "v"(alo), "i"(flo ? tlo - 65536 : tlo));
+        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r[2 * p + 1]) : "v"(ahi), "i"(fhi ? thi - 65536 : thi));
+    }
+}
+
+template <int CNT>
+__device__ __forceinline__ void lds_wait(u32x4 (&r)[8]) {
+    asm volatile("s_waitcnt lgkmcnt(%8)"
+                 : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]), "+v"(r[4]), "+v"(r[5]), "+v"(r[6]), "+v"(r[7])
+                 : "i"(CNT)
+                 : "memory");
+}
+
+template <class T, int NIN, int G>
+__device__ __forceinline__ void lds_step(uint32_t (&acc)[16][4], u32x4 (&ra)[8], u32x4 (&rb)[8], uint4 (&x)[NIN],
+                                         uint32_t laneoff, uint32_t laneoff_hi, const uint8_t *ibase,
+                                         const uint32_t (&ioff)[NIN], uint32_t ncol0) {
+    constexpr int NG = 4 * NIN;
+    u32x4(&cur)[8] = (G & 1) ? rb : ra;  // group G's results
+    u32x4(&nxt)[8] = (G & 1) ? ra : rb;
+    if constexpr (G + 1 < NG) {
+        lds_issue<G + 1>(nxt, word_of(x[(G + 1) >> 2], (G + 1) & 3), laneoff, laneoff_hi);
+        // input (G+1)>>2 is fully issued: its register may now take the next block's bytes
+        if constexpr (T::ROLL && ((G + 1) & 3) == 3) x[(G + 1) >> 2] = ldrow<T::LAUX>(ibase, ioff[(G + 1) >> 2] + ncol0);
+        lds_wait<8>(cur);
+    } else {
+        lds_wait<0>(cur);
+    }
+    constexpr int w = G & 3;
+#pragma unroll
+    for (int p = 0; p < 4; p++) xor3_into(acc[4 * w + p], cur[2 * p], cur[2 * p + 1]);
+}
+
+template <class T, int NIN, int... Gs>
+__device__ __forceinline__ void lookups_asm(std::integer_sequence<int, Gs...>, uint32_t (&acc)[16][4], uint4 (&x)[NIN],
+                                            uint32_t laneoff, const uint8_t *ibase, const uint32_t (&ioff)[NIN],
+                                            uint32_t ncol0) {
+    const uint32_t laneoff_hi = laneoff | 0x10000u;
+    u32x4 ra[8], rb[8];
+    lds_issue<0>(ra, x[0].x, laneoff, laneoff_hi);
+    (lds_step<T, NIN, Gs>(acc, ra, rb, x, laneoff, laneoff_hi, ibase, ioff, ncol0), ...);
+}
+
+// One 16-column lane block: out_j[col0 .. col0+16) = sum_i M[j][i] * in_i[col0 .. col0+16).
+// x holds this block's inputs on entry; with T::ROLL it holds the inputs at column ncol0 on exit
+// (each loaded as soon as this block has consumed that input, before this block's stores: gfx9's
+// vmcnt counts stores too, so a load issued behind the stores would also wait for them).
+template <class T, int NIN, int NOUT>
+__device__ __forceinline__ void combine_block(const uint8_t *lds, uint32_t laneoff, uint4 (&x)[NIN], uint8_t *obase,
+                                              const uint32_t (&ooff)[NOUT], uint32_t col0, const uint8_t *ibase,
+                                              const uint32_t (&ioff)[NIN], uint32_t ncol0) {
     uint32_t acc[16][4];  // acc[column][output group]: byte b = output 4*group + b
 #pragma unroll
     for (int c = 0; c < 16; c++)
 #pragma unroll
         for (int q = 0; q < 4; q++) acc[c][q] = 0;
-
-#pragma unroll
-    for (int i = 0; i < NIN; i++) {
-        const uint32_t xs[4] = {x[i].x, x[i].y, x[i].z, x[i].w};
-        const uint8_t *tlo = lds + (i * 2 + 0) * TABLE_BYTES;
-        const uint8_t *thi = lds + (i * 2 + 1) * TABLE_BYTES;
-#pragma unroll
-        for (int w = 0; w < 4; w++) {
-            const uint32_t lo = xs[w] & 0x0F0F0F0Fu;
-            const uint32_t hi = (xs[w] >> 4) & 0x0F0F0F0Fu;
-#pragma unroll
-            for (int p = 0; p < 4; p++) {
-                // address = nibble * 256 + laneoff, assembled by one v_perm:
-                // byte0 <- laneoff, byte1 <- nibble of byte p, bytes 2,3 <- 0
-                const uint32_t sel = 0x0C0C0000u | ((4u + p) << 8);
-                const uint32_t alo = __builtin_amdgcn_perm(lo, laneoff, sel);
-                const uint32_t ahi = __builtin_amdgcn_perm(hi, laneoff, sel);
-                const uint4 a = *reinterpret_cast<const uint4 *>(tlo + alo);
-                const uint4 b = *reinterpret_cast<const uint4 *>(thi + ahi);
-                const int c = 4 * w + p;
-                // v_bitop3_b32 (gfx950): acc ^ a ^ b in one VALU op (truth table 0x96)
-                acc[c][0] = __builtin_amdgcn_bitop3_b32(acc[c][0], a.x, b.x, 0x96);
-                acc[c][1] = __builtin_amdgcn_bitop3_b32(acc[c][1], a.y, b.y, 0x96);
-                acc[c][2] = __builtin_amdgcn_bitop3_b32(acc[c][2], a.z, b.z, 0x96);
-                acc[c][3] = __builtin_amdgcn_bitop3_b32(acc[c][3], a.w, b.w, 0x96);
-            }
-        }
-    }
-
+    if constexpr (T::ASM)
+        lookups_asm<T, NIN>(std::make_integer_sequence<int, 4 * NIN>{}, acc, x, laneoff, ibase, ioff, ncol0);
+    else
+        lookups_compiled<T, NIN>(acc, x, lds, laneoff, ibase, ioff, ncol0);
     // columns x outputs -> outputs x columns
 #pragma unroll
     for (int q = 0; q < 4; q++) {
@@ -137,30 +277,46 @@ __device__ __forceinline__ void combine_block(const uint8_t *lds, uint32_t laneo
         uint32_t o[4][4];  // o[b][w]: output 4q+b, columns 4w..4w+3
 #pragma unroll
         for (int w = 0; w < 4; w++)
-            transpose4x4(acc[4 * w + 0][q], acc[4 * w + 1][q], acc[4 * w + 2][q], acc[4 * w + 3][q],
-                         o[0][w], o[1][w], o[2][w], o[3][w]);
+            transpose4x4(acc[4 * w + 0][q], acc[4 * w + 1][q], acc[4 * w + 2][q], acc[4 * w + 3][q], o[0][w], o[1][w],
+                         o[2][w], o[3][w]);
 #pragma unroll
         for (int b = 0; b < 4; b++) {
             const int j = 4 * q + b;
-            if (j < NOUT) st16(obase + (ooff[j] + col0), make_uint4(o[b][0], o[b][1], o[b][2], o[b][3]));
+            if (j < NOUT) strow<T::SAUX>(obase, ooff[j] + col0, make_uint4(o[b][0], o[b][1], o[b][2], o[b][3]));
         }
     }
 }
 
-// Work split: the n*256 tiles (256 lane blocks = 4096 columns each) are divided into equal
-// contiguous ranges, one per resident workgroup; a workgroup rebuilds its LDS tables only when
-// its range crosses into the next chunkset (at most ceil(range/256)+1 times).
+// ---- work split ---------------------------------------------------------------------------------
+// The n*256 tiles (256 lane blocks = 4096 columns each) are divided into equal contiguous ranges,
+// one per resident workgroup; a workgroup rebuilds its LDS tables only when its range crosses into
+// the next chunkset. (Interleaving workgroups over neighbouring tiles measured slower:
+// DESIGN.md "Tuning log".)
 __device__ __forceinline__ void tile_range(size_t n, uint32_t &t0, uint32_t &t1) {
     const uint64_t total = (uint64_t)n * TILES_PER_CS;
     t0 = (uint32_t)(total * blockIdx.x / gridDim.x);
     t1 = (uint32_t)(total * (blockIdx.x + 1) / gridDim.x);
 }
 
-__global__ __launch_bounds__(WG, 2) void rlnc_encode_kernel(const uint8_t *__restrict__ src,
-                                                            size_t n,
-                                                            const uint8_t *__restrict__ coeffs,
-                                                            uint8_t *__restrict__ dst, size_t pitch,
-                                                            uint32_t poly, uint32_t marker) {
+// One tile of a workgroup's range for this lane: inputs were prefetched by the previous tile when
+// `have` (ROLL), else they are loaded now.
+template <class T, int NIN, int NOUT>
+__device__ __forceinline__ void stream_tile(const uint8_t *lds, uint32_t laneoff, uint32_t t, uint32_t t1, uint32_t cs,
+                                            uint32_t tile, const uint8_t *ibase, const uint32_t (&ioff)[NIN],
+                                            uint8_t *obase, const uint32_t (&ooff)[NOUT], uint4 (&x)[NIN], bool &have) {
+    const uint32_t block = tile * TILE_BLOCKS + threadIdx.x;
+    const bool active = block < MAIN_BLOCKS;
+    if (!(T::ROLL && have) && active) load_block<T, NIN>(x, ibase, ioff, block * COLS_PER_LANE);
+    have = t + 1 < t1 && (t + 1) / TILES_PER_CS == cs;
+    const uint32_t nblock = block + TILE_BLOCKS;
+    // branch-free prefetch: lanes with no next block re-load their own block (an L2 hit)
+    const uint32_t ncol0 = (have && nblock < MAIN_BLOCKS ? nblock : block) * COLS_PER_LANE;
+    if (active) combine_block<T, NIN, NOUT>(lds, laneoff, x, obase, ooff, block * COLS_PER_LANE, ibase, ioff, ncol0);
+}
+
+__global__ __launch_bounds__(WG, WAVES_PER_SIMD) __attribute__((amdgpu_waves_per_eu(WAVES_PER_SIMD, WAVES_PER_SIMD)))
+void rlnc_encode_kernel(const uint8_t *__restrict__ src, size_t n, const uint8_t *__restrict__ coeffs,
+                        uint8_t *__restrict__ dst, size_t pitch, uint32_t poly, uint32_t marker) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     uint32_t t0, t1;
     tile_range(n, t0, t1);
@@ -174,10 +330,13 @@ __global__ __launch_bounds__(WG, 2) void rlnc_encode_kernel(const uint8_t *__res
     uint32_t cur = 0xFFFFFFFFu;
     const uint8_t *ibase = src;
     uint8_t *obase = dst;
+    uint4 x[K];
+    bool have = false;
     for (uint32_t t = t0; t < t1; t++) {
         const uint32_t cs = t / TILES_PER_CS, tile = t % TILES_PER_CS;
         if (cs != cur) {
             cur = cs;
+            have = false;
             const uint8_t *M = coeffs + (size_t)cs * N * K;
             __syncthreads();
             build_tables<K, N>(lds, M, K, poly);
@@ -201,17 +360,13 @@ __global__ __launch_bounds__(WG, 2) void rlnc_encode_kernel(const uint8_t *__res
                 }
             }
         }
-        const uint32_t block = tile * TILE_BLOCKS + threadIdx.x;
-        if (block < MAIN_BLOCKS) combine_block<K, N>(lds, laneoff, ibase, ioff, obase, ooff, block * COLS_PER_LANE);
+        stream_tile<EncTune, K, N>(lds, laneoff, t, t1, cs, tile, ibase, ioff, obase, ooff, x, have);
     }
 }
 
-__global__ __launch_bounds__(WG, 2) void rlnc_decode_kernel(const uint8_t *__restrict__ coded,
-                                                            size_t pitch, size_t n,
-                                                            const RepairPlan *__restrict__ plan,
-                                                            uint8_t *__restrict__ dst,
-                                                            int32_t *__restrict__ status,
-                                                            uint32_t poly, uint32_t marker) {
+__global__ __launch_bounds__(WG, WAVES_PER_SIMD) __attribute__((amdgpu_waves_per_eu(WAVES_PER_SIMD, WAVES_PER_SIMD)))
+void rlnc_decode_kernel(const uint8_t *__restrict__ coded, size_t pitch, size_t n, const RepairPlan *__restrict__ plan,
+                        uint8_t *__restrict__ dst, int32_t *__restrict__ status, uint32_t poly, uint32_t marker) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     uint32_t t0, t1;
     tile_range(n, t0, t1);
@@ -226,10 +381,13 @@ __global__ __launch_bounds__(WG, 2) void rlnc_decode_kernel(const uint8_t *__res
     bool ready = false;
     const uint8_t *ibase = coded;
     uint8_t *obase = dst;
+    uint4 x[K];
+    bool have = false;
     for (uint32_t t = t0; t < t1; t++) {
         const uint32_t cs = t / TILES_PER_CS, tile = t % TILES_PER_CS;
         if (cs != cur) {
             cur = cs;
+            have = false;
             const RepairPlan *pl = plan + cs;
             // plan words are wave-uniform: keep them in SGPRs
             const uint32_t *pw = reinterpret_cast<const uint32_t *>(pl);
@@ -268,105 +426,120 @@ __global__ __launch_bounds__(WG, 2) void rlnc_decode_kernel(const uint8_t *__res
             }
         }
         if (!ready) continue;
-        const uint32_t block = tile * TILE_BLOCKS + threadIdx.x;
-        if (block < MAIN_BLOCKS) combine_block<K, K>(lds, laneoff, ibase, ioff, obase, ooff, block * COLS_PER_LANE);
+        stream_tile<DecTune, K, K>(lds, laneoff, t, t1, cs, tile, ibase, ioff, obase, ooff, x, have);
     }
 }
 
-// One thread per chunkset: replay rlnc's incremental rank test over the candidates' 10-byte
-// coding vectors in arrival order (chunkset.rs:173-184 semantics), then invert the accepted ones.
-__global__ void rlnc_plan_kernel(const uint8_t *__restrict__ coded, size_t pitch, size_t n,
-                                 const uint8_t *__restrict__ cand, RepairPlan *__restrict__ plan,
-                                 int8_t *__restrict__ verdicts, int32_t *__restrict__ status,
-                                 uint32_t poly) {
-    const size_t cs = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (cs >= n) return;
-    uint8_t basis[K][K], raw[K][K], piv[K], sel[K];
+// One wave per chunkset. Replays rlnc's incremental rank test over the candidates' 10-byte coding
+// vectors in arrival order (chunkset.rs:173-184: a piece is accepted iff it raises the rank;
+// after rank 10 every further piece is "ready to repair"), then inverts the accepted vectors by
+// Gauss-Jordan. Lane c holds column c (c < 10 for the rank test, c < 20 for the augmented inverse);
+// pivots and multipliers are wave-uniform values read with v_readlane.
+__global__ __launch_bounds__(64) void rlnc_plan_kernel(const uint8_t *__restrict__ coded, size_t pitch, size_t n,
+                                                       const uint8_t *__restrict__ cand,
+                                                       RepairPlan *__restrict__ plan,
+                                                       int8_t *__restrict__ verdicts,
+                                                       int32_t *__restrict__ status, uint32_t poly) {
+    const size_t cs = blockIdx.x;
+    const uint32_t lane = threadIdx.x;
+    const bool col = lane < K;
+    uint32_t basis[K], raw[K];
+    uint32_t piv[K], sel[K];
+#pragma unroll
+    for (int e = 0; e < (int)K; e++) basis[e] = raw[e] = piv[e] = sel[e] = 0;
     uint32_t rank = 0;
     bool ended = false;
+    int32_t my_verdict = -1;  // lane a < 16 keeps candidate a's verdict
     for (uint32_t a = 0; a < N; a++) {
         const uint32_t r = cand[cs * N + a];
-        int8_t v;
+        int32_t v;
         if (ended || r >= N) {
             ended = true;
             v = -1;
         } else if (rank == K) {
             v = 3;  // DECDS_ERR_CHUNKSET_READY_TO_REPAIR
         } else {
-            const uint8_t *cv = coded + (cs * N + r) * pitch;
-            uint8_t row[K];
-            for (uint32_t c = 0; c < K; c++) row[c] = cv[c];
-            for (uint32_t e = 0; e < rank; e++) {
-                const uint32_t f = row[piv[e]];
-                if (f)
-                    for (uint32_t c = 0; c < K; c++) row[c] ^= (uint8_t)gf_mul(f, basis[e][c], poly);
+            const uint32_t cv = col ? coded[(cs * N + r) * pitch + lane] : 0u;
+            uint32_t row = cv;
+#pragma unroll
+            for (int e = 0; e < (int)K; e++) {
+                if (e < (int)rank) {
+                    const uint32_t f = __builtin_amdgcn_readlane(row, piv[e]);
+                    if (f) row ^= gf_mul(f, basis[e], poly);
+                }
             }
-            uint32_t p = K;
-            for (uint32_t c = 0; c < K; c++)
-                if (row[c]) { p = c; break; }
-            if (p == K) {
+            const uint64_t nz = __ballot(col && row != 0);
+            if (!nz) {
                 v = 4;  // DECDS_ERR_CHUNK_DECODING_FAILED: piece not useful
             } else {
-                // normalise (a^-1 = a^254) and clear column p from the basis (RREF)
-                uint32_t inv = 1, b = row[p];
-                for (uint32_t e = 254; e; e >>= 1) {
-                    if (e & 1u) inv = gf_mul(inv, b, poly);
-                    b = gf_mul(b, b, poly);
+                const uint32_t p = __builtin_ctzll(nz);
+                const uint32_t inv = gf_inv(__builtin_amdgcn_readlane(row, p), poly);
+                row = gf_mul(row, inv, poly);
+#pragma unroll
+                for (int e = 0; e < (int)K; e++) {
+                    if (e < (int)rank) {
+                        const uint32_t f = __builtin_amdgcn_readlane(basis[e], p);
+                        if (f) basis[e] ^= gf_mul(f, row, poly);
+                    }
                 }
-                for (uint32_t c = 0; c < K; c++) row[c] = (uint8_t)gf_mul(row[c], inv, poly);
-                for (uint32_t e = 0; e < rank; e++) {
-                    const uint32_t f = basis[e][p];
-                    if (f)
-                        for (uint32_t c = 0; c < K; c++) basis[e][c] ^= (uint8_t)gf_mul(f, row[c], poly);
+#pragma unroll
+                for (int e = 0; e < (int)K; e++) {
+                    if (e == (int)rank) {
+                        basis[e] = row;
+                        raw[e] = cv;
+                        piv[e] = p;
+                        sel[e] = r;
+                    }
                 }
-                for (uint32_t c = 0; c < K; c++) {
-                    basis[rank][c] = row[c];
-                    raw[rank][c] = cv[c];
-                }
-                piv[rank] = (uint8_t)p;
-                sel[rank] = (uint8_t)r;
                 rank++;
                 v = 0;
             }
         }
-        verdicts[cs * N + a] = v;
+        if (lane == a) my_verdict = v;
     }
+    if (lane < N) verdicts[cs * N + lane] = (int8_t)my_verdict;
     RepairPlan *pl = plan + cs;
-    pl->rank = (uint8_t)rank;
+    if (lane == 0) pl->rank = (uint8_t)rank;
     if (rank < K) {
-        status[cs] = 5;  // DECDS_ERR_CHUNKSET_NOT_YET_READY
+        if (lane == 0) status[cs] = 5;  // DECDS_ERR_CHUNKSET_NOT_YET_READY
         return;
     }
-    // Gauss-Jordan inverse of raw (rows = accepted coding vectors): piece = raw^-1 * y
-    uint8_t a[K][2 * K];
-    for (uint32_t i = 0; i < K; i++)
-        for (uint32_t j = 0; j < 2 * K; j++) a[i][j] = j < K ? raw[i][j] : (uint8_t)(j - K == i);
-    for (uint32_t c = 0; c < K; c++) {
-        uint32_t p = c;
-        while (!a[p][c]) p++;  // full rank: a pivot exists
-        if (p != c)
-            for (uint32_t j = 0; j < 2 * K; j++) {
-                const uint8_t t = a[p][j];
-                a[p][j] = a[c][j];
-                a[c][j] = t;
+    // augmented [raw | I]: lane c < 10 holds column c of raw, lane 10 + c column c of I
+    uint32_t m[K];
+#pragma unroll
+    for (int i = 0; i < (int)K; i++) m[i] = lane < K ? raw[i] : (lane - K == (uint32_t)i ? 1u : 0u);
+#pragma unroll
+    for (int c = 0; c < (int)K; c++) {
+        uint32_t p = K;
+#pragma unroll
+        for (int i = (int)K - 1; i >= c; i--)
+            if (__builtin_amdgcn_readlane(m[i], c)) p = i;  // full rank: a pivot exists
+#pragma unroll
+        for (int i = c + 1; i < (int)K; i++)
+            if ((uint32_t)i == p) {
+                const uint32_t t = m[c];
+                m[c] = m[i];
+                m[i] = t;
             }
-        uint32_t inv = 1, b = a[c][c];
-        for (uint32_t e = 254; e; e >>= 1) {
-            if (e & 1u) inv = gf_mul(inv, b, poly);
-            b = gf_mul(b, b, poly);
-        }
-        for (uint32_t j = 0; j < 2 * K; j++) a[c][j] = (uint8_t)gf_mul(a[c][j], inv, poly);
-        for (uint32_t i = 0; i < K; i++) {
-            const uint32_t f = a[i][c];
-            if (i == c || !f) continue;
-            for (uint32_t j = 0; j < 2 * K; j++) a[i][j] ^= (uint8_t)gf_mul(f, a[c][j], poly);
+        const uint32_t inv = gf_inv(__builtin_amdgcn_readlane(m[c], c), poly);
+        m[c] = gf_mul(m[c], inv, poly);
+#pragma unroll
+        for (int i = 0; i < (int)K; i++) {
+            if (i == c) continue;
+            const uint32_t f = __builtin_amdgcn_readlane(m[i], c);
+            if (f) m[i] ^= gf_mul(f, m[c], poly);
         }
     }
-    for (uint32_t i = 0; i < K; i++) {
-        pl->sel[i] = sel[i];
-        for (uint32_t j = 0; j < K; j++) pl->inv[i * K + j] = a[i][K + j];
+    // inverse = right half: pl->inv[i][j] = m[i] of lane 10 + j
+    if (lane >= K && lane < 2 * K) {
+#pragma unroll
+        for (int i = 0; i < (int)K; i++) pl->inv[i * K + (lane - K)] = (uint8_t)m[i];
     }
-    status[cs] = 0;
+    if (lane == 0) {
+#pragma unroll
+        for (int e = 0; e < (int)K; e++) pl->sel[e] = (uint8_t)sel[e];
+        status[cs] = 0;
+    }
 }
 
 __device__ __forceinline__ uint64_t splitmix_word(uint64_t seed, uint64_t w) {
@@ -394,7 +567,7 @@ __global__ void fill_random_bytes_kernel(uint64_t seed, uint64_t off, uint8_t *d
 // ------------------------------------------------------------------------------ launchers ----
 static uint32_t stream_grid(const LaunchGeom &g, size_t n) {
     const uint64_t tiles = (uint64_t)n * TILES_PER_CS;
-    uint64_t grid = (uint64_t)g.num_cus * g.wgs_per_cu;
+    uint64_t grid = (uint64_t)g.num_cus * WGS_PER_CU;
     return (uint32_t)(tiles < grid ? tiles : grid);
 }
 
@@ -419,8 +592,7 @@ hipError_t launch_repair_plan(const uint8_t *coded, size_t pitch, size_t n, cons
                               uint8_t *plan, int8_t *verdicts, int32_t *status, uint32_t poly,
                               hipStream_t stream) {
     if (n == 0) return hipSuccess;
-    const uint32_t bs = 64;
-    hipLaunchKernelGGL(rlnc_plan_kernel, dim3((uint32_t)((n + bs - 1) / bs)), dim3(bs), 0, stream, coded,
+    hipLaunchKernelGGL(rlnc_plan_kernel, dim3((uint32_t)n), dim3(64), 0, stream, coded,
                        pitch, n, cand, reinterpret_cast<RepairPlan *>(plan), verdicts, status, poly);
     return hipGetLastError();
 }

@@ -1,0 +1,97 @@
+"""Interleaved A/B timing of several library builds in ONE process (cdna_hip_programming.md §5.4
+rule 24): every build is loaded with its own ctypes handle; rounds alternate between builds so DVFS
+and device drift hit all of them alike. Prints one JSON line per build (median / min over rounds).
+
+usage: python tools/abbench.py --n 1639 --rounds 12 lib_a.so lib_b.so[:pitch] ...
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=1639)
+    ap.add_argument("--rounds", type=int, default=12)
+    ap.add_argument("--warmup-s", type=float, default=3.0)
+    ap.add_argument("libs", nargs="+")
+    a = ap.parse_args()
+    import numpy as np
+    import torch
+    from decds_amd._capi import CHUNKSET_BYTES as CS, CODED_PIECE_BYTES as F, K, N, _declare
+
+    n = a.n
+    builds = []
+    for spec in a.libs:
+        path, _, pitch = spec.partition(":")
+        L = ctypes.CDLL(os.path.abspath(path), mode=ctypes.RTLD_LOCAL)
+        _declare(L)
+        h = ctypes.c_void_p()
+        assert L.decds_ctx_create(0, ctypes.byref(h)) == 0, L.decds_last_error()
+        builds.append({"tag": os.path.basename(path)[:-3] + ("@%s" % pitch if pitch else ""), "lib": L, "ctx": h,
+                       "pitch": int(pitch) if pitch else F, "cs": CS,
+                       "t": []})
+    maxcs = max(b["cs"] for b in builds)
+    maxpitch = max(b["pitch"] for b in builds)
+    st = torch.cuda.Stream()
+    vp = ctypes.c_void_p
+    src = torch.empty(n * maxcs + 64, dtype=torch.uint8, device="cuda")
+    builds[0]["lib"].decds_fill_random_device(builds[0]["ctx"], 1, 0, vp(src.data_ptr()), src.numel(), vp(st.cuda_stream))
+    coeffs = torch.from_numpy(np.random.default_rng(2).integers(0, 256, n * N * K, dtype=np.uint8)).cuda()
+    rng = np.random.default_rng(3)
+    cand = np.full((n, N), 0xFF, np.uint8)
+    for c in range(n):
+        cand[c, :K] = rng.permutation(N)[:K]
+    cand = torch.from_numpy(cand).cuda()
+    coded = torch.empty(n * N * maxpitch + 64, dtype=torch.uint8, device="cuda")
+    plan = torch.empty(n * 128, dtype=torch.uint8, device="cuda")
+    verd = torch.empty(n * N, dtype=torch.int8, device="cuda")
+    status = torch.empty(n, dtype=torch.int32, device="cuda")
+    out = torch.empty(n * maxcs + 64, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    sp = vp(st.cuda_stream)
+
+    def run(b, ev=None):
+        L, h, p = b["lib"], b["ctx"], b["pitch"]
+        if ev:
+            ev[0].record(st)
+        assert L.decds_encode_batch(h, vp(src.data_ptr()), n, vp(coeffs.data_ptr()), vp(coded.data_ptr()), p, sp) == 0
+        if ev:
+            ev[1].record(st)
+        assert L.decds_repair_plan_batch(h, vp(coded.data_ptr()), p, n, vp(cand.data_ptr()), vp(plan.data_ptr()),
+                                         vp(verd.data_ptr()), vp(status.data_ptr()), sp) == 0
+        if ev:
+            ev[2].record(st)
+        assert L.decds_decode_batch(h, vp(coded.data_ptr()), p, n, vp(plan.data_ptr()), vp(out.data_ptr()),
+                                    vp(status.data_ptr()), sp) == 0
+        if ev:
+            ev[3].record(st)
+
+    t0 = time.time()
+    while time.time() - t0 < a.warmup_s:
+        for b in builds:
+            run(b)
+        st.synchronize()
+    for r in range(a.rounds):
+        for b in (builds if r % 2 == 0 else builds[::-1]):
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+            run(b, ev)
+            st.synchronize()
+            b["t"].append([ev[0].elapsed_time(ev[1]), ev[1].elapsed_time(ev[2]), ev[2].elapsed_time(ev[3])])
+    for b in builds:
+        t = np.array(b["t"])
+        med, mn = np.median(t, axis=0), t.min(axis=0)
+        print(json.dumps({"tag": b["tag"], "n": n, "pitch": b["pitch"], "encode_ms": round(med[0], 4),
+                          "encode_min_ms": round(mn[0], 4), "plan_ms": round(med[1], 4), "decode_ms": round(med[2], 4),
+                          "decode_min_ms": round(mn[2], 4), "encode_GBps": round(n * (CS + N * F) / med[0] / 1e6, 1),
+                          "decode_GBps": round(n * (K * F + CS) / med[2] / 1e6, 1)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
