@@ -53,9 +53,10 @@ def cpu_baseline(n_sample, seed):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import numpy as np
     import oracle as o
+    # the GPU box's CPU share is 16 threads (os.cpu_count() reports the whole machine)
     threads = max(1, min(16, os.cpu_count() or 1))
     if n_sample <= 0:
-        n_sample = threads
+        n_sample = 8 * threads  # ~10-20 s of CPU work
     blob = o.fill_random(seed, n_sample * o.CS)
     coeffs = o.fill_random(seed + 1, n_sample * o.N * o.K)
     rng = np.random.default_rng(seed)

@@ -85,6 +85,8 @@ def _declare(L):
         "decds_repairing_chunkset_free": (None, [P]),
         "decds_blob_encode_host": (c.c_int, [P, VP, SZ, VP, VP, SZ]),
         "decds_blob_repair_host": (c.c_int, [P, VP, SZ, VP, SZ, VP, VP, SZ]),
+        "decds_host_register": (c.c_int, [VP, SZ]),
+        "decds_host_unregister": (c.c_int, [VP]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -101,6 +103,7 @@ EXPORTED = [
     "decds_repairing_chunkset_new", "decds_repairing_chunkset_add_chunk_unvalidated",
     "decds_repairing_chunkset_is_ready_to_repair", "decds_repairing_chunkset_repair",
     "decds_repairing_chunkset_free", "decds_blob_encode_host", "decds_blob_repair_host",
+    "decds_host_register", "decds_host_unregister",
 ]
 
 

@@ -76,26 +76,28 @@ def fill_random_host(seed, nbytes, byte_offset=0):
     return out
 
 
-def blob_encode_host(ctx, blob, coeffs, batch=64):
+def blob_encode_host(ctx, blob, coeffs, batch=64, out=None):
     """Blob::new's chunkset loop (blob.rs:252-264) on host buffers. Returns (n*16, F) uint8."""
     blob = np.ascontiguousarray(np.frombuffer(blob, dtype=np.uint8) if isinstance(blob, (bytes, bytearray)) else blob)
     n = -(-blob.size // CHUNKSET_BYTES)
     coeffs = np.ascontiguousarray(coeffs, dtype=np.uint8)
     if coeffs.size != n * N * K:
         raise ValueError("coeffs must hold n*16*10 bytes")
-    out = np.empty((n * N, CODED_PIECE_BYTES), dtype=np.uint8)
+    if out is None:
+        out = np.empty((n * N, CODED_PIECE_BYTES), dtype=np.uint8)
     vp = ctypes.c_void_p
     check(lib().decds_blob_encode_host(ctx.handle, vp(blob.ctypes.data), blob.size, vp(coeffs.ctypes.data),
                                        vp(out.ctypes.data), batch))
     return out
 
 
-def blob_repair_host(ctx, coded, cand, blob_len, batch=64):
+def blob_repair_host(ctx, coded, cand, blob_len, batch=64, out=None):
     """RepairingBlob add_chunk/get_repaired_chunkset (blob.rs:373-473). Returns (blob, status)."""
     coded = np.ascontiguousarray(coded, dtype=np.uint8)
     n = coded.shape[0] // N
     cand = np.ascontiguousarray(cand, dtype=np.uint8).reshape(n, N)
-    out = np.empty(blob_len, dtype=np.uint8)
+    if out is None:
+        out = np.empty(blob_len, dtype=np.uint8)
     status = np.empty(n, dtype=np.int32)
     vp = ctypes.c_void_p
     check(lib().decds_blob_repair_host(ctx.handle, vp(coded.ctypes.data), n, vp(cand.ctypes.data), blob_len,
@@ -103,5 +105,15 @@ def blob_repair_host(ctx, coded, cand, blob_len, batch=64):
     return out, status
 
 
+def host_register(arr):
+    """page-lock a numpy buffer for repeated host-path calls (decds_host_register)"""
+    check(lib().decds_host_register(ctypes.c_void_p(arr.ctypes.data), arr.nbytes))
+
+
+def host_unregister(arr):
+    check(lib().decds_host_unregister(ctypes.c_void_p(arr.ctypes.data)))
+
+
 __all__ = ["encode_batch", "repair_plan_batch", "decode_batch", "repair_batch", "fill_random_device",
-           "fill_random_host", "blob_encode_host", "blob_repair_host", "NO_CANDIDATE"]
+           "fill_random_host", "blob_encode_host", "blob_repair_host", "host_register", "host_unregister",
+           "NO_CANDIDATE"]

@@ -186,6 +186,8 @@ void decds_repairing_chunkset_free(decds_repairing_chunkset *r) { delete r; }
 // b-1's D2H proceed on the copy engines. Caller buffers are page-locked with hipHostRegister for
 // the duration of the call so the copies DMA directly from/to them.
 namespace {
+// Page-locks a caller buffer for the duration of one call unless the caller already did
+// (decds_host_register): then registration fails with "already registered" and is left alone.
 struct HostReg {
     void *p = nullptr;
     bool ok = false;
@@ -279,7 +281,7 @@ int decds_blob_repair_host(decds_ctx *ctx, const uint8_t *coded_host, size_t n, 
             (e = ddst[i].alloc(batch * CS)) || (e = dcand[i].alloc(batch * N)))
             return decds_hip_error(e, "hipMalloc");
     }
-    HostReg rout(out, blob_len);
+    HostReg rout(out, blob_len), rin(coded_host, n * N * F);
     int rc = DECDS_OK;
     std::vector<std::vector<int32_t>> stat_h(2, std::vector<int32_t>(batch));
     size_t pending_b0[2] = {(size_t)-1, (size_t)-1}, pending_nb[2] = {0, 0};
@@ -343,6 +345,17 @@ int decds_blob_repair_host(decds_ctx *ctx, const uint8_t *coded_host, size_t n, 
         (void)hipStreamDestroy(st[i]);
     }
     return rc;
+}
+
+int decds_host_register(const void *ptr, size_t len) {
+    if (!ptr || !len) return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "null or empty buffer");
+    hipError_t e = hipHostRegister(const_cast<void *>(ptr), len, hipHostRegisterDefault);
+    return e == hipSuccess ? DECDS_OK : decds_hip_error(e, "hipHostRegister");
+}
+
+int decds_host_unregister(const void *ptr) {
+    hipError_t e = hipHostUnregister(const_cast<void *>(ptr));
+    return e == hipSuccess ? DECDS_OK : decds_hip_error(e, "hipHostUnregister");
 }
 
 }  // extern "C"

@@ -63,14 +63,19 @@ int decds_rank_push(uint8_t *basis, uint8_t *pivots, uint32_t *rank, const uint8
 }
 
 void decds_fill_random_host(uint64_t seed, uint64_t off, uint8_t *dst, size_t nbytes) {
-    for (size_t i = 0; i < nbytes; i++) {
-        const uint64_t p = off + i;
-        uint64_t z = seed + ((p >> 3) + 1) * 0x9E3779B97F4A7C15ull;
+    auto word = [seed](uint64_t w) {
+        uint64_t z = seed + (w + 1) * 0x9E3779B97F4A7C15ull;
         z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
         z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-        z ^= z >> 31;
-        dst[i] = (uint8_t)(z >> (8 * (p & 7)));
+        return z ^ (z >> 31);
+    };
+    size_t i = 0;
+    for (; i < nbytes && ((off + i) & 7); i++) dst[i] = (uint8_t)(word((off + i) >> 3) >> (8 * ((off + i) & 7)));
+    for (; i + 8 <= nbytes; i += 8) {
+        const uint64_t z = word((off + i) >> 3);
+        std::memcpy(dst + i, &z, 8);  // little-endian: byte p%8 of the word
     }
+    for (; i < nbytes; i++) dst[i] = (uint8_t)(word((off + i) >> 3) >> (8 * ((off + i) & 7)));
 }
 
 }  // extern "C"

@@ -156,6 +156,11 @@ int decds_blob_repair_host(decds_ctx *ctx, const uint8_t *coded_host, size_t n_c
                            const uint8_t *cand_host, size_t blob_len, uint8_t *out,
                            int32_t *status_host, size_t batch);
 
+/* Page-lock a caller buffer once for many host-path calls (otherwise each call pins and unpins
+ * its buffers itself). Pair with decds_host_unregister before freeing the buffer. */
+int decds_host_register(const void *ptr, size_t len);
+int decds_host_unregister(const void *ptr);
+
 #ifdef __cplusplus
 }
 #endif

@@ -47,7 +47,16 @@ uint64_t orc_splitmix64_word(uint64_t seed, uint64_t w) {
 }
 
 void orc_fill_random(uint64_t seed, uint64_t byte_offset, uint8_t *out, size_t len) {
-    for (size_t i = 0; i < len; i++) {
+    size_t i = 0;
+    for (; i < len && ((byte_offset + i) & 7); i++) {
+        uint64_t p = byte_offset + i;
+        out[i] = (uint8_t)(orc_splitmix64_word(seed, p >> 3) >> (8 * (p & 7)));
+    }
+    for (; i + 8 <= len; i += 8) {
+        uint64_t z = orc_splitmix64_word(seed, (byte_offset + i) >> 3);
+        for (int b = 0; b < 8; b++) out[i + b] = (uint8_t)(z >> (8 * b));
+    }
+    for (; i < len; i++) {
         uint64_t p = byte_offset + i;
         out[i] = (uint8_t)(orc_splitmix64_word(seed, p >> 3) >> (8 * (p & 7)));
     }

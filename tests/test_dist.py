@@ -1,0 +1,88 @@
+"""Multi-process (world_size 2, gloo, CPU) coverage of the N>1 bench path: chunkset-index sharding
+with no data-path collective, each rank encoding/repairing its own shard, and the
+max-over-ranks timing reduction bench.py uses. The per-rank compute here is the CPU restatement;
+on the GPU node the same shard plan drives the HIP kernels."""
+import hashlib
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+
+import bench  # noqa: E402
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_shard_range_partitions():
+    for n_total in (1, 2, 3, 103, 205, 1639, 13108):
+        for world in (1, 2, 4, 8):
+            spans = [bench.shard_range(n_total, world, r) for r in range(world)]
+            assert spans[0][0] == 0 and spans[-1][1] == n_total
+            for (a, b), (c, d) in zip(spans, spans[1:]):
+                assert b == c and a <= b
+            assert max(b - a for a, b in spans) - min(b - a for a, b in spans) <= -(-n_total // world)
+
+
+def _worker(rank, world, port, n_total, blob_len, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import oracle as o
+    lo, hi = bench.shard_range(n_total, world, rank)
+    # each rank generates only its own slice of the global blob (counter-based stream)
+    have = min(blob_len, hi * o.CS) - lo * o.CS
+    blob = np.zeros((hi - lo) * o.CS, np.uint8)
+    blob[:have] = o.fill_random(0xDEC05002, have, lo * o.CS)
+    coeffs = o.fill_random(0xC0EF0002, (hi - lo) * o.N * o.K, lo * o.N * o.K)
+    coded = o.blob_encode(blob, coeffs, nthreads=2)
+    cand = np.stack([np.random.default_rng(c).permutation(o.N) for c in range(lo, hi)]).astype(np.uint8)
+    out, status = o.blob_repair(coded, cand, blob.size, nthreads=2)
+    assert (status == 0).all() and np.array_equal(out, blob)
+    digests = [hashlib.sha256(coded[j].tobytes()).hexdigest() for j in range(coded.shape[0])]
+    # bench.py's timing reduction: MAX over ranks
+    t = torch.tensor([float(rank + 1)], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    gathered = [None] * world
+    dist.all_gather_object(gathered, digests)
+    dist.barrier()
+    dist.destroy_process_group()
+    q.put((rank, float(t.item()), gathered))
+
+
+def test_two_rank_sharded_encode_matches_single_process():
+    import oracle as o
+    n_total, blob_len = 3, 2 * o.CS + 12345      # 3 chunksets, partial last one
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, n_total, blob_len, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    res.sort()
+    assert all(r[1] == 2.0 for r in res)                       # max over ranks
+    gathered = res[0][2]
+    assert gathered == res[1][2]
+    flat = [d for rank_digests in gathered for d in rank_digests]
+    # single-process reference over the whole blob
+    blob = o.fill_random(0xDEC05002, blob_len)
+    coeffs = o.fill_random(0xC0EF0002, n_total * o.N * o.K)
+    coded = o.blob_encode(blob, coeffs, nthreads=4)
+    assert flat == [hashlib.sha256(coded[j].tobytes()).hexdigest() for j in range(coded.shape[0])]
