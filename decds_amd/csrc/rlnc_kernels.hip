@@ -23,6 +23,7 @@
 namespace decds {
 
 // ---- geometry ---------------------------------------------------------------------------------
+constexpr uint32_t DECDS_NO_CANDIDATE_U8 = 0xFF;
 constexpr uint32_t WG = 256;                                  // 4 waves
 constexpr uint32_t WGS_PER_CU = 2;                            // 2 x 80 KiB LDS = the CU's 160 KiB
 constexpr uint32_t WAVES_PER_SIMD = WGS_PER_CU * WG / 256;    // 2 -> up to 256 VGPRs per lane
@@ -443,6 +444,20 @@ __global__ __launch_bounds__(64) void rlnc_plan_kernel(const uint8_t *__restrict
     const size_t cs = blockIdx.x;
     const uint32_t lane = threadIdx.x;
     const bool col = lane < K;
+    // GF(2^8) inverses for this polynomial: 4 per lane, computed in parallel once
+    __shared__ uint8_t inv_tab[256];
+#pragma unroll
+    for (int q = 0; q < 4; q++) inv_tab[lane * 4 + q] = (uint8_t)gf_inv(lane * 4 + q, poly);
+    // all candidates' row ids and coding vectors up front (one memory latency, not sixteen):
+    // lane c < 10 holds byte c of every candidate's coding vector
+    const uint32_t my_cand = lane < N ? cand[cs * N + lane] : (uint32_t)DECDS_NO_CANDIDATE_U8;
+    uint32_t cvs[N];
+#pragma unroll
+    for (int a = 0; a < (int)N; a++) {
+        const uint32_t r = __builtin_amdgcn_readlane(my_cand, a);
+        cvs[a] = (col && r < N) ? coded[(cs * N + r) * pitch + lane] : 0u;
+    }
+    __syncthreads();
     uint32_t basis[K], raw[K];
     uint32_t piv[K], sel[K];
 #pragma unroll
@@ -450,8 +465,9 @@ __global__ __launch_bounds__(64) void rlnc_plan_kernel(const uint8_t *__restrict
     uint32_t rank = 0;
     bool ended = false;
     int32_t my_verdict = -1;  // lane a < 16 keeps candidate a's verdict
+#pragma unroll
     for (uint32_t a = 0; a < N; a++) {
-        const uint32_t r = cand[cs * N + a];
+        const uint32_t r = __builtin_amdgcn_readlane(my_cand, a);
         int32_t v;
         if (ended || r >= N) {
             ended = true;
@@ -459,7 +475,7 @@ __global__ __launch_bounds__(64) void rlnc_plan_kernel(const uint8_t *__restrict
         } else if (rank == K) {
             v = 3;  // DECDS_ERR_CHUNKSET_READY_TO_REPAIR
         } else {
-            const uint32_t cv = col ? coded[(cs * N + r) * pitch + lane] : 0u;
+            const uint32_t cv = cvs[a];
             uint32_t row = cv;
 #pragma unroll
             for (int e = 0; e < (int)K; e++) {
@@ -473,7 +489,7 @@ __global__ __launch_bounds__(64) void rlnc_plan_kernel(const uint8_t *__restrict
                 v = 4;  // DECDS_ERR_CHUNK_DECODING_FAILED: piece not useful
             } else {
                 const uint32_t p = __builtin_ctzll(nz);
-                const uint32_t inv = gf_inv(__builtin_amdgcn_readlane(row, p), poly);
+                const uint32_t inv = inv_tab[__builtin_amdgcn_readlane(row, p)];
                 row = gf_mul(row, inv, poly);
 #pragma unroll
                 for (int e = 0; e < (int)K; e++) {
@@ -521,7 +537,7 @@ __global__ __launch_bounds__(64) void rlnc_plan_kernel(const uint8_t *__restrict
                 m[c] = m[i];
                 m[i] = t;
             }
-        const uint32_t inv = gf_inv(__builtin_amdgcn_readlane(m[c], c), poly);
+        const uint32_t inv = inv_tab[__builtin_amdgcn_readlane(m[c], c)];
         m[c] = gf_mul(m[c], inv, poly);
 #pragma unroll
         for (int i = 0; i < (int)K; i++) {

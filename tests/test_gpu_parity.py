@@ -294,3 +294,55 @@ def test_cfg2_one_gib_encode_repair_device_resident(ctx):
         assert st[c] == (0 if rank == K else 5)
     ok = torch.from_numpy(st == 0).cuda().repeat_interleave(CS)
     assert torch.equal(out[ok], src[ok])
+
+
+def test_repair_pitch_and_repeated_candidates(ctx):
+    # decode from a padded coded layout; a candidate row repeated in the arrival order is not useful
+    n, pitch = 2, F + 4093
+    data = o.fill_random(0xDEC05004, n * CS)
+    coeffs = o.fill_random(0xC0EF0004, n * N * K)
+    coded = torch.empty((n * N - 1) * pitch + F, dtype=torch.uint8, device="cuda")
+    codec.encode_batch(ctx, dev(data), n, dev(coeffs), coded, pitch)
+    cand = np.full((n, N), 0xFF, np.uint8)
+    cand[0, :12] = [3, 3, 7, 1, 0, 15, 2, 9, 11, 4, 5, 6]
+    cand[1, :16] = np.random.default_rng(8).permutation(N)
+    plan = torch.empty(n * 128, dtype=torch.uint8, device="cuda")
+    verd = torch.empty(n * N, dtype=torch.int8, device="cuda")
+    status = torch.empty(n, dtype=torch.int32, device="cuda")
+    out = torch.zeros(n * CS, dtype=torch.uint8, device="cuda")
+    codec.repair_batch(ctx, coded, n, dev(cand), plan, verd, out, status, pitch)
+    v = host(verd).reshape(n, N)
+    assert v[0, 1] == NOT_USEFUL
+    assert list(v[1, 10:]) == [AFTER_READY] * 6 or NOT_USEFUL in list(v[1])
+    st = host(status)
+    res = host(out)
+    for c in range(n):
+        if st[c] == 0:
+            assert np.array_equal(res[c * CS:(c + 1) * CS], data[c * CS:(c + 1) * CS])
+    assert st[0] == 0
+
+
+def test_blob_host_not_ready_chunkset(ctx):
+    blob_len = CS + 777
+    blob = o.fill_random(0xB10C, blob_len)
+    coeffs = o.fill_random(0xC0F0, 2 * N * K)
+    coded = codec.blob_encode_host(ctx, blob, coeffs)
+    cand = np.stack([np.random.default_rng(c).permutation(N) for c in range(2)]).astype(np.uint8)
+    cand[1, 9:] = 0xFF                                   # only 9 chunks of chunkset 1 arrive
+    out, status = codec.blob_repair_host(ctx, coded, cand, blob_len)
+    assert status[0] == 0 and status[1] == 5
+    assert np.array_equal(out[:CS], blob[:CS]) and not out[CS:].any()
+
+
+def test_encode_large_n_last_chunkset_bounds(ctx):
+    # the last chunkset of a large batch sits at the very end of its allocations
+    n = 40
+    src = torch.empty(n * CS, dtype=torch.uint8, device="cuda")
+    codec.fill_random_device(ctx, 0xABCD, src)
+    coeffs = o.fill_random(0xC0EF0005, n * N * K)
+    coded = torch.empty(n * N * F, dtype=torch.uint8, device="cuda")
+    codec.encode_batch(ctx, src, n, dev(coeffs), coded)
+    torch.cuda.synchronize()
+    c = n - 1
+    ref = o.chunkset_encode(src[c * CS:].cpu().numpy(), coeffs[c * 160:], nthreads=8)
+    assert np.array_equal(coded[c * N * F:].cpu().numpy().reshape(N, F), ref)

@@ -93,6 +93,40 @@ __global__ __launch_bounds__(WG, WAVES_PER_SIMD) void pattern_m_kernel(const uin
     }
 }
 
+// outputs written NP rows at a time: per tile, 16/NP passes each re-loading the 10 input rows
+// (the re-loads hit L2) and storing NP output rows -> fewer concurrent write streams per wave
+template <int NP>
+__global__ __launch_bounds__(WG, WAVES_PER_SIMD) void pattern_np_kernel(const uint8_t *__restrict__ src, size_t n,
+                                                                      uint8_t *__restrict__ dst, Geom g) {
+    uint32_t t0, t1;
+    tile_range(n, t0, t1);
+    uint32_t ioff[K], ooff[N];
+#pragma unroll
+    for (int i = 0; i < (int)K; i++) ioff[i] = (uint32_t)(i * g.istride);
+#pragma unroll
+    for (int j = 0; j < (int)N; j++) ooff[j] = (uint32_t)(j * g.ostride + g.opoff);
+    for (uint32_t t = t0; t < t1; t++) {
+        const uint32_t cs = t / TILES_PER_CS, tile = t % TILES_PER_CS;
+        const uint8_t *ibase = src + (size_t)cs * g.cstride;
+        uint8_t *obase = dst + (size_t)cs * N * g.ostride;
+        const uint32_t block = tile * TILE_BLOCKS + threadIdx.x;
+        if (block >= MAIN_BLOCKS) continue;
+        const uint32_t col0 = block * COLS_PER_LANE;
+#pragma unroll
+        for (int ps = 0; ps < (int)N / NP; ps++) {
+            uint4 x[K];
+            load_block<EncTune, K>(x, ibase, ioff, col0);
+#pragma unroll
+            for (int jj = 0; jj < NP; jj++) {
+                const int j = ps * NP + jj;
+                const uint4 a = x[j % K], b = x[(j + 3) % K];
+                strow<-1>(obase, ooff[j] + col0, make_uint4(a.x ^ b.y, a.y ^ b.z, a.z ^ b.w, a.w ^ b.x));
+            }
+            __builtin_amdgcn_s_waitcnt(0);  // keep the passes apart
+        }
+    }
+}
+
 __global__ void random_fill(uint64_t *p, size_t nw) {
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < nw; i += (size_t)gridDim.x * blockDim.x) {
         uint64_t z = (i + 1) * 0x9E3779B97F4A7C15ull;
@@ -135,10 +169,14 @@ int main(int argc, char **argv) {
     std::vector<Case> cases;
     for (int gi = 0; gi < (int)geoms.size(); gi++)
         for (const char *k : {"load+store", "store", "load"}) cases.push_back({k, gi, {}});
-    for (const char *k : {"m2", "m4"}) cases.push_back({k, 0, {}});
+    for (const char *k : {"m2", "np4", "np8"}) cases.push_back({k, 0, {}});
     auto launch = [&](const Case &c) {
         const Geom &g = geoms[c.g];
-        if (c.kind[0] == 'm' && c.kind[1] == '2')
+        if (c.kind[0] == 'n' && c.kind[2] == '4')
+            hipLaunchKernelGGL((pattern_np_kernel<4>), dim3(grid), dim3(WG), 0, 0, src, n, dst, g);
+        else if (c.kind[0] == 'n')
+            hipLaunchKernelGGL((pattern_np_kernel<8>), dim3(grid), dim3(WG), 0, 0, src, n, dst, g);
+        else if (c.kind[0] == 'm' && c.kind[1] == '2')
             hipLaunchKernelGGL((pattern_m_kernel<2>), dim3(grid), dim3(WG), 0, 0, src, n, dst, g);
         else if (c.kind[0] == 'm')
             hipLaunchKernelGGL((pattern_m_kernel<4>), dim3(grid), dim3(WG), 0, 0, src, n, dst, g);
@@ -171,7 +209,7 @@ int main(int argc, char **argv) {
         std::sort(c.ms.begin(), c.ms.end());
         const double med = c.ms[c.ms.size() / 2];
         const double rd = (double)n * CS, wr = (double)n * N * F;
-        const double bytes = (c.kind[0] == 'm' || c.kind[4] == '+') ? rd + wr : c.kind[0] == 's' ? wr : rd;
+        const double bytes = (c.kind[0] == 'm' || c.kind[0] == 'n' || c.kind[4] == '+') ? rd + wr : c.kind[0] == 's' ? wr : rd;
         printf("{\"geom\": \"%s\", \"kind\": \"%s\", \"n\": %zu, \"ms\": %.4f, \"GBps\": %.1f}\n", geoms[c.g].name,
                c.kind, n, med, bytes / med / 1e6);
     }
