@@ -313,7 +313,10 @@ def test_repair_pitch_and_repeated_candidates(ctx):
     codec.repair_batch(ctx, coded, n, dev(cand), plan, verd, out, status, pitch)
     v = host(verd).reshape(n, N)
     assert v[0, 1] == NOT_USEFUL
-    assert list(v[1, 10:]) == [AFTER_READY] * 6 or NOT_USEFUL in list(v[1])
+    ch = host(coded)
+    for c in range(n):
+        rows = np.stack([ch[(c * N + r) * pitch:(c * N + r) * pitch + F] for r in range(N)])
+        assert list(v[c]) == _oracle_verdicts(rows, cand[c])[0]
     st = host(status)
     res = host(out)
     for c in range(n):
