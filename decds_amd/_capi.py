@@ -86,6 +86,10 @@ def _declare(L):
         "decds_blob_encode_host": (c.c_int, [P, VP, SZ, VP, VP, SZ]),
         "decds_blob_repair_host": (c.c_int, [P, VP, SZ, VP, SZ, VP, VP, SZ]),
         "decds_host_register": (c.c_int, [VP, SZ]),
+        "decds_commit_batch": (c.c_int, [P, VP, SZ, SZ, c.c_uint64, VP, VP, VP, VP]),
+        "decds_blake3": (None, [VP, SZ, VP]),
+        "decds_merkle_tree": (c.c_int, [VP, SZ, VP, VP]),
+        "decds_merkle_verify": (c.c_int, [SZ, VP, VP, SZ, VP]),
         "decds_host_unregister": (c.c_int, [VP]),
     }
     for name, (res, args) in sig.items():
@@ -103,7 +107,8 @@ EXPORTED = [
     "decds_repairing_chunkset_new", "decds_repairing_chunkset_add_chunk_unvalidated",
     "decds_repairing_chunkset_is_ready_to_repair", "decds_repairing_chunkset_repair",
     "decds_repairing_chunkset_free", "decds_blob_encode_host", "decds_blob_repair_host",
-    "decds_host_register", "decds_host_unregister",
+    "decds_host_register", "decds_host_unregister", "decds_commit_batch", "decds_blake3",
+    "decds_merkle_tree", "decds_merkle_verify",
 ]
 
 

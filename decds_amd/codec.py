@@ -65,6 +65,17 @@ def repair_batch(ctx, coded, n, cand, plan, verdicts, dst, status, pitch=CODED_P
     decode_batch(ctx, coded, n, plan, dst, status, pitch, stream)
 
 
+def commit_batch(ctx, coded, n, digests, roots, proofs, first_chunkset_id=0, pitch=CODED_PIECE_BYTES, stream=None):
+    """ChunkSet::new's commitment (chunkset.rs:54-63) for n device-resident chunksets: per coded row
+    the BLAKE3 chunk digest (chunk.rs:40-46), per chunkset the 16-leaf Merkle root and proofs."""
+    _need(coded, (n * N - 1) * pitch + CODED_PIECE_BYTES, "coded")
+    _need(digests, n * N * 32, "digests")
+    _need(roots, n * 32, "roots")
+    _need(proofs, n * N * 4 * 32, "proofs")
+    check(lib().decds_commit_batch(ctx.handle, _ptr(coded), pitch, n, first_chunkset_id, _ptr(digests), _ptr(roots),
+                                   _ptr(proofs), _stream(stream)))
+
+
 def fill_random_device(ctx, seed, dst, nbytes=None, byte_offset=0, stream=None):
     nbytes = dst.numel() * dst.element_size() if nbytes is None else nbytes
     check(lib().decds_fill_random_device(ctx.handle, seed, byte_offset, _ptr(dst), nbytes, _stream(stream)))
@@ -114,6 +125,6 @@ def host_unregister(arr):
     check(lib().decds_host_unregister(ctypes.c_void_p(arr.ctypes.data)))
 
 
-__all__ = ["encode_batch", "repair_plan_batch", "decode_batch", "repair_batch", "fill_random_device",
+__all__ = ["commit_batch", "encode_batch", "repair_plan_batch", "decode_batch", "repair_batch", "fill_random_device",
            "fill_random_host", "blob_encode_host", "blob_repair_host", "host_register", "host_unregister",
            "NO_CANDIDATE"]

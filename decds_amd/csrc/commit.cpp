@@ -1,0 +1,134 @@
+// commit.cpp — C-ABI of the commitment layer: the batched device path (ChunkSet::new's digests,
+// chunkset Merkle roots and proofs) and host helpers for the blob-level tree (blob.rs:266-273),
+// which covers only the 32-byte chunkset roots.
+#include <cstring>
+#include <vector>
+
+#include "../../include/decds_rlnc.h"
+#include "blake3_impl.h"
+#include "capi_internal.h"
+#include "commit_kernels.h"
+#include "rlnc_layout.h"
+
+using namespace decds;
+
+namespace {
+
+void to_words(const uint8_t *b, size_t len, uint32_t w[16]) {
+    uint8_t blk[64] = {0};
+    std::memcpy(blk, b, len);
+    for (int i = 0; i < 16; i++)
+        w[i] = blk[4 * i] | (uint32_t)blk[4 * i + 1] << 8 | (uint32_t)blk[4 * i + 2] << 16 | (uint32_t)blk[4 * i + 3] << 24;
+}
+
+void to_bytes(const uint32_t w[8], uint8_t out[32]) {
+    for (int i = 0; i < 8; i++)
+        for (int b = 0; b < 4; b++) out[4 * i + b] = (uint8_t)(w[i] >> (8 * b));
+}
+
+// chaining value of chunk `index` (len <= 1024 bytes); `root` finalises a single-chunk message
+void chunk_cv(const uint8_t *p, size_t len, uint64_t index, bool root, uint32_t cv[8]) {
+    for (int i = 0; i < 8; i++) cv[i] = b3::K3.iv[i];
+    const size_t blocks = len == 0 ? 1 : (len + 63) / 64;
+    for (size_t b = 0; b < blocks; b++) {
+        const size_t bl = b + 1 < blocks ? 64 : len - 64 * b;
+        uint32_t m[16];
+        to_words(p + 64 * b, bl, m);
+        uint32_t flags = (b == 0 ? b3::CHUNK_START : 0u) | (b + 1 == blocks ? b3::CHUNK_END : 0u);
+        if (root && b + 1 == blocks) flags |= b3::ROOT;
+        b3::compress(cv, m, index, (uint32_t)bl, flags, cv);
+    }
+}
+
+// BLAKE3 tree hash of [p, p+len) starting at chunk `first`: left subtree = largest power-of-two
+// number of chunks that leaves at least one byte to the right (the BLAKE3 tree rule)
+void subtree_cv(const uint8_t *p, size_t len, uint64_t first, bool root, uint32_t cv[8]) {
+    if (len <= b3::CHUNK) {
+        chunk_cv(p, len, first, root, cv);
+        return;
+    }
+    size_t left_chunks = 1;
+    while ((left_chunks * 2) * b3::CHUNK < len) left_chunks *= 2;
+    const size_t left_len = left_chunks * b3::CHUNK;
+    uint32_t l[8], r[8];
+    subtree_cv(p, left_len, first, false, l);
+    subtree_cv(p + left_len, len - left_len, first + left_chunks, false, r);
+    b3::parent(l, r, root ? b3::ROOT : 0u, cv);
+}
+
+void hash_pair(const uint8_t *l, const uint8_t *r, uint8_t out[32]) {
+    uint8_t buf[64];
+    std::memcpy(buf, l, 32);
+    std::memcpy(buf + 32, r, 32);
+    uint32_t m[16], w[8];
+    to_words(buf, 64, m);
+    b3::compress(b3::K3.iv, m, 0, 64, b3::CHUNK_START | b3::CHUNK_END | b3::ROOT, w);
+    to_bytes(w, out);
+}
+
+}  // namespace
+
+extern "C" {
+
+void decds_blake3(const uint8_t *data, size_t len, uint8_t out[32]) {
+    uint32_t cv[8];
+    subtree_cv(data, len, 0, true, cv);
+    to_bytes(cv, out);
+}
+
+int decds_merkle_tree(const uint8_t *leaves, size_t n, uint8_t root[32], uint8_t *proofs) {
+    if (!leaves || !root || n == 0)
+        return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "no leaf nodes to build merkle tree on");
+    int depth = 0;
+    while (((size_t)1 << depth) < n) depth++;
+    std::vector<uint8_t> cur(leaves, leaves + n * 32), nxt;
+    std::vector<size_t> idx(n);
+    for (size_t i = 0; i < n; i++) idx[i] = i;
+    uint8_t zero[32] = {0};
+    for (int lvl = 0; cur.size() > 32; lvl++) {
+        const size_t len = cur.size() / 32, plen = (len + 1) / 2;
+        nxt.assign(plen * 32, 0);
+        for (size_t p = 0; p < plen; p++)
+            hash_pair(&cur[2 * p * 32], 2 * p + 1 < len ? &cur[(2 * p + 1) * 32] : zero, &nxt[p * 32]);
+        if (proofs)
+            for (size_t i = 0; i < n; i++) {
+                const size_t s = idx[i] ^ 1;
+                std::memcpy(proofs + (i * depth + lvl) * 32, s < len ? &cur[s * 32] : zero, 32);
+                idx[i] >>= 1;
+            }
+        uint8_t z2[32];
+        hash_pair(zero, zero, z2);  // merkle_tree.rs:41 — the padding hash climbs with the level
+        std::memcpy(zero, z2, 32);
+        cur.swap(nxt);
+    }
+    std::memcpy(root, cur.data(), 32);
+    return depth;
+}
+
+int decds_merkle_verify(size_t leaf_index, const uint8_t leaf[32], const uint8_t *proof, size_t proof_len,
+                        const uint8_t root[32]) {
+    uint8_t h[32], t[32];
+    std::memcpy(h, leaf, 32);
+    for (size_t k = 0; k < proof_len; k++) {
+        if ((leaf_index & 1) == 0)
+            hash_pair(h, proof + 32 * k, t);
+        else
+            hash_pair(proof + 32 * k, h, t);
+        std::memcpy(h, t, 32);
+        leaf_index >>= 1;
+    }
+    return std::memcmp(h, root, 32) == 0;
+}
+
+int decds_commit_batch(decds_ctx *ctx, const uint8_t *coded, size_t pitch, size_t n, uint64_t first_chunkset_id,
+                       uint8_t *digests, uint8_t *roots, uint8_t *proofs, void *stream) {
+    int s = decds_ctx_bind(ctx);
+    if (s) return s;
+    if (!coded || !digests || !roots || !proofs || n == 0)
+        return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "null buffer or no chunksets");
+    if (pitch < F) return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "coded pitch %zu < %llu", pitch, (unsigned long long)F);
+    hipError_t e = launch_commit(coded, pitch, n, first_chunkset_id, digests, roots, proofs, (hipStream_t)stream);
+    return e == hipSuccess ? DECDS_OK : decds_hip_error(e, "commit kernels launch");
+}
+
+}  // extern "C"

@@ -1,0 +1,209 @@
+// commit_kernels.hip — gfx950 kernels for the commitment layer that ChunkSet::new builds right
+// after encoding (chunkset.rs:54-63): the BLAKE3 digest of every coded chunk (chunk.rs:40-46,
+// message = chunkset_id as u64 LE || chunk_id as u64 LE || the 1,048,587-byte coded piece) and the
+// 16-leaf Merkle tree of each chunkset with every leaf's inclusion proof (merkle_tree.rs:23-116).
+//
+// Digest: one workgroup per coded row. The 1,048,603-byte message is 1024 full BLAKE3 chunks + one
+// 27-byte chunk; the root is PARENT|ROOT(subtree of the 1024 chunks, last chunk) — BLAKE3's tree
+// for 1025 chunks. ~17.4 K compressions per row (16,384 chunk blocks + 1,023 parents + 2):
+// VALU-bound at 12 VALU per G x 8 G x 7 rounds = 672 per 64-byte block.
+#include <hip/hip_runtime.h>
+
+#include "blake3_impl.h"
+#include "commit_kernels.h"
+#include "rlnc_layout.h"
+
+namespace decds {
+
+constexpr uint32_t MSG_BYTES = 16 + (uint32_t)F;                   // ids || coded piece
+constexpr uint32_t FULL_CHUNKS = MSG_BYTES / b3::CHUNK;            // 1024
+constexpr uint32_t LAST_BYTES = MSG_BYTES - FULL_CHUNKS * b3::CHUNK;  // 27
+static_assert(FULL_CHUNKS == 1024 && LAST_BYTES == 27, "BLAKE3 tree shape of a coded chunk message");
+
+constexpr uint32_t CPT = 4;                       // consecutive BLAKE3 chunks per thread
+constexpr uint32_t DG_WG = FULL_CHUNKS / CPT;     // 256 threads per row
+
+struct Block {
+    uint32_t w[16];
+};
+
+// One 64-byte message block (block b of full chunk c of a row). Message bytes 0..15 are the two
+// little-endian u64 ids, so piece offset = message offset - 16 (≡ 0 mod 16): every block starts at
+// the row's own misalignment s = piece mod 16. Byte-misaligned dwordx4 loads in this lane-per-chunk
+// order run at a third of the aligned rate (tools/hashmem.hip: 2.3 vs 5.5 TB/s), so each block is
+// read as 16-byte-ALIGNED words — four, plus a fifth when s != 0 — and funnel-shifted into place:
+// dword shift Q = s / 4 is a template parameter (the row picks the instantiation once, a
+// wave-uniform branch), byte shift r = s % 4 one v_alignbyte per message word. Q = -1: s == 0.
+// The fifth word of the last block of a row with s in 1..4 reaches up to 4 bytes past the row —
+// inside the same 16-byte granule as the row's last byte, so never a separate page.
+template <int Q>
+__device__ __forceinline__ Block load_block(const uint8_t *piece, const uint8_t *abase, uint32_t r, uint32_t c,
+                                            uint32_t b, uint64_t cs_id, uint64_t chunk_id) {
+    Block m;
+    const int64_t off = (int64_t)c * b3::CHUNK + b * b3::BLOCK - 16;
+    if (off >= 0) {
+        const uint4 *pa = reinterpret_cast<const uint4 *>(abase + off);
+        uint32_t w[20];
+#pragma unroll
+        for (int k = 0; k < (Q < 0 ? 4 : 5); k++) {
+            const uint4 v = pa[k];
+            w[4 * k] = v.x, w[4 * k + 1] = v.y, w[4 * k + 2] = v.z, w[4 * k + 3] = v.w;
+        }
+#pragma unroll
+        for (int i = 0; i < 16; i++) {
+            if constexpr (Q < 0)
+                m.w[i] = w[i];
+            else
+                m.w[i] = __builtin_amdgcn_alignbyte(w[i + Q + 1], w[i + Q], r);
+        }
+    } else {
+        // block 0 of chunk 0: ids, then piece bytes 0..47. The address is wave-uniform here: spelled
+        // byte-wise so it cannot become a scalar (s_load) access, which drops misalignment
+        m.w[0] = (uint32_t)cs_id, m.w[1] = (uint32_t)(cs_id >> 32);
+        m.w[2] = (uint32_t)chunk_id, m.w[3] = (uint32_t)(chunk_id >> 32);
+#pragma unroll
+        for (int i = 4; i < 16; i++) {
+            const uint8_t *p = piece + 4 * (i - 4);
+            m.w[i] = p[0] | (uint32_t)p[1] << 8 | (uint32_t)p[2] << 16 | (uint32_t)p[3] << 24;
+        }
+    }
+    return m;
+}
+
+// chaining value of full chunk c of a row (16 blocks)
+template <int Q>
+__device__ __forceinline__ void chunk_cv(const uint8_t *piece, const uint8_t *abase, uint32_t r, uint32_t c,
+                                         uint64_t cs_id, uint64_t chunk_id, uint32_t cv[8]) {
+#pragma unroll
+    for (int i = 0; i < 8; i++) cv[i] = b3::K3.iv[i];
+#pragma unroll 1
+    for (uint32_t b = 0; b < 16; b++) {
+        const Block m = load_block<Q>(piece, abase, r, c, b, cs_id, chunk_id);
+        const uint32_t flags = (b == 0 ? b3::CHUNK_START : 0u) | (b == 15 ? b3::CHUNK_END : 0u);
+        b3::compress(cv, m.w, c, b3::BLOCK, flags, cv);
+    }
+}
+
+// thread t: chunks 4t..4t+3 folded into the chaining value of their 4-chunk subtree (all lanes busy)
+template <int Q>
+__device__ __forceinline__ void subtree4_cv(const uint8_t *piece, uint32_t t, uint64_t cs_id, uint64_t chunk_id,
+                                            uint32_t acc[8]) {
+    const uint32_t s = (uint32_t)(reinterpret_cast<uintptr_t>(piece) & 15);
+    const uint8_t *abase = piece - s;
+    const uint32_t r = s & 3;
+    uint32_t a[8], b[8], lo[8], hi[8];
+    chunk_cv<Q>(piece, abase, r, 4 * t, cs_id, chunk_id, a);
+    chunk_cv<Q>(piece, abase, r, 4 * t + 1, cs_id, chunk_id, b);
+    b3::parent(a, b, 0, lo);
+    chunk_cv<Q>(piece, abase, r, 4 * t + 2, cs_id, chunk_id, a);
+    chunk_cv<Q>(piece, abase, r, 4 * t + 3, cs_id, chunk_id, b);
+    b3::parent(a, b, 0, hi);
+    b3::parent(lo, hi, 0, acc);
+}
+
+// Digest of one coded row per 256-thread workgroup: 4-chunk subtrees in registers, the 256
+// subtree values folded in LDS (8 PARENT levels), then thread 0 adds the 27-byte 1025th chunk under
+// the ROOT parent.
+__global__ __launch_bounds__(DG_WG) void chunk_digest_kernel(const uint8_t *__restrict__ coded, size_t pitch,
+                                                             uint64_t first_chunkset_id,
+                                                             uint8_t *__restrict__ digests) {
+    __shared__ uint32_t cvs[DG_WG][8];
+    const uint32_t row = blockIdx.x;                 // c*16 + j
+    const uint64_t cs_id = first_chunkset_id + row / N;
+    const uint64_t chunk_id = cs_id * N + row % N;   // chunkset.rs:47
+    const uint8_t *piece = coded + (size_t)row * pitch;
+    const uint32_t t = threadIdx.x;
+    uint32_t acc[8];
+    switch ((uint32_t)(reinterpret_cast<uintptr_t>(piece) & 15) >> 2 |
+            ((reinterpret_cast<uintptr_t>(piece) & 15) == 0 ? 4u : 0u)) {
+        case 0: subtree4_cv<0>(piece, t, cs_id, chunk_id, acc); break;
+        case 1: subtree4_cv<1>(piece, t, cs_id, chunk_id, acc); break;
+        case 2: subtree4_cv<2>(piece, t, cs_id, chunk_id, acc); break;
+        case 3: subtree4_cv<3>(piece, t, cs_id, chunk_id, acc); break;
+        default: subtree4_cv<-1>(piece, t, cs_id, chunk_id, acc); break;
+    }
+#pragma unroll
+    for (int i = 0; i < 8; i++) cvs[t][i] = acc[i];
+    __syncthreads();
+    // PARENT levels over the 256 subtree values (complete binary tree, in place)
+#pragma unroll 1
+    for (uint32_t width = DG_WG / 2; width >= 1; width /= 2) {
+        uint32_t out[8];
+        if (t < width) b3::parent(cvs[2 * t], cvs[2 * t + 1], 0, out);
+        __syncthreads();
+        if (t < width)
+#pragma unroll
+            for (int i = 0; i < 8; i++) cvs[t][i] = out[i];
+        __syncthreads();
+    }
+    if (t == 0) {
+        // last chunk: LAST_BYTES message bytes = the piece's final 27 bytes, one partial block
+        uint32_t m[16], last[8], root[8], left[8];
+#pragma unroll
+        for (int i = 0; i < 16; i++) {
+            uint32_t w = 0;
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+                if (4 * i + k < (int)LAST_BYTES) w |= (uint32_t)piece[FULL_CHUNKS * b3::CHUNK - 16 + 4 * i + k] << (8 * k);
+            m[i] = w;
+        }
+        b3::compress(b3::K3.iv, m, FULL_CHUNKS, LAST_BYTES, b3::CHUNK_START | b3::CHUNK_END, last);
+#pragma unroll
+        for (int i = 0; i < 8; i++) left[i] = cvs[0][i];
+        b3::parent(left, last, b3::ROOT, root);
+        uint32_t *d = reinterpret_cast<uint32_t *>(digests + (size_t)row * 32);
+#pragma unroll
+        for (int i = 0; i < 8; i++) d[i] = root[i];
+    }
+}
+
+// Merkle tree of one chunkset's 16 digests (merkle_tree.rs:23-50) and the 4-hash inclusion proof of
+// every leaf (merkle_tree.rs:75-116); 16 leaves make a complete tree, no zero-hash padding. Lane
+// j of a 16-lane group holds the node above leaf j; at level l its sibling node sits in lane
+// j ^ 2^l, which is also leaf j's proof element for that level. Every lane hashes its own parent
+// (redundantly within a pair), so the 4 levels cost 4 compressions with all lanes active.
+constexpr uint32_t MK_WG = 64;
+__global__ __launch_bounds__(MK_WG) void chunkset_merkle_kernel(const uint8_t *__restrict__ digests, size_t n,
+                                                                uint8_t *__restrict__ roots,
+                                                                uint8_t *__restrict__ proofs) {
+    const size_t g = (size_t)blockIdx.x * MK_WG + threadIdx.x;  // = cs * 16 + leaf
+    const uint32_t j = threadIdx.x & (N - 1);
+    const bool live = g < n * N;
+    uint32_t node[8];
+    const uint32_t *d = reinterpret_cast<const uint32_t *>(digests + (live ? g : 0) * 32);
+#pragma unroll
+    for (int w = 0; w < 8; w++) node[w] = d[w];
+    uint32_t *pr = reinterpret_cast<uint32_t *>(proofs + g * 4 * 32);
+#pragma unroll
+    for (uint32_t level = 0; level < 4; level++) {
+        uint32_t sib[8], l[8], r[8];
+        const bool right = (j >> level) & 1u;
+#pragma unroll
+        for (int w = 0; w < 8; w++) {
+            sib[w] = __shfl_xor(node[w], 1 << level, N);
+            l[w] = right ? sib[w] : node[w];
+            r[w] = right ? node[w] : sib[w];
+            if (live) pr[level * 8 + w] = sib[w];
+        }
+        b3::hash64(l, r, node);
+    }
+    if (live && j == 0) {
+        uint32_t *rt = reinterpret_cast<uint32_t *>(roots + (g / N) * 32);
+#pragma unroll
+        for (int w = 0; w < 8; w++) rt[w] = node[w];
+    }
+}
+
+hipError_t launch_commit(const uint8_t *coded, size_t pitch, size_t n, uint64_t first_chunkset_id, uint8_t *digests,
+                         uint8_t *roots, uint8_t *proofs, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(chunk_digest_kernel, dim3((uint32_t)(n * N)), dim3(DG_WG), 0, stream, coded, pitch,
+                       first_chunkset_id, digests);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(chunkset_merkle_kernel, dim3((uint32_t)((n * N + MK_WG - 1) / MK_WG)), dim3(MK_WG), 0, stream,
+                       digests, n, roots, proofs);
+    return hipGetLastError();
+}
+
+}  // namespace decds

@@ -156,6 +156,23 @@ int decds_blob_repair_host(decds_ctx *ctx, const uint8_t *coded_host, size_t n_c
                            const uint8_t *cand_host, size_t blob_len, uint8_t *out,
                            int32_t *status_host, size_t batch);
 
+/* ---- commitment layer (next row: chunk digests + Merkle trees) ------------ */
+/* ChunkSet::new's commitment for a batch (chunkset.rs:54-63): for coded row r = c*16+j,
+ * digests[r] = Chunk::digest = BLAKE3(chunkset_id u64 LE || chunk_id u64 LE || row) (chunk.rs:40-46)
+ * with chunkset_id = first_chunkset_id + c, chunk_id = chunkset_id*16 + j (chunkset.rs:47);
+ * roots[c] = MerkleTree root of the 16 digests (merkle_tree.rs:23-50); proofs[(c*16+j)*4 + k] =
+ * leaf j's 4-hash inclusion proof (merkle_tree.rs:75-116). Device pointers; 32-byte hashes. */
+int decds_commit_batch(decds_ctx *ctx, const uint8_t *coded, size_t pitch, size_t n_chunksets,
+                       uint64_t first_chunkset_id, uint8_t *digests, uint8_t *roots, uint8_t *proofs,
+                       void *stream);
+/* host helpers: BLAKE3 (crate blake3 as used by decds), the Merkle tree over arbitrary n leaves
+ * with decds' zero-hash padding (blob-level tree, blob.rs:266-273) and proof verification
+ * (merkle_tree.rs:131-146). decds_merkle_tree returns the proof depth (proofs: n x depth x 32). */
+void decds_blake3(const uint8_t *data, size_t len, uint8_t out[32]);
+int decds_merkle_tree(const uint8_t *leaves, size_t n, uint8_t root[32], uint8_t *proofs);
+int decds_merkle_verify(size_t leaf_index, const uint8_t leaf[32], const uint8_t *proof, size_t proof_len,
+                        const uint8_t root[32]);
+
 /* Page-lock a caller buffer once for many host-path calls (otherwise each call pins and unpins
  * its buffers itself). Pair with decds_host_unregister before freeing the buffer. */
 int decds_host_register(const void *ptr, size_t len);

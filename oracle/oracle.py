@@ -58,6 +58,10 @@ def lib():
             ("orc_matrix_inverse", c.c_int, [vp, vp, sz, u32]),
             ("orc_blob_encode", c.c_int, [vp, sz, vp, vp, u32, u8, c.c_int]),
             ("orc_blob_repair", c.c_int, [vp, sz, vp, sz, vp, vp, u32, u8, c.c_int]),
+            ("orc_blake3", None, [vp, sz, vp]),
+            ("orc_chunk_digest", None, [u64, u64, vp, sz, vp]),
+            ("orc_merkle", c.c_int, [vp, sz, vp, vp]),
+            ("orc_merkle_verify", c.c_int, [sz, vp, vp, sz, vp]),
         ]:
             f = getattr(L_, name)
             f.restype, f.argtypes = res, args
@@ -178,3 +182,41 @@ def blob_repair(coded, cand, blob_len, poly=POLY, marker=MARKER, nthreads=1):
     status = np.empty(n, dtype=np.int32)
     lib().orc_blob_repair(_p(coded), n, _p(cand), blob_len, _p(out), _p(status), poly, marker, nthreads)
     return out, status
+
+
+# ---- commitment layer (blake3_oracle.c) ----------------------------------------------------------
+def blake3(data):
+    data = np.ascontiguousarray(np.frombuffer(bytes(data), np.uint8) if isinstance(data, (bytes, bytearray)) else data,
+                                dtype=np.uint8)
+    out = np.empty(32, np.uint8)
+    lib().orc_blake3(_p(data) if data.size else None, data.size, _p(out))
+    return out.tobytes()
+
+
+def chunk_digest(chunkset_id, chunk_id, data):
+    """chunk.rs:40-46"""
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    out = np.empty(32, np.uint8)
+    lib().orc_chunk_digest(chunkset_id, chunk_id, _p(data), data.size, _p(out))
+    return out.tobytes()
+
+
+def merkle(leaves):
+    """merkle_tree.rs:23-116 -> (root, proofs[n][depth] of 32-byte hashes)"""
+    lv = np.ascontiguousarray(np.frombuffer(b"".join(leaves), np.uint8))
+    n = len(leaves)
+    depth = max(0, (n - 1).bit_length())
+    root = np.empty(32, np.uint8)
+    proofs = np.empty(max(1, n * depth * 32), np.uint8)
+    d = lib().orc_merkle(_p(lv), n, _p(root), _p(proofs))
+    assert d == depth
+    pr = [[proofs[(i * depth + k) * 32:(i * depth + k + 1) * 32].tobytes() for k in range(depth)] for i in range(n)]
+    return root.tobytes(), pr
+
+
+def merkle_verify(leaf_index, leaf, proof, root):
+    """merkle_tree.rs:131-146"""
+    pf = np.ascontiguousarray(np.frombuffer(b"".join(proof) or b"\0", np.uint8))
+    lf = np.frombuffer(leaf, np.uint8).copy()
+    rt = np.frombuffer(root, np.uint8).copy()
+    return bool(lib().orc_merkle_verify(leaf_index, _p(lf), _p(pf), len(proof), _p(rt)))

@@ -94,6 +94,13 @@ int orc_rank_push(uint8_t *basis /* k*k, RREF rows */, uint8_t *pivots /* k */, 
 /* Gauss-Jordan inverse of a k x k matrix; returns 0 if invertible */
 int orc_matrix_inverse(const uint8_t *m, uint8_t *inv, size_t k, uint32_t poly);
 
+/* commitment layer (blake3_oracle.c): BLAKE3, Chunk::digest, MerkleTree root/proofs/verify */
+void orc_blake3(const uint8_t *in, size_t len, uint8_t out[32]);
+void orc_chunk_digest(uint64_t chunkset_id, uint64_t chunk_id, const uint8_t *data, size_t len, uint8_t out[32]);
+int orc_merkle(const uint8_t *leaves, size_t n, uint8_t root[32], uint8_t *proofs);
+int orc_merkle_verify(size_t leaf_index, const uint8_t leaf[32], const uint8_t *proof, size_t plen,
+                      const uint8_t root[32]);
+
 #ifdef __cplusplus
 }
 #endif

@@ -17,6 +17,7 @@ def main():
     ap.add_argument("--tag", default=os.path.basename(os.environ.get("DECDS_LIB", "default")))
     ap.add_argument("--pitch", type=int, default=0)
     ap.add_argument("--check", action="store_true")
+    ap.add_argument("--commit", action="store_true", help="also time decds_commit_batch (BLAKE3 + Merkle)")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -39,8 +40,12 @@ def main():
     verd = torch.empty(n * N, dtype=torch.int8, device="cuda")
     status = torch.empty(n, dtype=torch.int32, device="cuda")
     out = torch.empty(n * CS, dtype=torch.uint8, device="cuda")
+    if a.commit:
+        dig = torch.empty(n * N * 32, dtype=torch.uint8, device="cuda")
+        roots = torch.empty(n * 32, dtype=torch.uint8, device="cuda")
+        proofs = torch.empty(n * N * 128, dtype=torch.uint8, device="cuda")
     torch.cuda.synchronize()
-    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(a.reps + 3)]
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(5)] for _ in range(a.reps + 3)]
     for r in range(a.reps + 3):
         e = ev[r]
         e[0].record(st)
@@ -50,6 +55,9 @@ def main():
         e[2].record(st)
         codec.decode_batch(ctx, coded, n, plan, out, status, pitch, stream=st)
         e[3].record(st)
+        if a.commit:
+            codec.commit_batch(ctx, coded, n, dig, roots, proofs, pitch=pitch, stream=st)
+            e[4].record(st)
     torch.cuda.synchronize()
     t = np.array([[e[0].elapsed_time(e[1]), e[1].elapsed_time(e[2]), e[2].elapsed_time(e[3])] for e in ev[3:]])
     med = np.median(t, axis=0)
@@ -60,11 +68,24 @@ def main():
            "encode_GBps": round(n * (CS + N * F) / med[0] / 1e6, 1),
            "decode_GBps": round(nr * (K * F + CS) / med[2] / 1e6, 1),
            "encode_min_ms": round(t[:, 0].min(), 4), "decode_min_ms": round(t[:, 2].min(), 4)}
+    if a.commit:
+        tc = np.array([e[3].elapsed_time(e[4]) for e in ev[3:]])
+        res["commit_ms"] = round(float(np.median(tc)), 4)
+        res["commit_GBps"] = round(n * N * F / res["commit_ms"] / 1e6, 1)
     if a.check:
         good = True
         for c in np.nonzero(s == 0)[0].tolist():
             good &= bool(torch.equal(out[c * CS:(c + 1) * CS], src[c * CS:(c + 1) * CS]))
         res["roundtrip_ok"] = good
+        if a.commit:  # spot-check digests of a few rows against the CPU restatement
+            sys.path.insert(0, os.path.join(ROOT, "oracle"))
+            import oracle as o
+            d = dig.cpu().numpy()
+            ok = True
+            for row in sorted({0, 1, 17, n * N - 1}):
+                piece = coded[row * pitch:row * pitch + F].cpu().numpy()
+                ok &= d[row * 32:(row + 1) * 32].tobytes() == o.chunk_digest(row // N, row, piece)
+            res["digest_ok"] = ok
     print(json.dumps(res), flush=True)
 
 
