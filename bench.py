@@ -42,6 +42,7 @@ def parse():
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--config", default="cfg2", choices=sorted(CONFIGS))
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-commit", action="store_true", help="skip timing the commitment kernels (row f1)")
     p.add_argument("--cpu-sample", type=int, default=0, help="chunksets in the CPU sample (0 = auto)")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
     return p.parse_args()
@@ -164,6 +165,25 @@ def main():
         assert torch.equal(out[c * CS:(c + 1) * CS], src[c * CS:(c + 1) * CS]), "repaired chunkset %d differs" % c
     n_ready = int((st == 0).sum())
 
+    # the next row, timed beside the headline step, never inside it: ChunkSet::new's
+    # commitment (BLAKE3 of every coded row + 16-leaf Merkle trees/proofs) over the same coded rows
+    commit = None
+    if not args.no_commit:
+        dig = torch.empty(n * N * 32, dtype=torch.uint8, device=dev)
+        roots = torch.empty(n * 32, dtype=torch.uint8, device=dev)
+        proofs = torch.empty(n * N * 128, dtype=torch.uint8, device=dev)
+        codec.commit_batch(ctx, coded, n, dig, roots, proofs, first_chunkset_id=lo, stream=stream)
+        cev = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
+        cev[0].record(stream)
+        for s in range(args.steps):
+            codec.commit_batch(ctx, coded, n, dig, roots, proofs, first_chunkset_id=lo, stream=stream)
+            cev[s + 1].record(stream)
+        stream.synchronize()
+        c_ms = cev[0].elapsed_time(cev[-1]) / args.steps
+        commit = {"kernels": "chunk_digest_kernel + chunkset_merkle_kernel", "ms": round(c_ms, 4),
+                  "coded_GBps": round(n * N * F / (c_ms * 1e-3) / 1e9, 1),
+                  "blob_GiBps": round(n * CS / GIB / (c_ms * 1e-3), 1), "bound": "valu (BLAKE3 rotates)"}
+
     enc_bytes = n * (CS + N * F)            # algorithmic HBM bytes of one encode launch
     dec_bytes = n_ready * (K * F + CS)      # ... of one decode launch (ready chunksets only)
     enc_gbs = enc_bytes / (enc_ms * 1e-3) / 1e9
@@ -198,6 +218,7 @@ def main():
                           "encode_blob_GiBps": round(n * CS / GIB / (enc_ms * 1e-3), 1),
                           "repair_blob_GiBps": round(n * CS / GIB / ((plan_ms + dec_ms) * 1e-3), 1),
                           "ready_chunksets": n_ready, "not_ready_chunksets": n - n_ready},
+            "commitment": commit,
         }
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args.cpu_sample, 0xDEC05002)

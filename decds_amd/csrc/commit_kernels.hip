@@ -20,6 +20,9 @@ constexpr uint32_t FULL_CHUNKS = MSG_BYTES / b3::CHUNK;            // 1024
 constexpr uint32_t LAST_BYTES = MSG_BYTES - FULL_CHUNKS * b3::CHUNK;  // 27
 static_assert(FULL_CHUNKS == 1024 && LAST_BYTES == 27, "BLAKE3 tree shape of a coded chunk message");
 
+#ifndef DECDS_DG_PREFETCH
+#define DECDS_DG_PREFETCH 1  // 1: block b+1's loads issued before block b's compression
+#endif
 constexpr uint32_t CPT = 4;                       // consecutive BLAKE3 chunks per thread
 constexpr uint32_t DG_WG = FULL_CHUNKS / CPT;     // 256 threads per row
 
@@ -76,12 +79,23 @@ __device__ __forceinline__ void chunk_cv(const uint8_t *piece, const uint8_t *ab
                                          uint64_t cs_id, uint64_t chunk_id, uint32_t cv[8]) {
 #pragma unroll
     for (int i = 0; i < 8; i++) cv[i] = b3::K3.iv[i];
+#if DECDS_DG_PREFETCH
+    Block m = load_block<Q>(piece, abase, r, c, 0, cs_id, chunk_id);
+#pragma unroll 1
+    for (uint32_t b = 0; b < 16; b++) {
+        const Block nxt = load_block<Q>(piece, abase, r, c, b < 15 ? b + 1 : b, cs_id, chunk_id);
+        const uint32_t flags = (b == 0 ? b3::CHUNK_START : 0u) | (b == 15 ? b3::CHUNK_END : 0u);
+        b3::compress(cv, m.w, c, b3::BLOCK, flags, cv);
+        m = nxt;
+    }
+#else
 #pragma unroll 1
     for (uint32_t b = 0; b < 16; b++) {
         const Block m = load_block<Q>(piece, abase, r, c, b, cs_id, chunk_id);
         const uint32_t flags = (b == 0 ? b3::CHUNK_START : 0u) | (b == 15 ? b3::CHUNK_END : 0u);
         b3::compress(cv, m.w, c, b3::BLOCK, flags, cv);
     }
+#endif
 }
 
 // thread t: chunks 4t..4t+3 folded into the chaining value of their 4-chunk subtree (all lanes busy)
