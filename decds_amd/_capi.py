@@ -34,6 +34,7 @@ STATUS_NAMES = {
     8: "EmptyDataForBlob",
     9: "InvalidChunksetId",
     10: "ChunksetAlreadyRepaired",
+    11: "InvalidProofInChunk",
     -1: "HipError",
     -2: "InvalidArgument",
     -3: "NoDevice",
@@ -78,7 +79,11 @@ def _declare(L):
         "decds_chunkset_get_chunk": (c.c_int, [P, SZ, VP, SZ, c.POINTER(SZ)]),
         "decds_chunkset_id": (SZ, [P]),
         "decds_chunkset_free": (None, [P]),
-        "decds_repairing_chunkset_new": (c.c_int, [P, SZ, c.POINTER(c.c_void_p)]),
+        "decds_chunkset_get_root_commitment": (c.c_int, [P, VP]),
+        "decds_chunkset_get_chunk_proof": (c.c_int, [P, SZ, VP, SZ, c.POINTER(SZ)]),
+        "decds_chunkset_append_blob_inclusion_proof": (c.c_int, [P, VP, SZ]),
+        "decds_repairing_chunkset_new": (c.c_int, [P, SZ, VP, c.POINTER(c.c_void_p)]),
+        "decds_repairing_chunkset_add_chunk": (c.c_int, [P, SZ, SZ, VP, SZ, VP, SZ]),
         "decds_repairing_chunkset_add_chunk_unvalidated": (c.c_int, [P, SZ, VP, SZ]),
         "decds_repairing_chunkset_is_ready_to_repair": (c.c_int, [P]),
         "decds_repairing_chunkset_repair": (c.c_int, [P, VP, SZ]),
@@ -88,6 +93,8 @@ def _declare(L):
         "decds_host_register": (c.c_int, [VP, SZ]),
         "decds_commit_batch": (c.c_int, [P, VP, SZ, SZ, c.c_uint64, VP, VP, VP, VP]),
         "decds_blake3": (None, [VP, SZ, VP]),
+        "decds_chunk_digest": (None, [c.c_uint64, c.c_uint64, VP, SZ, VP]),
+        "decds_validate_batch": (c.c_int, [P, VP, SZ, SZ, VP, VP, SZ, VP, SZ, VP, VP, VP, VP]),
         "decds_merkle_tree": (c.c_int, [VP, SZ, VP, VP]),
         "decds_merkle_verify": (c.c_int, [SZ, VP, VP, SZ, VP]),
         "decds_host_unregister": (c.c_int, [VP]),
@@ -108,7 +115,9 @@ EXPORTED = [
     "decds_repairing_chunkset_is_ready_to_repair", "decds_repairing_chunkset_repair",
     "decds_repairing_chunkset_free", "decds_blob_encode_host", "decds_blob_repair_host",
     "decds_host_register", "decds_host_unregister", "decds_commit_batch", "decds_blake3",
-    "decds_merkle_tree", "decds_merkle_verify",
+    "decds_merkle_tree", "decds_merkle_verify", "decds_chunk_digest", "decds_validate_batch",
+    "decds_chunkset_get_root_commitment", "decds_chunkset_get_chunk_proof",
+    "decds_chunkset_append_blob_inclusion_proof", "decds_repairing_chunkset_add_chunk",
 ]
 
 

@@ -76,6 +76,23 @@ def commit_batch(ctx, coded, n, digests, roots, proofs, first_chunkset_id=0, pit
                                    _ptr(proofs), _stream(stream)))
 
 
+def validate_batch(ctx, coded, n_rows, ids, proofs, proof_len, chunkset_roots, num_chunksets, digests, valid,
+                   blob_root=None, pitch=CODED_PIECE_BYTES, stream=None):
+    """BlobHeader::validate_chunk (blob.rs:211-215) for n_rows received device-resident rows.
+    ids: int64/uint64 tensor (n_rows, 2) = (chunkset_id, global chunk_id); proofs: n_rows x proof_len
+    x 32 bytes; chunkset_roots: num_chunksets x 32; blob_root: 32-byte device tensor or None."""
+    _need(coded, (n_rows - 1) * pitch + CODED_PIECE_BYTES if n_rows else 0, "coded")
+    _need(ids, n_rows * 16, "ids")
+    _need(proofs, n_rows * proof_len * 32, "proofs")
+    _need(chunkset_roots, num_chunksets * 32, "chunkset_roots")
+    _need(digests, n_rows * 32, "digests")
+    _need(valid, n_rows, "valid")
+    check(lib().decds_validate_batch(ctx.handle, _ptr(coded), pitch, n_rows, _ptr(ids), _ptr(proofs), proof_len,
+                                     _ptr(chunkset_roots), num_chunksets,
+                                     None if blob_root is None else _ptr(blob_root), _ptr(digests), _ptr(valid),
+                                     _stream(stream)))
+
+
 def fill_random_device(ctx, seed, dst, nbytes=None, byte_offset=0, stream=None):
     nbytes = dst.numel() * dst.element_size() if nbytes is None else nbytes
     check(lib().decds_fill_random_device(ctx.handle, seed, byte_offset, _ptr(dst), nbytes, _stream(stream)))

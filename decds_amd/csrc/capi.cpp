@@ -54,6 +54,7 @@ const char *decds_status_string(int s) {
         case DECDS_ERR_EMPTY_DATA_FOR_BLOB: return "empty data for blob";
         case DECDS_ERR_INVALID_CHUNKSET_ID: return "invalid chunkset id";
         case DECDS_ERR_CHUNKSET_ALREADY_REPAIRED: return "chunkset already repaired";
+        case DECDS_ERR_INVALID_PROOF_IN_CHUNK: return "invalid proof in chunk";
         case DECDS_ERR_HIP: return "HIP runtime error";
         case DECDS_ERR_INVALID_ARGUMENT: return "invalid argument";
         case DECDS_ERR_NO_DEVICE: return "no gfx950 device";

@@ -1,6 +1,7 @@
 // chunkset.cpp — host-side mirror of decds-lib's chunkset API (chunkset.rs) and of the blob-level
 // chunkset iteration (blob.rs) over the gfx950 batch kernels. Same names, argument meaning and
-// error behaviour as the reference; the Merkle/BLAKE3 commitment layer is out of scope.
+// error behaviour as the reference, including ChunkSet::new's commitment (digests, Merkle root,
+// proofs: computed on the device by decds_commit_batch) and RepairingChunkSet::add_chunk's proof check.
 //
 //   decds_chunkset_new                 ChunkSet::new                    chunkset.rs:37-69
 //   decds_chunkset_get_chunk           ChunkSet::get_chunk              chunkset.rs:87-89
@@ -45,12 +46,17 @@ std::mt19937_64 &rng() {
 
 struct decds_chunkset {
     size_t id;
-    std::vector<uint8_t> coded;  // 16 x F, rlnc full coded pieces
+    std::vector<uint8_t> coded;   // 16 x F, rlnc full coded pieces
+    uint8_t root[32];             // MerkleTree root of the 16 chunk digests (chunkset.rs:57)
+    uint8_t proofs[N][PROOF_SIZE][32];
+    std::vector<uint8_t> blob_proof;  // appended to every chunk's proof (chunkset.rs:98-102)
 };
 
 struct decds_repairing_chunkset {
     decds_ctx *ctx;
     size_t id;
+    bool has_commitment;
+    uint8_t commitment[32];
     uint8_t basis[K * K];
     uint8_t pivots[K];
     uint32_t rank;
@@ -76,14 +82,21 @@ int decds_chunkset_new(decds_ctx *ctx, size_t chunkset_id, const uint8_t *data, 
         std::lock_guard<std::mutex> g(g_rng_mu);
         for (auto &b : cv) b = (uint8_t)rng()();
     }
-    DevBuf dsrc, dcv, ddst;
+    DevBuf dsrc, dcv, ddst, dcommit;
+    constexpr size_t DIG = N * 32, ROOT = 32, PRF = N * PROOF_SIZE * 32;
     hipError_t e;
-    if ((e = dsrc.alloc(CS)) || (e = dcv.alloc(sizeof cv)) || (e = ddst.alloc(N * F))) return decds_hip_error(e, "hipMalloc");
+    if ((e = dsrc.alloc(CS)) || (e = dcv.alloc(sizeof cv)) || (e = ddst.alloc(N * F)) || (e = dcommit.alloc(DIG + ROOT + PRF)))
+        return decds_hip_error(e, "hipMalloc");
     if ((e = hipMemcpy(dsrc.p, data, CS, hipMemcpyHostToDevice)) || (e = hipMemcpy(dcv.p, cv, sizeof cv, hipMemcpyHostToDevice)))
         return decds_hip_error(e, "hipMemcpy H2D");
     if ((s = decds_encode_batch(ctx, dsrc.p, 1, dcv.p, ddst.p, F, nullptr))) return s;
-    auto *c = new decds_chunkset{chunkset_id, std::vector<uint8_t>(N * F)};
-    if ((e = hipMemcpy(c->coded.data(), ddst.p, N * F, hipMemcpyDeviceToHost))) {
+    // chunkset.rs:54-63: chunk digests -> 16-leaf Merkle tree -> root + one proof per chunk
+    if ((s = decds_commit_batch(ctx, ddst.p, F, 1, chunkset_id, dcommit.p, dcommit.p + DIG, dcommit.p + DIG + ROOT, nullptr)))
+        return s;
+    auto *c = new decds_chunkset{chunkset_id, std::vector<uint8_t>(N * F), {}, {}, {}};
+    if ((e = hipMemcpy(c->coded.data(), ddst.p, N * F, hipMemcpyDeviceToHost)) ||
+        (e = hipMemcpy(c->root, dcommit.p + DIG, ROOT, hipMemcpyDeviceToHost)) ||
+        (e = hipMemcpy(c->proofs, dcommit.p + DIG + ROOT, PRF, hipMemcpyDeviceToHost))) {
         delete c;
         return decds_hip_error(e, "hipMemcpy D2H");
     }
@@ -104,14 +117,44 @@ int decds_chunkset_get_chunk(const decds_chunkset *cs, size_t chunk_id, uint8_t 
     return DECDS_OK;
 }
 
+int decds_chunkset_get_root_commitment(const decds_chunkset *cs, uint8_t out[32]) {
+    if (!cs || !out) return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "null argument");
+    std::memcpy(out, cs->root, 32);
+    return DECDS_OK;
+}
+
+int decds_chunkset_get_chunk_proof(const decds_chunkset *cs, size_t chunk_id, uint8_t *out, size_t out_len,
+                                   size_t *proof_len) {
+    if (!cs) return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "null chunkset");
+    if (chunk_id >= N) return decds_set_error(DECDS_ERR_INVALID_SHARE_ID, "invalid erasure coded share id: %zu (num_shares: %u)",
+                                              chunk_id, N);
+    const size_t hashes = PROOF_SIZE + cs->blob_proof.size() / 32;
+    if (proof_len) *proof_len = hashes;
+    if (out) {
+        if (out_len < hashes * 32) return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "out buffer < %zu", hashes * 32);
+        std::memcpy(out, cs->proofs[chunk_id], PROOF_SIZE * 32);
+        if (!cs->blob_proof.empty()) std::memcpy(out + PROOF_SIZE * 32, cs->blob_proof.data(), cs->blob_proof.size());
+    }
+    return DECDS_OK;
+}
+
+int decds_chunkset_append_blob_inclusion_proof(decds_chunkset *cs, const uint8_t *blob_proof, size_t len) {
+    if (!cs || (len && !blob_proof)) return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "null argument");
+    cs->blob_proof.insert(cs->blob_proof.end(), blob_proof, blob_proof + len * 32);  // empty: no-op (chunkset.rs:99)
+    return DECDS_OK;
+}
+
 size_t decds_chunkset_id(const decds_chunkset *cs) { return cs ? cs->id : 0; }
 void decds_chunkset_free(decds_chunkset *cs) { delete cs; }
 
-int decds_repairing_chunkset_new(decds_ctx *ctx, size_t chunkset_id, decds_repairing_chunkset **out) {
+int decds_repairing_chunkset_new(decds_ctx *ctx, size_t chunkset_id, const uint8_t *commitment,
+                                 decds_repairing_chunkset **out) {
     if (!ctx || !out) return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "null argument");
     auto *r = new decds_repairing_chunkset;
     r->ctx = ctx;
     r->id = chunkset_id;
+    r->has_commitment = commitment != nullptr;
+    if (commitment) std::memcpy(r->commitment, commitment, 32);
     std::memset(r->basis, 0, sizeof r->basis);
     std::memset(r->pivots, 0, sizeof r->pivots);
     r->rank = 0;
@@ -140,6 +183,21 @@ int decds_repairing_chunkset_add_chunk_unvalidated(decds_repairing_chunkset *r, 
                                chunk_chunkset_id);
     r->rows.insert(r->rows.end(), data, data + F);
     return DECDS_OK;
+}
+
+int decds_repairing_chunkset_add_chunk(decds_repairing_chunkset *r, size_t chunk_chunkset_id, size_t chunk_id,
+                                       const uint8_t *data, size_t len, const uint8_t *proof, size_t proof_len) {
+    if (!r) return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "null repairing chunkset");
+    if (!r->has_commitment) return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "repairing chunkset has no commitment");
+    // chunkset.rs:152 -> chunk.rs:103-110: leaf chunk_id % 16, first PROOF_SIZE hashes
+    bool ok = proof && proof_len >= PROOF_SIZE && (data || len == 0);
+    if (ok) {
+        uint8_t leaf[32];
+        decds_chunk_digest(chunk_chunkset_id, chunk_id, data, len, leaf);
+        ok = decds_merkle_verify(chunk_id % N, leaf, proof, PROOF_SIZE, r->commitment) == 1;
+    }
+    if (!ok) return decds_set_error(DECDS_ERR_INVALID_PROOF_IN_CHUNK, "invalid proof in chunk of chunkset %zu", chunk_chunkset_id);
+    return decds_repairing_chunkset_add_chunk_unvalidated(r, chunk_chunkset_id, data, len);
 }
 
 int decds_repairing_chunkset_is_ready_to_repair(const decds_repairing_chunkset *r) {

@@ -76,6 +76,16 @@ void decds_blake3(const uint8_t *data, size_t len, uint8_t out[32]) {
     to_bytes(cv, out);
 }
 
+void decds_chunk_digest(uint64_t chunkset_id, uint64_t chunk_id, const uint8_t *data, size_t len, uint8_t out[32]) {
+    std::vector<uint8_t> msg(16 + len);
+    for (int b = 0; b < 8; b++) {
+        msg[b] = (uint8_t)(chunkset_id >> (8 * b));
+        msg[8 + b] = (uint8_t)(chunk_id >> (8 * b));
+    }
+    if (len) std::memcpy(msg.data() + 16, data, len);
+    decds_blake3(msg.data(), msg.size(), out);
+}
+
 int decds_merkle_tree(const uint8_t *leaves, size_t n, uint8_t root[32], uint8_t *proofs) {
     if (!leaves || !root || n == 0)
         return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "no leaf nodes to build merkle tree on");
@@ -129,6 +139,21 @@ int decds_commit_batch(decds_ctx *ctx, const uint8_t *coded, size_t pitch, size_
     if (pitch < F) return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "coded pitch %zu < %llu", pitch, (unsigned long long)F);
     hipError_t e = launch_commit(coded, pitch, n, first_chunkset_id, digests, roots, proofs, (hipStream_t)stream);
     return e == hipSuccess ? DECDS_OK : decds_hip_error(e, "commit kernels launch");
+}
+
+int decds_validate_batch(decds_ctx *ctx, const uint8_t *coded, size_t pitch, size_t n_rows, const uint64_t *ids,
+                         const uint8_t *proofs, size_t proof_len, const uint8_t *chunkset_roots,
+                         size_t num_chunksets, const uint8_t *blob_root, uint8_t *digests, uint8_t *valid,
+                         void *stream) {
+    int s = decds_ctx_bind(ctx);
+    if (s) return s;
+    if (!coded || !ids || !digests || !valid || (proof_len && !proofs) || (num_chunksets && !chunkset_roots))
+        return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "null buffer");
+    if (pitch < F) return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "coded pitch %zu < %llu", pitch, (unsigned long long)F);
+    if (n_rows > (1u << 30)) return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "row count %zu too large", n_rows);
+    hipError_t e = launch_validate(coded, pitch, n_rows, ids, proofs, proof_len, chunkset_roots, num_chunksets, blob_root,
+                                   digests, valid, (hipStream_t)stream);
+    return e == hipSuccess ? DECDS_OK : decds_hip_error(e, "validate kernels launch");
 }
 
 }  // extern "C"

@@ -118,13 +118,16 @@ __device__ __forceinline__ void subtree4_cv(const uint8_t *piece, uint32_t t, ui
 // Digest of one coded row per 256-thread workgroup: 4-chunk subtrees in registers, the 256
 // subtree values folded in LDS (8 PARENT levels), then thread 0 adds the 27-byte 1025th chunk under
 // the ROOT parent.
+// ids == NULL: row = c*16 + j of a freshly encoded batch, chunkset_id = first + c and chunk_id =
+// chunkset_id*16 + j (chunkset.rs:47); else the row's claimed (chunkset_id, chunk_id) = ids[2row..].
 __global__ __launch_bounds__(DG_WG) void chunk_digest_kernel(const uint8_t *__restrict__ coded, size_t pitch,
                                                              uint64_t first_chunkset_id,
+                                                             const uint64_t *__restrict__ ids,
                                                              uint8_t *__restrict__ digests) {
     __shared__ uint32_t cvs[DG_WG][8];
-    const uint32_t row = blockIdx.x;                 // c*16 + j
-    const uint64_t cs_id = first_chunkset_id + row / N;
-    const uint64_t chunk_id = cs_id * N + row % N;   // chunkset.rs:47
+    const uint32_t row = blockIdx.x;
+    const uint64_t cs_id = ids ? ids[2 * (size_t)row] : first_chunkset_id + row / N;
+    const uint64_t chunk_id = ids ? ids[2 * (size_t)row + 1] : cs_id * N + row % N;
     const uint8_t *piece = coded + (size_t)row * pitch;
     const uint32_t t = threadIdx.x;
     uint32_t acc[8];
@@ -208,15 +211,78 @@ __global__ __launch_bounds__(MK_WG) void chunkset_merkle_kernel(const uint8_t *_
     }
 }
 
+// BlobHeader::validate_chunk (blob.rs:211-215) per received row, one lane per row:
+// MerkleTree::verify_proof (merkle_tree.rs:131-146) = fold the proof from the leaf upwards,
+// sibling on the right when the index bit is 0, compare with the root.
+__device__ __forceinline__ bool verify_path(uint64_t index, const uint32_t leaf[8], const uint8_t *proof, size_t len,
+                                            const uint8_t *root) {
+    uint32_t h[8];
+#pragma unroll
+    for (int w = 0; w < 8; w++) h[w] = leaf[w];
+    for (size_t k = 0; k < len; k++) {
+        uint32_t sib[8], t[8];
+        const uint32_t *ps = reinterpret_cast<const uint32_t *>(proof + 32 * k);
+#pragma unroll
+        for (int w = 0; w < 8; w++) sib[w] = ps[w];
+        if ((index & 1) == 0)
+            b3::hash64(h, sib, t);
+        else
+            b3::hash64(sib, h, t);
+#pragma unroll
+        for (int w = 0; w < 8; w++) h[w] = t[w];
+        index >>= 1;
+    }
+    const uint32_t *r = reinterpret_cast<const uint32_t *>(root);
+    bool eq = true;
+#pragma unroll
+    for (int w = 0; w < 8; w++) eq &= h[w] == r[w];
+    return eq;
+}
+
+__global__ __launch_bounds__(64) void validate_kernel(const uint8_t *__restrict__ digests, size_t n_rows,
+                                                      const uint64_t *__restrict__ ids,
+                                                      const uint8_t *__restrict__ proofs, size_t proof_len,
+                                                      const uint8_t *__restrict__ chunkset_roots,
+                                                      size_t num_chunksets, const uint8_t *__restrict__ blob_root,
+                                                      uint8_t *__restrict__ valid) {
+    const size_t r = (size_t)blockIdx.x * 64 + threadIdx.x;
+    if (r >= n_rows) return;
+    const uint64_t cs_id = ids[2 * r], chunk_id = ids[2 * r + 1];
+    uint32_t leaf[8];
+    const uint32_t *d = reinterpret_cast<const uint32_t *>(digests + r * 32);
+#pragma unroll
+    for (int w = 0; w < 8; w++) leaf[w] = d[w];
+    const uint8_t *proof = proofs + r * proof_len * 32;
+    bool ok = proof_len >= PROOF_SIZE;
+    if (ok && blob_root) ok = verify_path(chunk_id, leaf, proof, proof_len, blob_root);       // chunk.rs:88-90
+    if (ok) ok = cs_id < num_chunksets;                                                        // blob.rs:213
+    if (ok) ok = verify_path(chunk_id % N, leaf, proof, PROOF_SIZE, chunkset_roots + cs_id * 32);  // chunk.rs:103-110
+    valid[r] = ok ? 1 : 0;
+}
+
 hipError_t launch_commit(const uint8_t *coded, size_t pitch, size_t n, uint64_t first_chunkset_id, uint8_t *digests,
                          uint8_t *roots, uint8_t *proofs, hipStream_t stream) {
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(chunk_digest_kernel, dim3((uint32_t)(n * N)), dim3(DG_WG), 0, stream, coded, pitch,
-                       first_chunkset_id, digests);
+                       first_chunkset_id, (const uint64_t *)nullptr, digests);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(chunkset_merkle_kernel, dim3((uint32_t)((n * N + MK_WG - 1) / MK_WG)), dim3(MK_WG), 0, stream,
                        digests, n, roots, proofs);
+    return hipGetLastError();
+}
+
+hipError_t launch_validate(const uint8_t *coded, size_t pitch, size_t n_rows, const uint64_t *ids,
+                           const uint8_t *proofs, size_t proof_len, const uint8_t *chunkset_roots,
+                           size_t num_chunksets, const uint8_t *blob_root, uint8_t *digests, uint8_t *valid,
+                           hipStream_t stream) {
+    if (n_rows == 0) return hipSuccess;
+    hipLaunchKernelGGL(chunk_digest_kernel, dim3((uint32_t)n_rows), dim3(DG_WG), 0, stream, coded, pitch, (uint64_t)0,
+                       ids, digests);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(validate_kernel, dim3((uint32_t)((n_rows + 63) / 64)), dim3(64), 0, stream, digests, n_rows,
+                       ids, proofs, proof_len, chunkset_roots, num_chunksets, blob_root, valid);
     return hipGetLastError();
 }
 

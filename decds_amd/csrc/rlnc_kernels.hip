@@ -431,11 +431,27 @@ void rlnc_decode_kernel(const uint8_t *__restrict__ coded, size_t pitch, size_t 
     }
 }
 
+// x * f for a per-lane x and a wave-uniform f: the branches test bits of f, so they are scalar
+__device__ __forceinline__ uint32_t gf_mul_uniform(uint32_t x, uint32_t f, uint32_t poly) {
+    uint32_t acc = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        if (f & (1u << i)) acc ^= x;
+        x = (x << 1) ^ ((x & 0x80u) ? poly : 0u);
+    }
+    return acc & 0xFFu;
+}
+
 // One wave per chunkset. Replays rlnc's incremental rank test over the candidates' 10-byte coding
 // vectors in arrival order (chunkset.rs:173-184: a piece is accepted iff it raises the rank;
-// after rank 10 every further piece is "ready to repair"), then inverts the accepted vectors by
-// Gauss-Jordan. Lane c holds column c (c < 10 for the rank test, c < 20 for the augmented inverse);
-// pivots and multipliers are wave-uniform values read with v_readlane.
+// after rank 10 every further piece is "ready to repair") and, in the same pass, inverts the
+// accepted vectors. Each basis row is augmented: lanes 0..9 hold its coefficient part (kept in
+// reduced row-echelon form), lanes 10..19 the combination of accepted raw vectors it equals (the
+// k-th accepted vector enters as unit vector k). Because the coefficient part is RREF, the factors
+// that reduce a new row against the basis are the new row's own entries at the basis pivots, so
+// all reductions of one step are independent (ILP across the basis instead of a serial chain).
+// At rank 10 the coefficient parts are unit vectors e_piv, so B = E·R = P and R^-1 = Pᵀ·E: row i
+// of the inverse is the combination part of the basis row whose pivot is column i.
 __global__ __launch_bounds__(64) void rlnc_plan_kernel(const uint8_t *__restrict__ coded, size_t pitch, size_t n,
                                                        const uint8_t *__restrict__ cand,
                                                        RepairPlan *__restrict__ plan,
@@ -458,10 +474,9 @@ __global__ __launch_bounds__(64) void rlnc_plan_kernel(const uint8_t *__restrict
         cvs[a] = (col && r < N) ? coded[(cs * N + r) * pitch + lane] : 0u;
     }
     __syncthreads();
-    uint32_t basis[K], raw[K];
-    uint32_t piv[K], sel[K];
+    uint32_t basis[K], piv[K], sel[K];
 #pragma unroll
-    for (int e = 0; e < (int)K; e++) basis[e] = raw[e] = piv[e] = sel[e] = 0;
+    for (int e = 0; e < (int)K; e++) basis[e] = piv[e] = sel[e] = 0;
     uint32_t rank = 0;
     bool ended = false;
     int32_t my_verdict = -1;  // lane a < 16 keeps candidate a's verdict
@@ -476,33 +491,35 @@ __global__ __launch_bounds__(64) void rlnc_plan_kernel(const uint8_t *__restrict
             v = 3;  // DECDS_ERR_CHUNKSET_READY_TO_REPAIR
         } else {
             const uint32_t cv = cvs[a];
-            uint32_t row = cv;
+            // augmented row [cv | unit(rank)]
+            uint32_t row = col ? cv : (lane == K + rank ? 1u : 0u);
+            uint32_t red = 0;
 #pragma unroll
             for (int e = 0; e < (int)K; e++) {
                 if (e < (int)rank) {
-                    const uint32_t f = __builtin_amdgcn_readlane(row, piv[e]);
-                    if (f) row ^= gf_mul(f, basis[e], poly);
+                    const uint32_t f = __builtin_amdgcn_readlane(cv, piv[e]);
+                    red ^= gf_mul_uniform(basis[e], f, poly);
                 }
             }
+            row ^= red;
             const uint64_t nz = __ballot(col && row != 0);
             if (!nz) {
                 v = 4;  // DECDS_ERR_CHUNK_DECODING_FAILED: piece not useful
             } else {
                 const uint32_t p = __builtin_ctzll(nz);
                 const uint32_t inv = inv_tab[__builtin_amdgcn_readlane(row, p)];
-                row = gf_mul(row, inv, poly);
+                row = gf_mul_uniform(row, inv, poly);
 #pragma unroll
                 for (int e = 0; e < (int)K; e++) {
                     if (e < (int)rank) {
                         const uint32_t f = __builtin_amdgcn_readlane(basis[e], p);
-                        if (f) basis[e] ^= gf_mul(f, row, poly);
+                        basis[e] ^= gf_mul_uniform(row, f, poly);
                     }
                 }
 #pragma unroll
                 for (int e = 0; e < (int)K; e++) {
                     if (e == (int)rank) {
                         basis[e] = row;
-                        raw[e] = cv;
                         piv[e] = p;
                         sel[e] = r;
                     }
@@ -520,36 +537,10 @@ __global__ __launch_bounds__(64) void rlnc_plan_kernel(const uint8_t *__restrict
         if (lane == 0) status[cs] = 5;  // DECDS_ERR_CHUNKSET_NOT_YET_READY
         return;
     }
-    // augmented [raw | I]: lane c < 10 holds column c of raw, lane 10 + c column c of I
-    uint32_t m[K];
-#pragma unroll
-    for (int i = 0; i < (int)K; i++) m[i] = lane < K ? raw[i] : (lane - K == (uint32_t)i ? 1u : 0u);
-#pragma unroll
-    for (int c = 0; c < (int)K; c++) {
-        uint32_t p = K;
-#pragma unroll
-        for (int i = (int)K - 1; i >= c; i--)
-            if (__builtin_amdgcn_readlane(m[i], c)) p = i;  // full rank: a pivot exists
-#pragma unroll
-        for (int i = c + 1; i < (int)K; i++)
-            if ((uint32_t)i == p) {
-                const uint32_t t = m[c];
-                m[c] = m[i];
-                m[i] = t;
-            }
-        const uint32_t inv = inv_tab[__builtin_amdgcn_readlane(m[c], c)];
-        m[c] = gf_mul(m[c], inv, poly);
-#pragma unroll
-        for (int i = 0; i < (int)K; i++) {
-            if (i == c) continue;
-            const uint32_t f = __builtin_amdgcn_readlane(m[i], c);
-            if (f) m[i] ^= gf_mul(f, m[c], poly);
-        }
-    }
-    // inverse = right half: pl->inv[i][j] = m[i] of lane 10 + j
+    // inverse row piv[e] = combination part of basis row e: lane 10 + k writes inv[piv[e]][k]
     if (lane >= K && lane < 2 * K) {
 #pragma unroll
-        for (int i = 0; i < (int)K; i++) pl->inv[i * K + (lane - K)] = (uint8_t)m[i];
+        for (int e = 0; e < (int)K; e++) pl->inv[piv[e] * K + (lane - K)] = (uint8_t)basis[e];
     }
     if (lane == 0) {
 #pragma unroll

@@ -11,6 +11,7 @@ constexpr uint32_t N = 16;                   // NUM_ERASURE_CODED_CHUNKS = DECDS
 constexpr uint64_t CS = 10ull * (1ull << 20);  // ChunkSet::BYTE_LENGTH (chunkset.rs:20, chunk.rs:14)
 constexpr uint64_t L = (CS + 1 + K - 1) / K;   // PADDED_CHUNK_BYTE_LEN (chunkset.rs:117) = 1,048,577
 constexpr uint64_t F = L + K;                  // full coded piece: coding vector || payload
+constexpr uint32_t PROOF_SIZE = 4;           // ChunkSet::PROOF_SIZE = log2(16) chunkset-level proof hashes (chunkset.rs:22)
 static_assert(L == 1048577ull, "piece length pinned by chunkset.rs:117");
 
 constexpr uint32_t POLY_DEFAULT = 0x11D;     // rlnc 0.4.0 GF(2^8) polynomial [recalled, run-time parameter]

@@ -49,6 +49,7 @@ extern "C" {
 #define DECDS_ERR_EMPTY_DATA_FOR_BLOB 8            /* EmptyDataForBlob                errors.rs:6  */
 #define DECDS_ERR_INVALID_CHUNKSET_ID 9            /* InvalidChunksetId(id, n)        errors.rs:34 */
 #define DECDS_ERR_CHUNKSET_ALREADY_REPAIRED 10     /* ChunksetAlreadyRepaired(id)     errors.rs:27 */
+#define DECDS_ERR_INVALID_PROOF_IN_CHUNK 11        /* InvalidProofInChunk(id)         errors.rs:40 */
 #define DECDS_ERR_HIP (-1)                         /* HIP runtime failure (text: decds_last_error) */
 #define DECDS_ERR_INVALID_ARGUMENT (-2)
 #define DECDS_ERR_NO_DEVICE (-3)
@@ -115,12 +116,21 @@ int decds_rank_push(uint8_t *basis, uint8_t *pivots, uint32_t *rank, const uint8
 
 /* ---- chunkset-level mirror (decds-lib/src/chunkset.rs), host buffers ----------------------- */
 typedef struct decds_chunkset decds_chunkset;
-/* ChunkSet::new(chunkset_id, data) (chunkset.rs:37-69, minus the BLAKE3/Merkle commitment which
- * is out of scope): len != 10 MiB -> DECDS_ERR_INVALID_CHUNKSET_SIZE. coeffs: 16 x 10 coding
- * vectors, or NULL to draw them from the library's RNG (the reference draws from rand::rng(),
- * chunkset.rs:42). */
+/* ChunkSet::new(chunkset_id, data) (chunkset.rs:37-69): RLNC encode + the commitment (16 chunk
+ * digests, Merkle root, 16 proofs) on the device. len != 10 MiB -> DECDS_ERR_INVALID_CHUNKSET_SIZE.
+ * coeffs: 16 x 10 coding vectors, or NULL to draw them from the library's RNG (the reference
+ * draws from rand::rng(), chunkset.rs:42). */
 int decds_chunkset_new(decds_ctx *ctx, size_t chunkset_id, const uint8_t *data, size_t len,
                        const uint8_t *coeffs, decds_chunkset **out);
+/* ChunkSet::get_root_commitment (chunkset.rs:72-74): 32-byte Merkle root of the 16 chunk digests */
+int decds_chunkset_get_root_commitment(const decds_chunkset *cs, uint8_t out[32]);
+/* the proof carried by ProofCarryingChunk `chunk_id` (chunkset.rs:59-63, 98-102): 4 chunkset-level
+ * hashes, then the blob-level hashes appended by decds_chunkset_append_blob_inclusion_proof.
+ * Writes *proof_len hashes (32 B each) if out_len allows, else DECDS_ERR_INVALID_ARGUMENT. */
+int decds_chunkset_get_chunk_proof(const decds_chunkset *cs, size_t chunk_id, uint8_t *out, size_t out_len,
+                                   size_t *proof_len);
+/* ChunkSet::append_blob_inclusion_proof (chunkset.rs:98-102): appended to every chunk's proof */
+int decds_chunkset_append_blob_inclusion_proof(decds_chunkset *cs, const uint8_t *blob_proof, size_t len);
 /* ChunkSet::get_chunk (chunkset.rs:87-89): copies the 1,048,587-byte erasure-coded data of local
  * chunk `chunk_id`; *global_chunk_id = chunkset_id*16 + chunk_id (chunkset.rs:47) */
 int decds_chunkset_get_chunk(const decds_chunkset *cs, size_t chunk_id, uint8_t *out,
@@ -129,8 +139,18 @@ size_t decds_chunkset_id(const decds_chunkset *cs);
 void decds_chunkset_free(decds_chunkset *cs);
 
 typedef struct decds_repairing_chunkset decds_repairing_chunkset;
-/* RepairingChunkSet::new (chunkset.rs:129-135) */
-int decds_repairing_chunkset_new(decds_ctx *ctx, size_t chunkset_id, decds_repairing_chunkset **out);
+/* RepairingChunkSet::new(chunkset_id, commitment) (chunkset.rs:129-135). commitment: the chunkset's
+ * 32-byte root, used by decds_repairing_chunkset_add_chunk; may be NULL if only
+ * add_chunk_unvalidated is used. */
+int decds_repairing_chunkset_new(decds_ctx *ctx, size_t chunkset_id, const uint8_t *commitment,
+                                 decds_repairing_chunkset **out);
+/* RepairingChunkSet::add_chunk (chunkset.rs:151-157): the chunk (chunkset_id, global chunk_id,
+ * data, proof) must prove inclusion in the commitment (chunk.rs:103-110: leaf chunk_id % 16, the
+ * first 4 proof hashes, digest over the ids and data) or DECDS_ERR_INVALID_PROOF_IN_CHUNK;
+ * otherwise exactly add_chunk_unvalidated. A proof of fewer than 4 hashes is invalid (the
+ * reference's slice would panic). */
+int decds_repairing_chunkset_add_chunk(decds_repairing_chunkset *rcs, size_t chunk_chunkset_id, size_t chunk_id,
+                                       const uint8_t *data, size_t len, const uint8_t *proof, size_t proof_len);
 /* RepairingChunkSet::add_chunk_unvalidated (chunkset.rs:173-184): chunk_chunkset_id is the
  * chunk's get_chunkset_id(); data/len its get_erasure_coded_data() */
 int decds_repairing_chunkset_add_chunk_unvalidated(decds_repairing_chunkset *rcs,
@@ -169,9 +189,25 @@ int decds_commit_batch(decds_ctx *ctx, const uint8_t *coded, size_t pitch, size_
  * with decds' zero-hash padding (blob-level tree, blob.rs:266-273) and proof verification
  * (merkle_tree.rs:131-146). decds_merkle_tree returns the proof depth (proofs: n x depth x 32). */
 void decds_blake3(const uint8_t *data, size_t len, uint8_t out[32]);
+/* Chunk::digest (chunk.rs:40-46) on the host: BLAKE3(chunkset_id u64 LE || chunk_id u64 LE || data) */
+void decds_chunk_digest(uint64_t chunkset_id, uint64_t chunk_id, const uint8_t *data, size_t len, uint8_t out[32]);
 int decds_merkle_tree(const uint8_t *leaves, size_t n, uint8_t root[32], uint8_t *proofs);
 int decds_merkle_verify(size_t leaf_index, const uint8_t leaf[32], const uint8_t *proof, size_t proof_len,
                         const uint8_t root[32]);
+
+/* ---- repair-side validation (next row) ---------------------------------------- */
+/* BlobHeader::validate_chunk (blob.rs:211-215) for a batch of received chunks, all device pointers.
+ * Row r (coded + r*pitch, 1,048,587 B) claims ids[2r] = chunkset_id and ids[2r+1] = global chunk_id,
+ * and carries proofs[r*proof_len .. (r+1)*proof_len) (32-byte hashes: 4 chunkset-level, then the
+ * blob-level ones). digests[r] = Chunk::digest of the row under its claimed ids. valid[r] = 1 iff
+ *   (blob_root == NULL or MerkleTree::verify_proof(chunk_id, digest, proof, blob_root))   chunk.rs:88-90
+ *   and chunkset_id < num_chunksets                                                        blob.rs:213
+ *   and verify_proof(chunk_id % 16, digest, proof[0..4], chunkset_roots[chunkset_id])     chunk.rs:103-110
+ * else 0; proof_len < 4 makes every row invalid. */
+int decds_validate_batch(decds_ctx *ctx, const uint8_t *coded, size_t pitch, size_t n_rows, const uint64_t *ids,
+                         const uint8_t *proofs, size_t proof_len, const uint8_t *chunkset_roots,
+                         size_t num_chunksets, const uint8_t *blob_root, uint8_t *digests, uint8_t *valid,
+                         void *stream);
 
 /* Page-lock a caller buffer once for many host-path calls (otherwise each call pins and unpins
  * its buffers itself). Pair with decds_host_unregister before freeing the buffer. */

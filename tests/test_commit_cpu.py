@@ -63,6 +63,40 @@ def test_chunk_digest_layout():
     assert d == o.blake3((7).to_bytes(8, "little") + (115).to_bytes(8, "little") + data.tobytes())
 
 
+def test_host_chunk_digest_matches_oracle():
+    # the host Chunk::digest the chunkset mirror's add_chunk validates with, on a full coded piece
+    from decds_amd.chunkset import Chunk
+    data = o.fill_random(11, 1048587)
+    for cs_id, chunk_id in [(0, 0), (7, 7 * 16 + 3), (2**40 + 1, (2**40 + 1) * 16 + 15)]:
+        out = ctypes.create_string_buffer(32)
+        _capi.lib().decds_chunk_digest(cs_id, chunk_id, data.tobytes(), data.size, out)
+        assert out.raw == o.chunk_digest(cs_id, chunk_id, data)
+        assert Chunk(cs_id, chunk_id, data.tobytes()).digest() == out.raw
+
+
+def test_host_chunk_validation_semantics():
+    # chunk.rs:88-110 over a 3-chunkset blob built from synthetic digests: chunkset-level proofs are
+    # the first 4 hashes, the blob-level path follows (chunkset.rs:98-102)
+    from decds_amd.chunkset import Chunk
+    rows = {(c, c * 16 + j): o.fill_random(100 * c + j, 257).tobytes() for c in range(3) for j in range(16)}
+    leaves = {k: o.chunk_digest(k[0], k[1], np.frombuffer(v, np.uint8)) for k, v in rows.items()}
+    cs_roots, cs_proofs = [], []
+    for c in range(3):
+        r, p = o.merkle([leaves[(c, c * 16 + j)] for j in range(16)])
+        cs_roots.append(r)
+        cs_proofs.append(p)
+    blob_root, blob_proofs = o.merkle(cs_roots)
+    for (c, gid), data in rows.items():
+        ch = Chunk(c, gid, data, cs_proofs[c][gid % 16] + blob_proofs[c])
+        assert ch.validate_inclusion_in_chunkset(cs_roots[c])
+        assert ch.validate_inclusion_in_blob(blob_root)
+        assert not ch.validate_inclusion_in_chunkset(cs_roots[(c + 1) % 3])
+        short = Chunk(c, gid, data, cs_proofs[c][gid % 16][:3])
+        assert not short.validate_inclusion_in_chunkset(cs_roots[c])
+        wrong_id = Chunk(c, gid ^ 1, data, cs_proofs[c][gid % 16] + blob_proofs[c])
+        assert not wrong_id.validate_inclusion_in_blob(blob_root)
+
+
 def host_merkle(leaves):
     n = len(leaves)
     depth = max(0, (n - 1).bit_length())

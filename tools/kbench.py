@@ -16,6 +16,7 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--tag", default=os.path.basename(os.environ.get("DECDS_LIB", "default")))
     ap.add_argument("--pitch", type=int, default=0)
+    ap.add_argument("--dst-off", type=int, default=0, help="byte offset of the coded buffer (alignment study)")
     ap.add_argument("--check", action="store_true")
     ap.add_argument("--commit", action="store_true", help="also time decds_commit_batch (BLAKE3 + Merkle)")
     a = ap.parse_args()
@@ -35,7 +36,8 @@ def main():
     for c in range(n):
         cand[c, :K] = rng.permutation(N)[:K]
     cand = torch.from_numpy(cand).cuda()
-    coded = torch.empty((n * N - 1) * pitch + F, dtype=torch.uint8, device="cuda")
+    coded_buf = torch.empty((n * N - 1) * pitch + F + a.dst_off, dtype=torch.uint8, device="cuda")
+    coded = coded_buf[a.dst_off:]
     plan = torch.empty(n * 128, dtype=torch.uint8, device="cuda")
     verd = torch.empty(n * N, dtype=torch.int8, device="cuda")
     status = torch.empty(n, dtype=torch.int32, device="cuda")
@@ -63,7 +65,7 @@ def main():
     med = np.median(t, axis=0)
     s = status.cpu().numpy()
     nr = int((s == 0).sum())
-    res = {"tag": a.tag, "n": n, "pitch": pitch, "encode_ms": round(med[0], 4), "plan_ms": round(med[1], 4),
+    res = {"tag": a.tag, "n": n, "pitch": pitch, "dst_off": a.dst_off, "encode_ms": round(med[0], 4), "plan_ms": round(med[1], 4),
            "decode_ms": round(med[2], 4),
            "encode_GBps": round(n * (CS + N * F) / med[0] / 1e6, 1),
            "decode_GBps": round(nr * (K * F + CS) / med[2] / 1e6, 1),
