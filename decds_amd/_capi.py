@@ -35,6 +35,10 @@ STATUS_NAMES = {
     9: "InvalidChunksetId",
     10: "ChunksetAlreadyRepaired",
     11: "InvalidProofInChunk",
+    12: "BlobHeaderSerializationFailed",
+    13: "BlobHeaderDeserializationFailed",
+    14: "ProofCarryingChunkSerializationFailed",
+    15: "ProofCarryingChunkDeserializationFailed",
     -1: "HipError",
     -2: "InvalidArgument",
     -3: "NoDevice",
@@ -95,6 +99,16 @@ def _declare(L):
         "decds_blake3": (None, [VP, SZ, VP]),
         "decds_chunk_digest": (None, [c.c_uint64, c.c_uint64, VP, SZ, VP]),
         "decds_validate_batch": (c.c_int, [P, VP, SZ, SZ, VP, VP, SZ, VP, SZ, VP, VP, VP, VP]),
+        "decds_blake3_parallel": (None, [VP, SZ, VP, c.c_int]),
+        "decds_pcc_encoded_len": (SZ, [c.c_uint64, c.c_uint64, SZ, SZ]),
+        "decds_pcc_to_bytes": (c.c_int, [c.c_uint64, c.c_uint64, VP, SZ, VP, SZ, VP, SZ, c.POINTER(SZ)]),
+        "decds_pcc_from_bytes": (c.c_int, [VP, SZ, c.POINTER(c.c_uint64), c.POINTER(c.c_uint64),
+                                           c.POINTER(c.c_void_p), c.POINTER(SZ), c.POINTER(c.c_void_p),
+                                           c.POINTER(SZ), c.POINTER(SZ)]),
+        "decds_blob_header_encoded_len": (SZ, [c.c_uint64, c.c_uint64, SZ]),
+        "decds_blob_header_to_bytes": (c.c_int, [c.c_uint64, c.c_uint64, VP, VP, VP, SZ, VP, SZ, c.POINTER(SZ)]),
+        "decds_blob_header_from_bytes": (c.c_int, [VP, SZ, c.POINTER(c.c_uint64), c.POINTER(c.c_uint64), VP, VP,
+                                                   c.POINTER(c.c_void_p), c.POINTER(SZ), c.POINTER(SZ)]),
         "decds_merkle_tree": (c.c_int, [VP, SZ, VP, VP]),
         "decds_merkle_verify": (c.c_int, [SZ, VP, VP, SZ, VP]),
         "decds_host_unregister": (c.c_int, [VP]),
@@ -118,6 +132,8 @@ EXPORTED = [
     "decds_merkle_tree", "decds_merkle_verify", "decds_chunk_digest", "decds_validate_batch",
     "decds_chunkset_get_root_commitment", "decds_chunkset_get_chunk_proof",
     "decds_chunkset_append_blob_inclusion_proof", "decds_repairing_chunkset_add_chunk",
+    "decds_blake3_parallel", "decds_pcc_encoded_len", "decds_pcc_to_bytes", "decds_pcc_from_bytes",
+    "decds_blob_header_encoded_len", "decds_blob_header_to_bytes", "decds_blob_header_from_bytes",
 ]
 
 

@@ -55,6 +55,10 @@ const char *decds_status_string(int s) {
         case DECDS_ERR_INVALID_CHUNKSET_ID: return "invalid chunkset id";
         case DECDS_ERR_CHUNKSET_ALREADY_REPAIRED: return "chunkset already repaired";
         case DECDS_ERR_INVALID_PROOF_IN_CHUNK: return "invalid proof in chunk";
+        case DECDS_ERR_BLOB_HEADER_SERIALIZATION_FAILED: return "failed to serialize blob header";
+        case DECDS_ERR_BLOB_HEADER_DESERIALIZATION_FAILED: return "failed to deserialize blob header";
+        case DECDS_ERR_PCC_SERIALIZATION_FAILED: return "failed to serialize proof carrying chunk";
+        case DECDS_ERR_PCC_DESERIALIZATION_FAILED: return "failed to deserialize proof carrying chunk";
         case DECDS_ERR_HIP: return "HIP runtime error";
         case DECDS_ERR_INVALID_ARGUMENT: return "invalid argument";
         case DECDS_ERR_NO_DEVICE: return "no gfx950 device";

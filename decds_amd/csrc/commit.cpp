@@ -2,6 +2,7 @@
 // chunkset Merkle roots and proofs) and host helpers for the blob-level tree (blob.rs:266-273),
 // which covers only the 32-byte chunkset roots.
 #include <cstring>
+#include <thread>
 #include <vector>
 
 #include "../../include/decds_rlnc.h"
@@ -56,6 +57,23 @@ void subtree_cv(const uint8_t *p, size_t len, uint64_t first, bool root, uint32_
     b3::parent(l, r, root ? b3::ROOT : 0u, cv);
 }
 
+// the same tree with the two halves of each split on separate threads while the thread budget lasts
+void subtree_cv_par(const uint8_t *p, size_t len, uint64_t first, bool root, uint32_t cv[8], int threads) {
+    if (threads <= 1 || len <= ((size_t)1 << 20)) {
+        subtree_cv(p, len, first, root, cv);
+        return;
+    }
+    size_t left_chunks = 1;
+    while ((left_chunks * 2) * b3::CHUNK < len) left_chunks *= 2;
+    const size_t left_len = left_chunks * b3::CHUNK;
+    uint32_t l[8], r[8];
+    const int lt = threads / 2;
+    std::thread t([&] { subtree_cv_par(p, left_len, first, false, l, lt); });
+    subtree_cv_par(p + left_len, len - left_len, first + left_chunks, false, r, threads - lt);
+    t.join();
+    b3::parent(l, r, root ? b3::ROOT : 0u, cv);
+}
+
 void hash_pair(const uint8_t *l, const uint8_t *r, uint8_t out[32]) {
     uint8_t buf[64];
     std::memcpy(buf, l, 32);
@@ -73,6 +91,12 @@ extern "C" {
 void decds_blake3(const uint8_t *data, size_t len, uint8_t out[32]) {
     uint32_t cv[8];
     subtree_cv(data, len, 0, true, cv);
+    to_bytes(cv, out);
+}
+
+void decds_blake3_parallel(const uint8_t *data, size_t len, uint8_t out[32], int nthreads) {
+    uint32_t cv[8];
+    subtree_cv_par(data, len, 0, true, cv, nthreads < 1 ? 1 : nthreads);
     to_bytes(cv, out);
 }
 

@@ -50,6 +50,10 @@ extern "C" {
 #define DECDS_ERR_INVALID_CHUNKSET_ID 9            /* InvalidChunksetId(id, n)        errors.rs:34 */
 #define DECDS_ERR_CHUNKSET_ALREADY_REPAIRED 10     /* ChunksetAlreadyRepaired(id)     errors.rs:27 */
 #define DECDS_ERR_INVALID_PROOF_IN_CHUNK 11        /* InvalidProofInChunk(id)         errors.rs:40 */
+#define DECDS_ERR_BLOB_HEADER_SERIALIZATION_FAILED 12    /* BlobHeaderSerializationFailed     errors.rs:13 */
+#define DECDS_ERR_BLOB_HEADER_DESERIALIZATION_FAILED 13  /* BlobHeaderDeserializationFailed   errors.rs:15 */
+#define DECDS_ERR_PCC_SERIALIZATION_FAILED 14            /* ProofCarryingChunkSerializationFailed   errors.rs:18 */
+#define DECDS_ERR_PCC_DESERIALIZATION_FAILED 15          /* ProofCarryingChunkDeserializationFailed errors.rs:20 */
 #define DECDS_ERR_HIP (-1)                         /* HIP runtime failure (text: decds_last_error) */
 #define DECDS_ERR_INVALID_ARGUMENT (-2)
 #define DECDS_ERR_NO_DEVICE (-3)
@@ -208,6 +212,31 @@ int decds_validate_batch(decds_ctx *ctx, const uint8_t *coded, size_t pitch, siz
                          const uint8_t *proofs, size_t proof_len, const uint8_t *chunkset_roots,
                          size_t num_chunksets, const uint8_t *blob_root, uint8_t *digests, uint8_t *valid,
                          void *stream);
+
+/* ---- wire / on-disk format (next row): bincode 2 standard(), consts.rs:2 ----- */
+/* ProofCarryingChunk::to_bytes / from_bytes (chunk.rs:152-170): varint chunkset_id, varint chunk_id,
+ * varint data length + data, varint proof length + 32-byte hashes. from_bytes is zero-copy: *data
+ * and *proof point into `bytes`; *consumed = bytes read (the file flow rejects trailing bytes,
+ * decds-bin utils.rs:60-70). Truncated or malformed input -> DECDS_ERR_PCC_DESERIALIZATION_FAILED. */
+size_t decds_pcc_encoded_len(uint64_t chunkset_id, uint64_t chunk_id, size_t data_len, size_t proof_len);
+int decds_pcc_to_bytes(uint64_t chunkset_id, uint64_t chunk_id, const uint8_t *data, size_t data_len,
+                       const uint8_t *proof, size_t proof_len, uint8_t *out, size_t cap, size_t *written);
+int decds_pcc_from_bytes(const uint8_t *bytes, size_t len, uint64_t *chunkset_id, uint64_t *chunk_id,
+                         const uint8_t **data, size_t *data_len, const uint8_t **proof, size_t *proof_len,
+                         size_t *consumed);
+/* BlobHeader::to_bytes / from_bytes (blob.rs:168-197): varint byte_length, varint num_chunksets,
+ * digest, root commitment, varint count + chunkset roots; from_bytes also rejects
+ * num_chunksets != count (blob.rs:187-191). */
+size_t decds_blob_header_encoded_len(uint64_t byte_length, uint64_t num_chunksets, size_t n_roots);
+int decds_blob_header_to_bytes(uint64_t byte_length, uint64_t num_chunksets, const uint8_t digest[32],
+                               const uint8_t root[32], const uint8_t *chunkset_roots, size_t n_roots, uint8_t *out,
+                               size_t cap, size_t *written);
+int decds_blob_header_from_bytes(const uint8_t *bytes, size_t len, uint64_t *byte_length, uint64_t *num_chunksets,
+                                 uint8_t digest[32], uint8_t root[32], const uint8_t **chunkset_roots, size_t *n_roots,
+                                 size_t *consumed);
+/* blake3::hash of a whole blob (Blob::new's header digest, blob.rs:249) with BLAKE3's subtrees
+ * split over up to nthreads host threads (same result as decds_blake3) */
+void decds_blake3_parallel(const uint8_t *data, size_t len, uint8_t out[32], int nthreads);
 
 /* Page-lock a caller buffer once for many host-path calls (otherwise each call pins and unpins
  * its buffers itself). Pair with decds_host_unregister before freeing the buffer. */
