@@ -55,6 +55,13 @@ def lib():
             raise ImportError(
                 "decds_amd: %s is missing — build it with `python -m decds_amd.build` "
                 "(hipcc --offload-arch=gfx950); there is no fallback implementation" % LIB_PATH)
+        try:
+            # torch ships its own libamdhip64: load it first so the library binds to the same HIP
+            # runtime instead of a second copy from /opt/rocm (two runtimes in one process break
+            # torch's device init and pointer sharing)
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = ctypes.CDLL(LIB_PATH)
         _declare(L)
         _lib = L

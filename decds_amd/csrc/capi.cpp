@@ -3,6 +3,8 @@
 // launchers. Every compute entry point runs the gfx950 kernels; there is no host fallback.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -94,6 +96,7 @@ int decds_ctx_create(int device, decds_ctx **out) {
     c->poly = POLY_DEFAULT;
     c->marker = (uint8_t)MARKER_DEFAULT;
     c->geom.num_cus = prop.multiProcessorCount;
+    if (const char *w = std::getenv("DECDS_WGS_PER_CU")) c->geom.wgs_per_cu = std::atoi(w) == 1 ? 1 : 2;
     *out = c;
     return DECDS_OK;
 }

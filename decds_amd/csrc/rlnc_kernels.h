@@ -8,6 +8,8 @@ namespace decds {
 
 struct LaunchGeom {
     int num_cus;          // CUs on the device (256 on MI355X)
+    int wgs_per_cu = 2;   // resident streaming workgroups per CU (2 x 80 KiB LDS = all of it);
+                          // 1 leaves half the CU for a concurrent kernel (DECDS_WGS_PER_CU=1)
 };
 
 hipError_t launch_encode(const LaunchGeom &g, const uint8_t *src, size_t n, const uint8_t *coeffs,

@@ -78,18 +78,44 @@ __device__ __forceinline__ uint32_t gf_inv(uint32_t a, uint32_t poly) {  // a^25
 
 // Build the 2*NIN replicated nibble tables for a NOUT x NIN coefficient matrix M (row-major in
 // global memory, row stride ldm). Caller brackets with __syncthreads().
+// Multiplication by a constant is linear over GF(2), so row (i, h, nib) = XOR of the products of
+// C[.][i] with the set bits of nib << 4h: thread (i, h, output quad q) forms the 4 basis words
+// { C[4q+jj][i] * x^(4h+k) : jj < 4 } (xtime chains) and the 16 rows' dwords q by one XOR each
+// (nib & (nib-1) is nib minus its lowest bit), writing replica 0; a second pass copies each
+// 16-byte row into replicas 1..15. ~30 VALU per thread instead of 5120 bit-serial multiplies.
 template <int NIN, int NOUT>
 __device__ __forceinline__ void build_tables(uint8_t *lds, const uint8_t *M, uint32_t ldm, uint32_t poly) {
+    for (uint32_t p = threadIdx.x; p < NIN * 8; p += WG) {
+        const uint32_t q = p & 3u, h = (p >> 2) & 1u, i = p >> 3;
+        uint32_t bw[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (uint32_t jj = 0; jj < 4; jj++) {
+            const uint32_t j = 4 * q + jj;
+            uint32_t c = j < (uint32_t)NOUT ? M[j * ldm + i] : 0u;
+            if (h) {
+#pragma unroll
+                for (int k = 0; k < 4; k++) c = (c << 1) ^ ((c & 0x80u) ? poly : 0u);
+            }
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                bw[k] |= c << (8 * jj);
+                c = (c << 1) ^ ((c & 0x80u) ? poly : 0u);
+            }
+        }
+        uint32_t w[16];
+        w[0] = 0;
+#pragma unroll
+        for (int nib = 1; nib < 16; nib++) w[nib] = w[nib & (nib - 1)] ^ bw[__builtin_ctz(nib)];
+        uint8_t *base = lds + (i * 2 + h) * TABLE_BYTES + 4 * q;
+#pragma unroll
+        for (int nib = 0; nib < 16; nib++) *reinterpret_cast<uint32_t *>(base + nib * ROW_BYTES) = w[nib];
+    }
+    __syncthreads();
     for (uint32_t r = threadIdx.x; r < NIN * 32; r += WG) {
-        const uint32_t i = r >> 5, h = (r >> 4) & 1u, n = r & 15u;
-        const uint32_t m = n << (4 * h);
-        uint32_t v[4] = {0, 0, 0, 0};
+        uint8_t *row = lds + r * ROW_BYTES;
+        const uint4 val = *reinterpret_cast<const uint4 *>(row);
 #pragma unroll
-        for (int j = 0; j < NOUT; j++) v[j >> 2] |= gf_mul(M[j * ldm + i], m, poly) << (8 * (j & 3));
-        const uint4 val = make_uint4(v[0], v[1], v[2], v[3]);
-        uint8_t *row = lds + (i * 2 + h) * TABLE_BYTES + n * ROW_BYTES;
-#pragma unroll
-        for (int c = 0; c < 16; c++) *reinterpret_cast<uint4 *>(row + c * 16) = val;
+        for (int c = 1; c < 16; c++) *reinterpret_cast<uint4 *>(row + c * 16) = val;
     }
 }
 
@@ -289,26 +315,53 @@ __device__ __forceinline__ void combine_block(const uint8_t *lds, uint32_t laneo
 }
 
 // ---- work split ---------------------------------------------------------------------------------
-// The n*256 tiles (256 lane blocks = 4096 columns each) are divided into equal contiguous ranges,
-// one per resident workgroup; a workgroup rebuilds its LDS tables only when its range crosses into
-// the next chunkset. (Interleaving workgroups over neighbouring tiles measured slower:
-// DESIGN.md "Tuning log".)
+// SUPER == 0: the n*256 tiles (256 lane blocks = 4096 columns each) are divided into equal
+// contiguous ranges, one per resident workgroup (each workgroup rebuilds its LDS tables only when
+// its range crosses into the next chunkset).
+// SUPER > 0: super-tiles of SUPER consecutive tiles of one chunkset are dealt round-robin to the
+// workgroups, so at any moment the resident workgroups sweep a few whole chunksets side by side
+// (every coded row written by many workgroups at once) at the price of a table rebuild per
+// super-tile.
+#ifndef DECDS_ENC_SUPER
+#define DECDS_ENC_SUPER 0
+#endif
+#ifndef DECDS_DEC_SUPER
+#define DECDS_DEC_SUPER 8
+#endif
 __device__ __forceinline__ void tile_range(size_t n, uint32_t &t0, uint32_t &t1) {
     const uint64_t total = (uint64_t)n * TILES_PER_CS;
     t0 = (uint32_t)(total * blockIdx.x / gridDim.x);
     t1 = (uint32_t)(total * (blockIdx.x + 1) / gridDim.x);
 }
 
-// One tile of a workgroup's range for this lane: inputs were prefetched by the previous tile when
-// `have` (ROLL), else they are loaded now.
+// calls f(chunkset, tile, next_is_consecutive) for this workgroup's tiles in order
+template <uint32_t S, class Fn>
+__device__ __forceinline__ void walk_tiles(size_t n, Fn &&f) {
+    if constexpr (S == 0) {
+        uint32_t t0, t1;
+        tile_range(n, t0, t1);
+        for (uint32_t t = t0; t < t1; t++) f(t / TILES_PER_CS, t % TILES_PER_CS, t + 1 < t1 && (t + 1) % TILES_PER_CS != 0);
+    } else {
+        static_assert(TILES_PER_CS % S == 0, "super-tile size");
+        constexpr uint32_t SPC = TILES_PER_CS / S;
+        const uint32_t total = (uint32_t)n * SPC;
+        for (uint32_t st = blockIdx.x; st < total; st += gridDim.x) {
+            const uint32_t cs = st / SPC, tb = (st % SPC) * S;
+            for (uint32_t k = 0; k < S; k++) f(cs, tb + k, k + 1 < S);
+        }
+    }
+}
+
+// One tile for this lane: inputs were prefetched by the previous tile when `have` (ROLL), else
+// they are loaded now; `next` says whether the following tile is the next one of this chunkset.
 template <class T, int NIN, int NOUT>
-__device__ __forceinline__ void stream_tile(const uint8_t *lds, uint32_t laneoff, uint32_t t, uint32_t t1, uint32_t cs,
-                                            uint32_t tile, const uint8_t *ibase, const uint32_t (&ioff)[NIN],
-                                            uint8_t *obase, const uint32_t (&ooff)[NOUT], uint4 (&x)[NIN], bool &have) {
+__device__ __forceinline__ void stream_tile(const uint8_t *lds, uint32_t laneoff, uint32_t tile, bool next,
+                                            const uint8_t *ibase, const uint32_t (&ioff)[NIN], uint8_t *obase,
+                                            const uint32_t (&ooff)[NOUT], uint4 (&x)[NIN], bool &have) {
     const uint32_t block = tile * TILE_BLOCKS + threadIdx.x;
     const bool active = block < MAIN_BLOCKS;
     if (!(T::ROLL && have) && active) load_block<T, NIN>(x, ibase, ioff, block * COLS_PER_LANE);
-    have = t + 1 < t1 && (t + 1) / TILES_PER_CS == cs;
+    have = next;
     const uint32_t nblock = block + TILE_BLOCKS;
     // branch-free prefetch: lanes with no next block re-load their own block (an L2 hit)
     const uint32_t ncol0 = (have && nblock < MAIN_BLOCKS ? nblock : block) * COLS_PER_LANE;
@@ -319,8 +372,6 @@ __global__ __launch_bounds__(WG, WAVES_PER_SIMD) __attribute__((amdgpu_waves_per
 void rlnc_encode_kernel(const uint8_t *__restrict__ src, size_t n, const uint8_t *__restrict__ coeffs,
                         uint8_t *__restrict__ dst, size_t pitch, uint32_t poly, uint32_t marker) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    uint32_t t0, t1;
-    tile_range(n, t0, t1);
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t laneoff = (lane & 15u) * 16u;
     uint32_t ioff[K], ooff[N];
@@ -331,46 +382,44 @@ void rlnc_encode_kernel(const uint8_t *__restrict__ src, size_t n, const uint8_t
     uint32_t cur = 0xFFFFFFFFu;
     const uint8_t *ibase = src;
     uint8_t *obase = dst;
+    const uint8_t *M = coeffs;
     uint4 x[K];
     bool have = false;
-    for (uint32_t t = t0; t < t1; t++) {
-        const uint32_t cs = t / TILES_PER_CS, tile = t % TILES_PER_CS;
+    walk_tiles<DECDS_ENC_SUPER>(n, [&](uint32_t cs, uint32_t tile, bool next) {
         if (cs != cur) {
             cur = cs;
             have = false;
-            const uint8_t *M = coeffs + (size_t)cs * N * K;
+            M = coeffs + (size_t)cs * N * K;
             __syncthreads();
             build_tables<K, N>(lds, M, K, poly);
             __syncthreads();
             ibase = src + (size_t)cs * CS;
             obase = dst + (size_t)cs * N * pitch;
-            if (tile == 0 && threadIdx.x < 64) {
-                // coding-vector prefix of the 16 full coded pieces (rlnc layout: cv || payload)
-                for (uint32_t idx = lane; idx < N * K; idx += 64) obase[(idx / K) * pitch + idx % K] = M[idx];
-                // last 17 columns: piece 9 carries the boundary marker, then zero padding
-                for (uint32_t idx = lane; idx < TAIL_COLS * N; idx += 64) {
-                    const uint32_t j = idx % N, col = MAIN_COLS + idx / N;
-                    uint32_t y = 0;
+        }
+        if (tile == 0 && threadIdx.x < 64) {
+            // coding-vector prefix of the 16 full coded pieces (rlnc layout: cv || payload)
+            for (uint32_t idx = lane; idx < N * K; idx += 64) obase[(idx / K) * pitch + idx % K] = M[idx];
+            // last 17 columns: piece 9 carries the boundary marker, then zero padding
+            for (uint32_t idx = lane; idx < TAIL_COLS * N; idx += 64) {
+                const uint32_t j = idx % N, col = MAIN_COLS + idx / N;
+                uint32_t y = 0;
 #pragma unroll
-                    for (uint32_t i = 0; i < K; i++) {
-                        const uint64_t p = (uint64_t)i * L + col;
-                        const uint32_t xv = p < CS ? ibase[p] : (p == CS ? marker : 0u);
-                        y ^= tbl_mul(lds, i, j, xv);
-                    }
-                    obase[j * pitch + K + col] = (uint8_t)y;
+                for (uint32_t i = 0; i < K; i++) {
+                    const uint64_t p = (uint64_t)i * L + col;
+                    const uint32_t xv = p < CS ? ibase[p] : (p == CS ? marker : 0u);
+                    y ^= tbl_mul(lds, i, j, xv);
                 }
+                obase[j * pitch + K + col] = (uint8_t)y;
             }
         }
-        stream_tile<EncTune, K, N>(lds, laneoff, t, t1, cs, tile, ibase, ioff, obase, ooff, x, have);
-    }
+        stream_tile<EncTune, K, N>(lds, laneoff, tile, next, ibase, ioff, obase, ooff, x, have);
+    });
 }
 
 __global__ __launch_bounds__(WG, WAVES_PER_SIMD) __attribute__((amdgpu_waves_per_eu(WAVES_PER_SIMD, WAVES_PER_SIMD)))
 void rlnc_decode_kernel(const uint8_t *__restrict__ coded, size_t pitch, size_t n, const RepairPlan *__restrict__ plan,
                         uint8_t *__restrict__ dst, int32_t *__restrict__ status, uint32_t poly, uint32_t marker) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    uint32_t t0, t1;
-    tile_range(n, t0, t1);
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t laneoff = (lane & 15u) * 16u;
     uint32_t ioff[K], ooff[K];
@@ -384,8 +433,7 @@ void rlnc_decode_kernel(const uint8_t *__restrict__ coded, size_t pitch, size_t 
     uint8_t *obase = dst;
     uint4 x[K];
     bool have = false;
-    for (uint32_t t = t0; t < t1; t++) {
-        const uint32_t cs = t / TILES_PER_CS, tile = t % TILES_PER_CS;
+    walk_tiles<DECDS_DEC_SUPER>(n, [&](uint32_t cs, uint32_t tile, bool next) {
         if (cs != cur) {
             cur = cs;
             have = false;
@@ -407,28 +455,28 @@ void rlnc_decode_kernel(const uint8_t *__restrict__ coded, size_t pitch, size_t 
                 for (int k = 0; k < (int)K; k++) ioff[k] = (uint32_t)(sel[k] * pitch + K);
                 ibase = coded + (size_t)cs * N * pitch;
                 obase = dst + (size_t)cs * CS;
-                if (tile == 0 && threadIdx.x < 64) {
-                    // last 17 columns; piece 9's must decode to marker || zeros (rlnc
-                    // get_decoded_data strips them; a mismatch is a repairing failure)
-                    bool ok = true;
-                    for (uint32_t idx = lane; idx < TAIL_COLS * K; idx += 64) {
-                        const uint32_t i = idx % K, col = MAIN_COLS + idx / K;
-                        uint32_t z = 0;
-#pragma unroll
-                        for (uint32_t k = 0; k < K; k++) z ^= tbl_mul(lds, k, i, ibase[ioff[k] + col]);
-                        const uint64_t p = (uint64_t)i * L + col;
-                        if (p < CS)
-                            obase[p] = (uint8_t)z;
-                        else
-                            ok &= z == (p == CS ? marker : 0u);
-                    }
-                    if (__any(!ok) && lane == 0) status[cs] = 6;  // DECDS_ERR_CHUNKSET_REPAIRING_FAILED
-                }
             }
         }
-        if (!ready) continue;
-        stream_tile<DecTune, K, K>(lds, laneoff, t, t1, cs, tile, ibase, ioff, obase, ooff, x, have);
-    }
+        if (!ready) return;
+        if (tile == 0 && threadIdx.x < 64) {
+            // last 17 columns; piece 9's must decode to marker || zeros (rlnc
+            // get_decoded_data strips them; a mismatch is a repairing failure)
+            bool ok = true;
+            for (uint32_t idx = lane; idx < TAIL_COLS * K; idx += 64) {
+                const uint32_t i = idx % K, col = MAIN_COLS + idx / K;
+                uint32_t z = 0;
+#pragma unroll
+                for (uint32_t k = 0; k < K; k++) z ^= tbl_mul(lds, k, i, ibase[ioff[k] + col]);
+                const uint64_t p = (uint64_t)i * L + col;
+                if (p < CS)
+                    obase[p] = (uint8_t)z;
+                else
+                    ok &= z == (p == CS ? marker : 0u);
+            }
+            if (__any(!ok) && lane == 0) status[cs] = 6;  // DECDS_ERR_CHUNKSET_REPAIRING_FAILED
+        }
+        stream_tile<DecTune, K, K>(lds, laneoff, tile, next, ibase, ioff, obase, ooff, x, have);
+    });
 }
 
 // x * f for a per-lane x and a wave-uniform f: the branches test bits of f, so they are scalar
@@ -574,7 +622,7 @@ __global__ void fill_random_bytes_kernel(uint64_t seed, uint64_t off, uint8_t *d
 // ------------------------------------------------------------------------------ launchers ----
 static uint32_t stream_grid(const LaunchGeom &g, size_t n) {
     const uint64_t tiles = (uint64_t)n * TILES_PER_CS;
-    uint64_t grid = (uint64_t)g.num_cus * WGS_PER_CU;
+    uint64_t grid = (uint64_t)g.num_cus * (g.wgs_per_cu == 1 ? 1 : WGS_PER_CU);
     return (uint32_t)(tiles < grid ? tiles : grid);
 }
 
