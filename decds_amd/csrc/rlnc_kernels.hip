@@ -76,8 +76,20 @@ __device__ __forceinline__ uint32_t gf_inv(uint32_t a, uint32_t poly) {  // a^25
     return r;
 }
 
+// Workgroup barrier for the LDS tables only: every wave's LDS accesses have completed, nothing
+// else. __syncthreads() also drains each wave's outstanding global stores (a release fence), which
+// made every table rebuild cost a full store-queue drain.
+__device__ __forceinline__ void lds_barrier() {
+#ifdef DECDS_FULL_SYNC
+    __syncthreads();
+#else
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0); vmcnt / expcnt left unconstrained
+    __builtin_amdgcn_s_barrier();
+#endif
+}
+
 // Build the 2*NIN replicated nibble tables for a NOUT x NIN coefficient matrix M (row-major in
-// global memory, row stride ldm). Caller brackets with __syncthreads().
+// global memory, row stride ldm). Caller brackets with lds_barrier().
 // Multiplication by a constant is linear over GF(2), so row (i, h, nib) = XOR of the products of
 // C[.][i] with the set bits of nib << 4h: thread (i, h, output quad q) forms the 4 basis words
 // { C[4q+jj][i] * x^(4h+k) : jj < 4 } (xtime chains) and the 16 rows' dwords q by one XOR each
@@ -110,7 +122,7 @@ __device__ __forceinline__ void build_tables(uint8_t *lds, const uint8_t *M, uin
 #pragma unroll
         for (int nib = 0; nib < 16; nib++) *reinterpret_cast<uint32_t *>(base + nib * ROW_BYTES) = w[nib];
     }
-    __syncthreads();
+    lds_barrier();
     for (uint32_t r = threadIdx.x; r < NIN * 32; r += WG) {
         uint8_t *row = lds + r * ROW_BYTES;
         const uint4 val = *reinterpret_cast<const uint4 *>(row);
@@ -390,9 +402,9 @@ void rlnc_encode_kernel(const uint8_t *__restrict__ src, size_t n, const uint8_t
             cur = cs;
             have = false;
             M = coeffs + (size_t)cs * N * K;
-            __syncthreads();
+            lds_barrier();
             build_tables<K, N>(lds, M, K, poly);
-            __syncthreads();
+            lds_barrier();
             ibase = src + (size_t)cs * CS;
             obase = dst + (size_t)cs * N * pitch;
         }
@@ -445,9 +457,9 @@ void rlnc_decode_kernel(const uint8_t *__restrict__ coded, size_t pitch, size_t 
             const uint32_t w2 = __builtin_amdgcn_readfirstlane(pw[2]);
             ready = ((w2 >> 16) & 0xFFu) == K;  // RepairPlan::rank at byte 10
             if (ready) {
-                __syncthreads();
+                lds_barrier();
                 build_tables<K, K>(lds, pl->inv, K, poly);
-                __syncthreads();
+                lds_barrier();
                 const uint32_t sel[K] = {w0 & 0xFFu, (w0 >> 8) & 0xFFu, (w0 >> 16) & 0xFFu, w0 >> 24,
                                          w1 & 0xFFu, (w1 >> 8) & 0xFFu, (w1 >> 16) & 0xFFu, w1 >> 24,
                                          w2 & 0xFFu, (w2 >> 8) & 0xFFu};
