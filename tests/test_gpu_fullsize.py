@@ -1,0 +1,97 @@
+"""BASELINE config 3/4 at full size on one GPU: a 16 GiB blob (1639 chunksets, the last one holding
+4 MiB of data) encoded in one batch, repaired from exactly 10 random survivors per chunkset, and
+committed + validated (rows f1, f2). Spot chunksets / rows are bit-exact against the oracle; every
+other check is a size-independent property (decode∘encode = id, rank-deficient sets reported
+not-ready exactly where the oracle's rank test says so, every row's proof verifies, a flipped byte
+does not)."""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+from decds_amd import codec  # noqa: E402
+from decds_amd._capi import CHUNKSET_BYTES as CS, CODED_PIECE_BYTES as F, K, N  # noqa: E402
+import oracle as o  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+
+def _rank_of(cvs, cand):
+    """the oracle decoder's rank after the candidates' coefficient prefixes (chunkset.rs:173-184)"""
+    dec = o.Decoder(3, K)
+    for r in cand:
+        if r == 0xFF or dec.is_already_decoded():
+            break
+        dec.decode(np.concatenate([cvs[r], np.zeros(3, np.uint8)]))
+    return dec.rank()
+
+
+def test_cfg3_16gib_encode_repair_commit_validate(ctx):
+    blob_len = 16 << 30
+    n = -(-blob_len // CS)
+    assert n == 1639
+    src = torch.zeros(n * CS, dtype=torch.uint8, device="cuda")
+    codec.fill_random_device(ctx, 0xDEC05003, src, nbytes=blob_len)
+    coeffs = o.fill_random(0xC0EF0003, n * N * K)
+    coded = torch.empty(n * N * F, dtype=torch.uint8, device="cuda")
+    codec.encode_batch(ctx, src, n, torch.from_numpy(coeffs).cuda(), coded)
+    torch.cuda.synchronize()
+    for c in (0, 820, n - 1):
+        ref = o.chunkset_encode(src[c * CS:(c + 1) * CS].cpu().numpy(), coeffs[c * 160:(c + 1) * 160], nthreads=8)
+        assert np.array_equal(coded[c * N * F:(c + 1) * N * F].cpu().numpy().reshape(N, F), ref), c
+
+    # repair from exactly 10 random survivors per chunkset (cfg4)
+    rng = np.random.default_rng(0x5EED0003)
+    cand = np.full((n, N), 0xFF, np.uint8)
+    for c in range(n):
+        cand[c, :K] = rng.permutation(N)[:K]
+    plan = torch.empty(n * 128, dtype=torch.uint8, device="cuda")
+    verd = torch.empty(n * N, dtype=torch.int8, device="cuda")
+    status = torch.empty(n, dtype=torch.int32, device="cuda")
+    out = torch.empty(n * CS, dtype=torch.uint8, device="cuda")
+    codec.repair_batch(ctx, coded, n, torch.from_numpy(cand).cuda(), plan, verd, out, status)
+    st = status.cpu().numpy()
+    cv = coeffs.reshape(n, N, K)
+    expect = np.array([0 if _rank_of(cv[c], cand[c]) == K else 5 for c in range(n)])
+    assert np.array_equal(st, expect)
+    assert 0 < int((st == 5).sum()) < 30     # ~0.39 % of 1639 are rank-deficient
+    for c in np.nonzero(st == 0)[0].tolist():
+        assert torch.equal(out[c * CS:(c + 1) * CS], src[c * CS:(c + 1) * CS]), c
+    del out, src
+
+    # commitment of every coded row, then the blob-level tree and validation of all 26,224 rows
+    dig = torch.empty(n * N * 32, dtype=torch.uint8, device="cuda")
+    roots = torch.empty(n * 32, dtype=torch.uint8, device="cuda")
+    proofs = torch.empty(n * N * 128, dtype=torch.uint8, device="cuda")
+    codec.commit_batch(ctx, coded, n, dig, roots, proofs)
+    torch.cuda.synchronize()
+    d = dig.cpu().numpy()
+    for row in (0, 1, 13107, n * N - 1):
+        piece = coded[row * F:(row + 1) * F].cpu().numpy()
+        assert d[row * 32:(row + 1) * 32].tobytes() == o.chunk_digest(row // N, row, piece), row
+    leaves = [d[((n - 1) * N + j) * 32:((n - 1) * N + j + 1) * 32].tobytes() for j in range(N)]
+    r = roots.cpu().numpy()
+    assert r[(n - 1) * 32:n * 32].tobytes() == o.merkle(leaves)[0]
+    cs_roots = [r[c * 32:(c + 1) * 32].tobytes() for c in range(n)]
+    blob_root, blob_proofs = o.merkle(cs_roots)
+    depth = len(blob_proofs[0])
+    assert depth == 11
+    pr = proofs.cpu().numpy().reshape(n * N, 128)
+    full = np.empty((n * N, 4 + depth, 32), np.uint8)
+    full[:, :4] = pr.reshape(n * N, 4, 32)
+    bp = np.frombuffer(b"".join(b"".join(p) for p in blob_proofs), np.uint8).reshape(n, depth, 32)
+    full[:, 4:] = np.repeat(bp, N, axis=0)
+    ids = torch.tensor([(row // N, row) for row in range(n * N)], dtype=torch.int64).cuda()
+    fp = torch.from_numpy(full.reshape(-1)).cuda()
+    vdig = torch.empty(n * N * 32, dtype=torch.uint8, device="cuda")
+    valid = torch.empty(n * N, dtype=torch.uint8, device="cuda")
+    broot = torch.from_numpy(np.frombuffer(blob_root, np.uint8).copy()).cuda()
+    codec.validate_batch(ctx, coded, n * N, ids, fp, 4 + depth, roots, n, vdig, valid, blob_root=broot)
+    torch.cuda.synchronize()
+    assert int(valid.sum()) == n * N
+    assert torch.equal(vdig, dig)
+    # one flipped payload byte invalidates exactly its row
+    coded[777 * F + 4321] ^= 1
+    codec.validate_batch(ctx, coded, n * N, ids, fp, 4 + depth, roots, n, vdig, valid, blob_root=broot)
+    v = valid.cpu().numpy()
+    assert int(v.sum()) == n * N - 1 and v[777] == 0
