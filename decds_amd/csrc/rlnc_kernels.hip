@@ -40,10 +40,12 @@ static_assert(TILES_PER_CS == 256, "tile geometry");
 //   ROLL : the next block's input i is loaded as soon as this block has consumed input i
 //   LAUX / SAUX : cache-policy word of the streaming loads / stores (buffer instructions; gfx950:
 //          sc0 = 1, nt = 2, sc1 = 16); -1 = plain global_load / global_store
-template <bool ASM_, bool ROLL_, int LAUX_, int SAUX_>
+//   SYNC : workgroup barrier per tile (1: at the tile's start, 2: before its stores) so the 4 waves
+//          write each row's 4 KiB span of the tile together instead of drifting apart
+template <bool ASM_, bool ROLL_, int LAUX_, int SAUX_, int SYNC_ = 0>
 struct Tune {
     static constexpr bool ASM = ASM_, ROLL = ROLL_;
-    static constexpr int LAUX = LAUX_, SAUX = SAUX_;
+    static constexpr int LAUX = LAUX_, SAUX = SAUX_, SYNC = SYNC_;
 };
 #ifndef DECDS_ENC_TUNE
 #define DECDS_ENC_TUNE false, false, -1, -1
@@ -51,8 +53,14 @@ struct Tune {
 #ifndef DECDS_DEC_TUNE
 #define DECDS_DEC_TUNE true, true, -1, 2
 #endif
-using EncTune = Tune<DECDS_ENC_TUNE>;
-using DecTune = Tune<DECDS_DEC_TUNE>;
+#ifndef DECDS_ENC_SYNC
+#define DECDS_ENC_SYNC 0
+#endif
+#ifndef DECDS_DEC_SYNC
+#define DECDS_DEC_SYNC 0
+#endif
+using EncTune = Tune<DECDS_ENC_TUNE, DECDS_ENC_SYNC>;
+using DecTune = Tune<DECDS_DEC_TUNE, DECDS_DEC_SYNC>;
 
 // ---- GF(2^8) ----------------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t gf_mul(uint32_t a, uint32_t b, uint32_t poly) {
@@ -88,22 +96,39 @@ __device__ __forceinline__ void lds_barrier() {
 #endif
 }
 
-// Build the 2*NIN replicated nibble tables for a NOUT x NIN coefficient matrix M (row-major in
-// global memory, row stride ldm). Caller brackets with lds_barrier().
+// The 4 coefficient bytes thread p = 8i + 4h + q (< NIN*8) of build_tables combines:
+// M[(4q + jj) * ldm + i], jj < 4 (zero for outputs >= NOUT and for idle threads). (Loading it one
+// chunkset ahead measured no faster)
+template <int NIN, int NOUT>
+__device__ __forceinline__ uint32_t table_coeffs(const uint8_t *M, uint32_t ldm) {
+    static_assert(NIN * 8 <= (int)WG, "one coefficient word per thread");
+    const uint32_t p = threadIdx.x;
+    uint32_t w = 0;
+    if (p < NIN * 8) {
+        const uint32_t q = p & 3u, i = p >> 3;
+#pragma unroll
+        for (uint32_t jj = 0; jj < 4; jj++)
+            if (4 * q + jj < (uint32_t)NOUT) w |= (uint32_t)M[(4 * q + jj) * ldm + i] << (8 * jj);
+    }
+    return w;
+}
+
+// Build the 2*NIN replicated nibble tables of a NOUT x NIN coefficient matrix from the words of
+// table_coeffs. Caller brackets with lds_barrier().
 // Multiplication by a constant is linear over GF(2), so row (i, h, nib) = XOR of the products of
 // C[.][i] with the set bits of nib << 4h: thread (i, h, output quad q) forms the 4 basis words
 // { C[4q+jj][i] * x^(4h+k) : jj < 4 } (xtime chains) and the 16 rows' dwords q by one XOR each
 // (nib & (nib-1) is nib minus its lowest bit), writing replica 0; a second pass copies each
 // 16-byte row into replicas 1..15. ~30 VALU per thread instead of 5120 bit-serial multiplies.
 template <int NIN, int NOUT>
-__device__ __forceinline__ void build_tables(uint8_t *lds, const uint8_t *M, uint32_t ldm, uint32_t poly) {
-    for (uint32_t p = threadIdx.x; p < NIN * 8; p += WG) {
+__device__ __forceinline__ void build_tables(uint8_t *lds, uint32_t cw, uint32_t poly) {
+    const uint32_t p = threadIdx.x;
+    if (p < NIN * 8) {
         const uint32_t q = p & 3u, h = (p >> 2) & 1u, i = p >> 3;
         uint32_t bw[4] = {0, 0, 0, 0};
 #pragma unroll
         for (uint32_t jj = 0; jj < 4; jj++) {
-            const uint32_t j = 4 * q + jj;
-            uint32_t c = j < (uint32_t)NOUT ? M[j * ldm + i] : 0u;
+            uint32_t c = (cw >> (8 * jj)) & 0xFFu;
             if (h) {
 #pragma unroll
                 for (int k = 0; k < 4; k++) c = (c << 1) ^ ((c & 0x80u) ? poly : 0u);
@@ -309,6 +334,7 @@ __device__ __forceinline__ void combine_block(const uint8_t *lds, uint32_t laneo
         lookups_asm<T, NIN>(std::make_integer_sequence<int, 4 * NIN>{}, acc, x, laneoff, ibase, ioff, ncol0);
     else
         lookups_compiled<T, NIN>(acc, x, lds, laneoff, ibase, ioff, ncol0);
+    if constexpr (T::SYNC == 2) __builtin_amdgcn_s_barrier();  // the 4 waves store the tile together
     // columns x outputs -> outputs x columns
 #pragma unroll
     for (int q = 0; q < 4; q++) {
@@ -327,62 +353,125 @@ __device__ __forceinline__ void combine_block(const uint8_t *lds, uint32_t laneo
 }
 
 // ---- work split ---------------------------------------------------------------------------------
-// SUPER == 0: the n*256 tiles (256 lane blocks = 4096 columns each) are divided into equal
-// contiguous ranges, one per resident workgroup (each workgroup rebuilds its LDS tables only when
-// its range crosses into the next chunkset).
-// SUPER > 0: super-tiles of SUPER consecutive tiles of one chunkset are dealt round-robin to the
-// workgroups, so at any moment the resident workgroups sweep a few whole chunksets side by side
-// (every coded row written by many workgroups at once) at the price of a table rebuild per
-// super-tile.
-#ifndef DECDS_ENC_SUPER
-#define DECDS_ENC_SUPER 0
+// The n*256 tiles (256 lane blocks = 4096 columns each) are walked in one of three orders:
+// MAP == 0: equal contiguous ranges, one per resident workgroup (each workgroup rebuilds its LDS
+//   tables only when its range crosses into the next chunkset).
+// MAP > 0: super-tiles of MAP consecutive tiles of one chunkset dealt round-robin to the
+//   workgroups, so the resident workgroups sweep a few whole chunksets side by side, at the price
+//   of a table rebuild per super-tile.
+// MAP == MAP_BAND: XCD bands. The dispatcher deals workgroups round-robin over the 8 XCDs
+//   (workgroup b runs on XCD b % 8, cdna_hip_programming.md T1), so the P = grid / 8 workgroups of
+//   XCD x sweep chunksets x, x + 8, x + 16, ... one at a time, workgroup q = b / 8 taking tiles
+//   q, q + P, q + 2P, ...: at any moment each XCD reads and writes one contiguous band of P tiles
+//   (P x 4 KiB of every row) of one chunkset; the DRAM sees 8 x 26 wide streams instead of
+//   512 x 26 narrow ones. Needs grid % 8 == 0 and n close to a multiple of 8 (launcher checks).
+constexpr int MAP_BAND = -1;
+constexpr uint32_t NXCD = 8;
+#ifndef DECDS_ENC_MAP
+#define DECDS_ENC_MAP 0
 #endif
-#ifndef DECDS_DEC_SUPER
-#define DECDS_DEC_SUPER 8
+#ifndef DECDS_DEC_MAP
+#define DECDS_DEC_MAP 8
 #endif
+#ifndef DECDS_ENC_SHARE
+#define DECDS_ENC_SHARE 500
+#endif
+#ifndef DECDS_DEC_SHARE
+#define DECDS_DEC_SHARE 500
+#endif
+// Contiguous tile range of this workgroup. The grid is 2 workgroups per CU: workgroups
+// [0, grid/2) are dispatched first (one per CU) and their waves are older than those of their CU
+// partner in [grid/2, grid); the SIMDs arbitrate by age, so the first half runs faster
+// (per-wave stamps, tools/tracebench.py: 8-17 % at n = 103 / 1639). SHARE (per mille) is the part
+// of the tiles the first half takes, so both halves finish together (500 = equal ranges).
+template <uint32_t SHARE>
 __device__ __forceinline__ void tile_range(size_t n, uint32_t &t0, uint32_t &t1) {
     const uint64_t total = (uint64_t)n * TILES_PER_CS;
-    t0 = (uint32_t)(total * blockIdx.x / gridDim.x);
-    t1 = (uint32_t)(total * (blockIdx.x + 1) / gridDim.x);
-}
-
-// calls f(chunkset, tile, next_is_consecutive) for this workgroup's tiles in order
-template <uint32_t S, class Fn>
-__device__ __forceinline__ void walk_tiles(size_t n, Fn &&f) {
-    if constexpr (S == 0) {
-        uint32_t t0, t1;
-        tile_range(n, t0, t1);
-        for (uint32_t t = t0; t < t1; t++) f(t / TILES_PER_CS, t % TILES_PER_CS, t + 1 < t1 && (t + 1) % TILES_PER_CS != 0);
+    const uint32_t h = gridDim.x / 2, b = blockIdx.x;
+    if (SHARE == 500 || (gridDim.x & 1u)) {
+        t0 = (uint32_t)(total * b / gridDim.x);
+        t1 = (uint32_t)(total * (b + 1) / gridDim.x);
     } else {
-        static_assert(TILES_PER_CS % S == 0, "super-tile size");
-        constexpr uint32_t SPC = TILES_PER_CS / S;
-        const uint32_t total = (uint32_t)n * SPC;
-        for (uint32_t st = blockIdx.x; st < total; st += gridDim.x) {
-            const uint32_t cs = st / SPC, tb = (st % SPC) * S;
-            for (uint32_t k = 0; k < S; k++) f(cs, tb + k, k + 1 < S);
+        const uint64_t first = total * SHARE / 1000;
+        if (b < h) {
+            t0 = (uint32_t)(first * b / h);
+            t1 = (uint32_t)(first * (b + 1) / h);
+        } else {
+            t0 = (uint32_t)(first + (total - first) * (b - h) / h);
+            t1 = (uint32_t)(first + (total - first) * (b - h + 1) / h);
         }
     }
 }
 
+// Calls f(chunkset, tile, step, next, next_chunkset) for this workgroup's tiles in order: when
+// `next`, the workgroup's following tile is tile + step of the same chunkset; next_chunkset is the
+// chunkset it visits after the current one (>= n: none), for loading its coefficients early.
+template <int MAP, uint32_t SHARE = 500, class Fn>
+__device__ __forceinline__ void walk_tiles(size_t n, Fn &&f) {
+    if constexpr (MAP == 0) {
+        uint32_t t0, t1;
+        tile_range<SHARE>(n, t0, t1);
+        for (uint32_t t = t0; t < t1; t++) {
+            const uint32_t cs = t / TILES_PER_CS, tile = t % TILES_PER_CS;
+            f(cs, tile, 1u, t + 1 < t1 && tile + 1 < TILES_PER_CS,
+              (cs + 1) * TILES_PER_CS < t1 ? cs + 1 : 0xFFFFFFFFu);
+        }
+    } else if constexpr (MAP > 0) {
+        static_assert(TILES_PER_CS % MAP == 0, "super-tile size");
+        constexpr uint32_t SPC = TILES_PER_CS / MAP;
+        const uint32_t total = (uint32_t)n * SPC;
+        for (uint32_t st = blockIdx.x; st < total; st += gridDim.x) {
+            const uint32_t cs = st / SPC, tb = (st % SPC) * MAP;
+            const uint32_t ncs = st + gridDim.x < total ? (st + gridDim.x) / SPC : 0xFFFFFFFFu;
+            for (uint32_t k = 0; k < (uint32_t)MAP; k++) f(cs, tb + k, 1u, k + 1 < (uint32_t)MAP, ncs);
+        }
+    } else {
+        static_assert(MAP == MAP_BAND, "work map");
+        const uint32_t P = gridDim.x / NXCD, x = blockIdx.x % NXCD, q = blockIdx.x / NXCD;
+        if (q >= P) return;
+        for (uint32_t cs = x; cs < n; cs += NXCD)
+            for (uint32_t tile = q; tile < TILES_PER_CS; tile += P) f(cs, tile, P, tile + P < TILES_PER_CS, cs + NXCD);
+    }
+}
+
 // One tile for this lane: inputs were prefetched by the previous tile when `have` (ROLL), else
-// they are loaded now; `next` says whether the following tile is the next one of this chunkset.
+// they are loaded now; `next` says whether the following tile is tile + step of this chunkset.
 template <class T, int NIN, int NOUT>
-__device__ __forceinline__ void stream_tile(const uint8_t *lds, uint32_t laneoff, uint32_t tile, bool next,
-                                            const uint8_t *ibase, const uint32_t (&ioff)[NIN], uint8_t *obase,
-                                            const uint32_t (&ooff)[NOUT], uint4 (&x)[NIN], bool &have) {
+__device__ __forceinline__ void stream_tile(const uint8_t *lds, uint32_t laneoff, uint32_t tile, uint32_t step,
+                                            bool next, const uint8_t *ibase, const uint32_t (&ioff)[NIN],
+                                            uint8_t *obase, const uint32_t (&ooff)[NOUT], uint4 (&x)[NIN],
+                                            bool &have) {
+    if constexpr (T::SYNC == 1) __builtin_amdgcn_s_barrier();  // the 4 waves start the tile together
     const uint32_t block = tile * TILE_BLOCKS + threadIdx.x;
     const bool active = block < MAIN_BLOCKS;
     if (!(T::ROLL && have) && active) load_block<T, NIN>(x, ibase, ioff, block * COLS_PER_LANE);
     have = next;
-    const uint32_t nblock = block + TILE_BLOCKS;
+    const uint32_t nblock = block + step * TILE_BLOCKS;
     // branch-free prefetch: lanes with no next block re-load their own block (an L2 hit)
     const uint32_t ncol0 = (have && nblock < MAIN_BLOCKS ? nblock : block) * COLS_PER_LANE;
     if (active) combine_block<T, NIN, NOUT>(lds, laneoff, x, obase, ooff, block * COLS_PER_LANE, ibase, ioff, ncol0);
 }
 
+// Timing-study builds only (DECDS_TIMING_TRACE): every wave stamps its start and end with the
+// 100 MHz real-time counter; decds_debug_trace copies the stamps out (kernel 0 encode, 1 decode).
+#ifdef DECDS_TIMING_TRACE
+constexpr uint32_t TRACE_WAVES = 4096;
+__device__ uint64_t g_trace[2][2 * TRACE_WAVES];
+#define TRACE_BEGIN(k)                                                                              \
+    const uint32_t trace_w_ = blockIdx.x * (WG / 64) + threadIdx.x / 64;                            \
+    if ((threadIdx.x & 63u) == 0 && trace_w_ < TRACE_WAVES) g_trace[k][2 * trace_w_] = __builtin_amdgcn_s_memrealtime()
+#define TRACE_END(k) \
+    if ((threadIdx.x & 63u) == 0 && trace_w_ < TRACE_WAVES) g_trace[k][2 * trace_w_ + 1] = __builtin_amdgcn_s_memrealtime()
+#else
+#define TRACE_BEGIN(k)
+#define TRACE_END(k)
+#endif
+
+template <int MAP>
 __global__ __launch_bounds__(WG, WAVES_PER_SIMD) __attribute__((amdgpu_waves_per_eu(WAVES_PER_SIMD, WAVES_PER_SIMD)))
 void rlnc_encode_kernel(const uint8_t *__restrict__ src, size_t n, const uint8_t *__restrict__ coeffs,
                         uint8_t *__restrict__ dst, size_t pitch, uint32_t poly, uint32_t marker) {
+    TRACE_BEGIN(0);
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t laneoff = (lane & 15u) * 16u;
@@ -397,14 +486,22 @@ void rlnc_encode_kernel(const uint8_t *__restrict__ src, size_t n, const uint8_t
     const uint8_t *M = coeffs;
     uint4 x[K];
     bool have = false;
-    walk_tiles<DECDS_ENC_SUPER>(n, [&](uint32_t cs, uint32_t tile, bool next) {
+    [[maybe_unused]] bool built = false;
+    walk_tiles<MAP, DECDS_ENC_SHARE>(n, [&](uint32_t cs, uint32_t tile, uint32_t step, bool next, uint32_t) {
         if (cs != cur) {
             cur = cs;
             have = false;
             M = coeffs + (size_t)cs * N * K;
-            lds_barrier();
-            build_tables<K, N>(lds, M, K, poly);
-            lds_barrier();
+            const uint32_t cw = table_coeffs<K, N>(M, K);
+#ifdef DECDS_TIMING_NOREBUILD  // timing study only: keep the first chunkset's tables (wrong output)
+            if (!built)
+#endif
+            {
+                lds_barrier();
+                build_tables<K, N>(lds, cw, poly);
+                lds_barrier();
+                built = true;
+            }
             ibase = src + (size_t)cs * CS;
             obase = dst + (size_t)cs * N * pitch;
         }
@@ -424,13 +521,16 @@ void rlnc_encode_kernel(const uint8_t *__restrict__ src, size_t n, const uint8_t
                 obase[j * pitch + K + col] = (uint8_t)y;
             }
         }
-        stream_tile<EncTune, K, N>(lds, laneoff, tile, next, ibase, ioff, obase, ooff, x, have);
+        stream_tile<EncTune, K, N>(lds, laneoff, tile, step, next, ibase, ioff, obase, ooff, x, have);
     });
+    TRACE_END(0);
 }
 
+template <int MAP>
 __global__ __launch_bounds__(WG, WAVES_PER_SIMD) __attribute__((amdgpu_waves_per_eu(WAVES_PER_SIMD, WAVES_PER_SIMD)))
 void rlnc_decode_kernel(const uint8_t *__restrict__ coded, size_t pitch, size_t n, const RepairPlan *__restrict__ plan,
                         uint8_t *__restrict__ dst, int32_t *__restrict__ status, uint32_t poly, uint32_t marker) {
+    TRACE_BEGIN(1);
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t laneoff = (lane & 15u) * 16u;
@@ -445,21 +545,28 @@ void rlnc_decode_kernel(const uint8_t *__restrict__ coded, size_t pitch, size_t 
     uint8_t *obase = dst;
     uint4 x[K];
     bool have = false;
-    walk_tiles<DECDS_DEC_SUPER>(n, [&](uint32_t cs, uint32_t tile, bool next) {
+    [[maybe_unused]] bool built = false;
+    walk_tiles<MAP, DECDS_DEC_SHARE>(n, [&](uint32_t cs, uint32_t tile, uint32_t step, bool next, uint32_t) {
         if (cs != cur) {
             cur = cs;
             have = false;
-            const RepairPlan *pl = plan + cs;
             // plan words are wave-uniform: keep them in SGPRs
-            const uint32_t *pw = reinterpret_cast<const uint32_t *>(pl);
+            const uint32_t *pw = reinterpret_cast<const uint32_t *>(plan + cs);
             const uint32_t w0 = __builtin_amdgcn_readfirstlane(pw[0]);
             const uint32_t w1 = __builtin_amdgcn_readfirstlane(pw[1]);
             const uint32_t w2 = __builtin_amdgcn_readfirstlane(pw[2]);
             ready = ((w2 >> 16) & 0xFFu) == K;  // RepairPlan::rank at byte 10
             if (ready) {
-                lds_barrier();
-                build_tables<K, K>(lds, pl->inv, K, poly);
-                lds_barrier();
+                const uint32_t cw = table_coeffs<K, K>(plan[cs].inv, K);
+#ifdef DECDS_TIMING_NOREBUILD  // timing study only: keep the first chunkset's tables (wrong output)
+                if (!built)
+#endif
+                {
+                    lds_barrier();
+                    build_tables<K, K>(lds, cw, poly);
+                    lds_barrier();
+                    built = true;
+                }
                 const uint32_t sel[K] = {w0 & 0xFFu, (w0 >> 8) & 0xFFu, (w0 >> 16) & 0xFFu, w0 >> 24,
                                          w1 & 0xFFu, (w1 >> 8) & 0xFFu, (w1 >> 16) & 0xFFu, w1 >> 24,
                                          w2 & 0xFFu, (w2 >> 8) & 0xFFu};
@@ -487,9 +594,17 @@ void rlnc_decode_kernel(const uint8_t *__restrict__ coded, size_t pitch, size_t 
             }
             if (__any(!ok) && lane == 0) status[cs] = 6;  // DECDS_ERR_CHUNKSET_REPAIRING_FAILED
         }
-        stream_tile<DecTune, K, K>(lds, laneoff, tile, next, ibase, ioff, obase, ooff, x, have);
+        stream_tile<DecTune, K, K>(lds, laneoff, tile, step, next, ibase, ioff, obase, ooff, x, have);
     });
+    TRACE_END(1);
 }
+
+#ifdef DECDS_TIMING_TRACE
+extern "C" int decds_debug_trace(int kernel, uint64_t *out) {
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_trace), sizeof(g_trace[0]), (size_t)kernel * sizeof(g_trace[0]),
+                                    hipMemcpyDeviceToHost);
+}
+#endif
 
 // x * f for a per-lane x and a wave-uniform f: the branches test bits of f, so they are scalar
 __device__ __forceinline__ uint32_t gf_mul_uniform(uint32_t x, uint32_t f, uint32_t poly) {
@@ -638,20 +753,41 @@ static uint32_t stream_grid(const LaunchGeom &g, size_t n) {
     return (uint32_t)(tiles < grid ? tiles : grid);
 }
 
+// The band walk needs whole XCD groups and a batch that splits evenly enough over the 8 XCDs
+// (at most 5 % of XCD-rounds idle); other batches take the fallback map.
+static bool band_ok(uint32_t grid, size_t n) {
+    return grid >= NXCD && grid % NXCD == 0 && ((NXCD - n % NXCD) % NXCD) * 20 <= n;
+}
+constexpr int ENC_MAP_FALLBACK = 0, DEC_MAP_FALLBACK = 8;
+
 hipError_t configure_kernels() {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(rlnc_encode_kernel),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
-    if (e != hipSuccess) return e;
-    return hipFuncSetAttribute(reinterpret_cast<const void *>(rlnc_decode_kernel),
-                               hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+    const void *fns[] = {reinterpret_cast<const void *>(rlnc_encode_kernel<DECDS_ENC_MAP>),
+                         reinterpret_cast<const void *>(rlnc_encode_kernel<ENC_MAP_FALLBACK>),
+                         reinterpret_cast<const void *>(rlnc_decode_kernel<DECDS_DEC_MAP>),
+                         reinterpret_cast<const void *>(rlnc_decode_kernel<DEC_MAP_FALLBACK>)};
+    for (const void *f : fns) {
+        hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 
 hipError_t launch_encode(const LaunchGeom &g, const uint8_t *src, size_t n, const uint8_t *coeffs,
                          uint8_t *dst, size_t pitch, uint32_t poly, uint32_t marker,
                          hipStream_t stream) {
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(rlnc_encode_kernel, dim3(stream_grid(g, n)), dim3(WG), LDS_BYTES, stream, src, n,
-                       coeffs, dst, pitch, poly, marker);
+    uint32_t grid = stream_grid(g, n);
+    if (DECDS_ENC_MAP == MAP_BAND && band_ok(grid & ~(NXCD - 1), n)) {
+        grid &= ~(NXCD - 1);
+        hipLaunchKernelGGL(rlnc_encode_kernel<DECDS_ENC_MAP>, dim3(grid), dim3(WG), LDS_BYTES, stream, src, n,
+                           coeffs, dst, pitch, poly, marker);
+    } else if (DECDS_ENC_MAP != MAP_BAND) {
+        hipLaunchKernelGGL(rlnc_encode_kernel<DECDS_ENC_MAP>, dim3(grid), dim3(WG), LDS_BYTES, stream, src, n,
+                           coeffs, dst, pitch, poly, marker);
+    } else {
+        hipLaunchKernelGGL(rlnc_encode_kernel<ENC_MAP_FALLBACK>, dim3(grid), dim3(WG), LDS_BYTES, stream, src, n,
+                           coeffs, dst, pitch, poly, marker);
+    }
     return hipGetLastError();
 }
 
@@ -668,8 +804,19 @@ hipError_t launch_decode(const LaunchGeom &g, const uint8_t *coded, size_t pitch
                          const uint8_t *plan, uint8_t *dst, int32_t *status, uint32_t poly,
                          uint32_t marker, hipStream_t stream) {
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(rlnc_decode_kernel, dim3(stream_grid(g, n)), dim3(WG), LDS_BYTES, stream, coded,
-                       pitch, n, reinterpret_cast<const RepairPlan *>(plan), dst, status, poly, marker);
+    uint32_t grid = stream_grid(g, n);
+    const RepairPlan *pl = reinterpret_cast<const RepairPlan *>(plan);
+    if (DECDS_DEC_MAP == MAP_BAND && band_ok(grid & ~(NXCD - 1), n)) {
+        grid &= ~(NXCD - 1);
+        hipLaunchKernelGGL(rlnc_decode_kernel<DECDS_DEC_MAP>, dim3(grid), dim3(WG), LDS_BYTES, stream, coded, pitch,
+                           n, pl, dst, status, poly, marker);
+    } else if (DECDS_DEC_MAP != MAP_BAND) {
+        hipLaunchKernelGGL(rlnc_decode_kernel<DECDS_DEC_MAP>, dim3(grid), dim3(WG), LDS_BYTES, stream, coded, pitch,
+                           n, pl, dst, status, poly, marker);
+    } else {
+        hipLaunchKernelGGL(rlnc_decode_kernel<DEC_MAP_FALLBACK>, dim3(grid), dim3(WG), LDS_BYTES, stream, coded,
+                           pitch, n, pl, dst, status, poly, marker);
+    }
     return hipGetLastError();
 }
 

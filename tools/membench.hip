@@ -24,7 +24,7 @@ __global__ __launch_bounds__(WG, WAVES_PER_SIMD) void pattern_kernel(const uint8
                                                                    uint8_t *__restrict__ dst, Geom g,
                                                                    uint4 *__restrict__ sink) {
     uint32_t t0, t1;
-    tile_range(n, t0, t1);
+    tile_range<500>(n, t0, t1);
     uint32_t ioff[K], ooff[N];
 #pragma unroll
     for (int i = 0; i < (int)K; i++) ioff[i] = (uint32_t)(i * g.istride);
@@ -99,7 +99,7 @@ template <int NP>
 __global__ __launch_bounds__(WG, WAVES_PER_SIMD) void pattern_np_kernel(const uint8_t *__restrict__ src, size_t n,
                                                                       uint8_t *__restrict__ dst, Geom g) {
     uint32_t t0, t1;
-    tile_range(n, t0, t1);
+    tile_range<500>(n, t0, t1);
     uint32_t ioff[K], ooff[N];
 #pragma unroll
     for (int i = 0; i < (int)K; i++) ioff[i] = (uint32_t)(i * g.istride);
