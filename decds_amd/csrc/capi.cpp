@@ -95,6 +95,7 @@ int decds_ctx_create(int device, decds_ctx **out) {
     c->device = device;
     c->poly = POLY_DEFAULT;
     c->marker = (uint8_t)MARKER_DEFAULT;
+    c->gen = host_gf_generator(POLY_DEFAULT);
     c->geom.num_cus = prop.multiProcessorCount;
     if (const char *w = std::getenv("DECDS_WGS_PER_CU")) c->geom.wgs_per_cu = std::atoi(w) == 1 ? 1 : 2;
     *out = c;
@@ -110,6 +111,9 @@ int decds_ctx_set_field(decds_ctx *ctx, uint32_t poly, uint8_t marker) {
     if (!ctx) return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "null context");
     if (poly < 0x100 || poly > 0x1FF) return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "poly must be degree 8");
     if (marker == 0) return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "marker must be non-zero");
+    const uint32_t gen = host_gf_generator(poly);
+    if (gen == 0) return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "poly 0x%X is reducible: no GF(2^8)", poly);
+    ctx->gen = gen;
     ctx->poly = poly;
     ctx->marker = marker;
     return DECDS_OK;
@@ -154,7 +158,7 @@ int decds_repair_plan_batch(decds_ctx *ctx, const uint8_t *coded, size_t coded_p
     if (!coded || !cand || !plan || !verdicts || !status)
         return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "null buffer");
     hipError_t e = launch_repair_plan(coded, coded_pitch, n, cand, plan, verdicts, status, ctx->poly,
-                                      (hipStream_t)stream);
+                                      ctx->gen, (hipStream_t)stream);
     return e == hipSuccess ? DECDS_OK : decds_hip_error(e, "rlnc_plan_kernel launch");
 }
 

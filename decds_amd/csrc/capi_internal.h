@@ -9,6 +9,7 @@ struct decds_ctx {
     int device;
     uint32_t poly;     // GF(2^8) polynomial incl. x^8 (rlnc 0.4.0: 0x11D [recalled])
     uint8_t marker;    // boundary marker appended by rlnc Encoder::new (0x81 [recalled])
+    uint32_t gen;      // smallest generator of GF(2^8)* under poly (the plan kernel's log/exp tables)
     decds::LaunchGeom geom;
 };
 
@@ -20,4 +21,6 @@ namespace decds {
 // host-side GF(2^8) helpers for the 10-byte coding vectors (control path, not the hot path)
 uint8_t host_gf_mul(uint8_t a, uint8_t b, uint32_t poly);
 uint8_t host_gf_inv(uint8_t a, uint32_t poly);
+// smallest element of multiplicative order 255, or 0 when poly is reducible (no field)
+uint32_t host_gf_generator(uint32_t poly);
 }  // namespace decds

@@ -28,6 +28,22 @@ uint8_t host_gf_inv(uint8_t a, uint32_t poly) {
     return a ? r : 0;
 }
 
+uint32_t host_gf_generator(uint32_t poly) {
+    for (uint32_t g = 2; g < 256; g++) {
+        // order 255 = 3 * 5 * 17 iff g^(255/p) != 1 for each prime p, and g^255 == 1
+        auto pw = [&](uint32_t e) {
+            uint8_t r = 1, b = (uint8_t)g;
+            for (; e; e >>= 1) {
+                if (e & 1u) r = host_gf_mul(r, b, poly);
+                b = host_gf_mul(b, b, poly);
+            }
+            return r;
+        };
+        if (pw(255) == 1 && pw(85) != 1 && pw(51) != 1 && pw(15) != 1) return g;
+    }
+    return 0;
+}
+
 }  // namespace decds
 
 using namespace decds;

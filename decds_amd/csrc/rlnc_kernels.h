@@ -17,7 +17,7 @@ hipError_t launch_encode(const LaunchGeom &g, const uint8_t *src, size_t n, cons
                          hipStream_t stream);
 hipError_t launch_repair_plan(const uint8_t *coded, size_t pitch, size_t n, const uint8_t *cand,
                               uint8_t *plan, int8_t *verdicts, int32_t *status, uint32_t poly,
-                              hipStream_t stream);
+                              uint32_t gen, hipStream_t stream);
 hipError_t launch_decode(const LaunchGeom &g, const uint8_t *coded, size_t pitch, size_t n,
                          const uint8_t *plan, uint8_t *dst, int32_t *status, uint32_t poly,
                          uint32_t marker, hipStream_t stream);

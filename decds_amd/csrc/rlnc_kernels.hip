@@ -74,16 +74,6 @@ __device__ __forceinline__ uint32_t gf_mul(uint32_t a, uint32_t b, uint32_t poly
     return acc & 0xFFu;
 }
 
-__device__ __forceinline__ uint32_t gf_inv(uint32_t a, uint32_t poly) {  // a^254
-    uint32_t r = 1;
-#pragma unroll
-    for (int e = 0; e < 8; e++) {
-        if (254u & (1u << e)) r = gf_mul(r, a, poly);
-        a = gf_mul(a, a, poly);
-    }
-    return r;
-}
-
 // Workgroup barrier for the LDS tables only: every wave's LDS accesses have completed, nothing
 // else. __syncthreads() also drains each wave's outstanding global stores (a release fence), which
 // made every table rebuild cost a full store-queue drain.
@@ -606,17 +596,6 @@ extern "C" int decds_debug_trace(int kernel, uint64_t *out) {
 }
 #endif
 
-// x * f for a per-lane x and a wave-uniform f: the branches test bits of f, so they are scalar
-__device__ __forceinline__ uint32_t gf_mul_uniform(uint32_t x, uint32_t f, uint32_t poly) {
-    uint32_t acc = 0;
-#pragma unroll
-    for (int i = 0; i < 8; i++) {
-        if (f & (1u << i)) acc ^= x;
-        x = (x << 1) ^ ((x & 0x80u) ? poly : 0u);
-    }
-    return acc & 0xFFu;
-}
-
 // One wave per chunkset. Replays rlnc's incremental rank test over the candidates' 10-byte coding
 // vectors in arrival order (chunkset.rs:173-184: a piece is accepted iff it raises the rank;
 // after rank 10 every further piece is "ready to repair") and, in the same pass, inverts the
@@ -627,31 +606,56 @@ __device__ __forceinline__ uint32_t gf_mul_uniform(uint32_t x, uint32_t f, uint3
 // all reductions of one step are independent (ILP across the basis instead of a serial chain).
 // At rank 10 the coefficient parts are unit vectors e_piv, so B = E·R = P and R^-1 = Pᵀ·E: row i
 // of the inverse is the combination part of the basis row whose pivot is column i.
+// Products use log / exp tables of the generator `gen` in LDS: x * f = exp[log x + log f] — one
+// table read per product, and the products of one step are independent reads (a bit-serial
+// multiply by a wave-uniform factor is a chain of 8 scalar branches).
 __global__ __launch_bounds__(64) void rlnc_plan_kernel(const uint8_t *__restrict__ coded, size_t pitch, size_t n,
                                                        const uint8_t *__restrict__ cand,
                                                        RepairPlan *__restrict__ plan,
                                                        int8_t *__restrict__ verdicts,
-                                                       int32_t *__restrict__ status, uint32_t poly) {
+                                                       int32_t *__restrict__ status, uint32_t poly,
+                                                       uint32_t gen) {
     const size_t cs = blockIdx.x;
     const uint32_t lane = threadIdx.x;
     const bool col = lane < K;
-    // GF(2^8) inverses for this polynomial: 4 per lane, computed in parallel once
-    __shared__ uint8_t inv_tab[256];
-#pragma unroll
-    for (int q = 0; q < 4; q++) inv_tab[lane * 4 + q] = (uint8_t)gf_inv(lane * 4 + q, poly);
-    // all candidates' row ids and coding vectors up front (one memory latency, not sixteen):
-    // lane c < 10 holds byte c of every candidate's coding vector
+    // the arrival order, and the 10-byte coding vector of every coded row of the chunkset (lane
+    // c < 10 loads byte c of rows 0..15): both in flight while the tables below are built
     const uint32_t my_cand = lane < N ? cand[cs * N + lane] : (uint32_t)DECDS_NO_CANDIDATE_U8;
-    uint32_t cvs[N];
+    uint32_t rowcv[N];
 #pragma unroll
-    for (int a = 0; a < (int)N; a++) {
-        const uint32_t r = __builtin_amdgcn_readlane(my_cand, a);
-        cvs[a] = (col && r < N) ? coded[(cs * N + r) * pitch + lane] : 0u;
+    for (int r = 0; r < (int)N; r++) rowcv[r] = col ? coded[(cs * N + r) * pitch + lane] : 0u;
+    // exp[i] = gen^i for i < 510 (doubled: exp[log a + log b] needs no reduction mod 255),
+    // log[gen^i] = i. Lane l starts at gen^(4l) (square-and-multiply) and steps 4 times.
+    __shared__ uint8_t s_exp[512], s_log[256], s_cv[N * 16];
+    {
+        uint32_t v = 1, b = gen;
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            if ((4 * lane >> k) & 1u) v = gf_mul(v, b, poly);
+            b = gf_mul(b, b, poly);
+        }
+#pragma unroll
+        for (uint32_t q = 0; q < 4; q++) {
+            const uint32_t i = 4 * lane + q;
+            if (i < 255) {
+                s_exp[i] = (uint8_t)v;
+                s_exp[i + 255] = (uint8_t)v;
+                s_log[v] = (uint8_t)i;
+            }
+            v = gf_mul(v, gen, poly);
+        }
+        if (lane == 0) s_log[0] = 0;  // log 0 is never used unmasked; keep the reads defined
+    }
+    if (col) {
+#pragma unroll
+        for (int r = 0; r < (int)N; r++) s_cv[r * 16 + lane] = (uint8_t)rowcv[r];
     }
     __syncthreads();
-    uint32_t basis[K], piv[K], sel[K];
+    // Every term below is computed unconditionally and masked by selects: no branch splits the
+    // ten independent table reads of a step, so they are all in flight together.
+    uint32_t basis[K], lgb[K], piv[K], sel[K];  // lgb[e] = log basis[e] (masked where basis[e] == 0)
 #pragma unroll
-    for (int e = 0; e < (int)K; e++) basis[e] = piv[e] = sel[e] = 0;
+    for (int e = 0; e < (int)K; e++) basis[e] = lgb[e] = piv[e] = sel[e] = 0;
     uint32_t rank = 0;
     bool ended = false;
     int32_t my_verdict = -1;  // lane a < 16 keeps candidate a's verdict
@@ -665,31 +669,29 @@ __global__ __launch_bounds__(64) void rlnc_plan_kernel(const uint8_t *__restrict
         } else if (rank == K) {
             v = 3;  // DECDS_ERR_CHUNKSET_READY_TO_REPAIR
         } else {
-            const uint32_t cv = cvs[a];
-            // augmented row [cv | unit(rank)]
+            const uint32_t cv = col ? s_cv[r * 16 + lane] : 0u;
+            // augmented row [cv | unit(rank)] minus its projection on the basis
             uint32_t row = col ? cv : (lane == K + rank ? 1u : 0u);
-            uint32_t red = 0;
 #pragma unroll
             for (int e = 0; e < (int)K; e++) {
-                if (e < (int)rank) {
-                    const uint32_t f = __builtin_amdgcn_readlane(cv, piv[e]);
-                    red ^= gf_mul_uniform(basis[e], f, poly);
-                }
+                const uint32_t f = e < (int)rank ? __builtin_amdgcn_readlane(cv, piv[e]) : 0u;
+                const uint32_t t = s_exp[lgb[e] + s_log[f]];
+                row ^= (f != 0 && basis[e] != 0) ? t : 0u;
             }
-            row ^= red;
             const uint64_t nz = __ballot(col && row != 0);
             if (!nz) {
                 v = 4;  // DECDS_ERR_CHUNK_DECODING_FAILED: piece not useful
             } else {
                 const uint32_t p = __builtin_ctzll(nz);
-                const uint32_t inv = inv_tab[__builtin_amdgcn_readlane(row, p)];
-                row = gf_mul_uniform(row, inv, poly);
+                // row /= row[p]: log of the inverse = 255 - log (exp is doubled, so 255 is fine)
+                const uint32_t linv = 255u - s_log[__builtin_amdgcn_readlane(row, p)];
+                row = row ? s_exp[s_log[row] + linv] : 0u;
+                const uint32_t lrow = s_log[row];
 #pragma unroll
                 for (int e = 0; e < (int)K; e++) {
-                    if (e < (int)rank) {
-                        const uint32_t f = __builtin_amdgcn_readlane(basis[e], p);
-                        basis[e] ^= gf_mul_uniform(row, f, poly);
-                    }
+                    const uint32_t f = e < (int)rank ? __builtin_amdgcn_readlane(basis[e], p) : 0u;
+                    const uint32_t t = s_exp[lrow + s_log[f]];
+                    basis[e] ^= (f != 0 && row != 0) ? t : 0u;
                 }
 #pragma unroll
                 for (int e = 0; e < (int)K; e++) {
@@ -698,6 +700,7 @@ __global__ __launch_bounds__(64) void rlnc_plan_kernel(const uint8_t *__restrict
                         piv[e] = p;
                         sel[e] = r;
                     }
+                    lgb[e] = s_log[basis[e]];
                 }
                 rank++;
                 v = 0;
@@ -793,10 +796,10 @@ hipError_t launch_encode(const LaunchGeom &g, const uint8_t *src, size_t n, cons
 
 hipError_t launch_repair_plan(const uint8_t *coded, size_t pitch, size_t n, const uint8_t *cand,
                               uint8_t *plan, int8_t *verdicts, int32_t *status, uint32_t poly,
-                              hipStream_t stream) {
+                              uint32_t gen, hipStream_t stream) {
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(rlnc_plan_kernel, dim3((uint32_t)n), dim3(64), 0, stream, coded,
-                       pitch, n, cand, reinterpret_cast<RepairPlan *>(plan), verdicts, status, poly);
+                       pitch, n, cand, reinterpret_cast<RepairPlan *>(plan), verdicts, status, poly, gen);
     return hipGetLastError();
 }
 

@@ -64,7 +64,8 @@ typedef struct decds_ctx decds_ctx;
 int decds_ctx_create(int device, decds_ctx **out);
 int decds_ctx_destroy(decds_ctx *ctx);
 /* GF(2^8) polynomial (with the x^8 bit, e.g. 0x11D) and boundary marker used by rlnc 0.4.0.
- * Defaults 0x11D / 0x81. Exposed so an identification run can re-pin them. */
+ * Defaults 0x11D / 0x81. Exposed so an identification run can re-pin them. The
+ * polynomial must be irreducible (a reducible one is no field: DECDS_ERR_INVALID_ARGUMENT). */
 int decds_ctx_set_field(decds_ctx *ctx, uint32_t poly, uint8_t marker);
 int decds_ctx_get_field(const decds_ctx *ctx, uint32_t *poly, uint8_t *marker);
 const char *decds_status_string(int status);
