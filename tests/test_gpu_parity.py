@@ -84,9 +84,22 @@ def test_field_parameter_other_polynomial(ctx, kat):
     ctx.set_field(0x11B, 0x81)
     try:
         coded = gpu_encode(ctx, data, coeffs, 1)
+        # repair under 0x11B too: 2 is not a generator there, so the plan kernel's log/exp tables
+        # run on the host-found generator 3
+        cand = np.array([15, 3, 8, 0, 12, 5, 9, 1, 14, 6, 2, 4, 7, 10, 11, 13], np.uint8)
+        plan = torch.empty(128, dtype=torch.uint8, device="cuda")
+        verd = torch.empty(N, dtype=torch.int8, device="cuda")
+        status = torch.empty(1, dtype=torch.int32, device="cuda")
+        out = torch.zeros(CS, dtype=torch.uint8, device="cuda")
+        codec.repair_batch(ctx, dev(coded.reshape(-1)), 1, dev(cand), plan, verd, out, status)
+        assert host(status)[0] == 0 and np.array_equal(host(out), data)
     finally:
         ctx.set_field(0x11D, 0x81)
     assert [sha(coded[j]) for j in range(N)] == kat["cfg1_poly_0x11b_coded_sha256"]
+    # a reducible polynomial is no field (x^8 + 1 = (x + 1)^8): refused, the field is unchanged
+    with pytest.raises(decds_amd.DecdsError) as e:
+        ctx.set_field(0x101, 0x81)
+    assert e.value.kind == "InvalidArgument"
 
 
 def _oracle_verdicts(coded, cand):

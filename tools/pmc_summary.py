@@ -10,10 +10,16 @@ import csv
 import glob
 import json
 import os
+import re
 import shutil
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def kname(name):
+    """'void decds::rlnc_encode_kernel<0>(...)' -> 'decds::rlnc_encode_kernel'"""
+    return re.sub(r"<[^<>]*>$", "", re.sub(r"^void ", "", name.split("(")[0]))
 
 
 def main():
@@ -26,12 +32,12 @@ def main():
     agg = collections.defaultdict(list)
     for f in glob.glob(os.path.join(src, "pmc*", "*_counter_collection.csv")):
         for r in csv.DictReader(open(f)):
-            agg[(r["Kernel_Name"].split("(")[0], r["Counter_Name"])].append(float(r["Counter_Value"]))
+            agg[(kname(r["Kernel_Name"]), r["Counter_Name"])].append(float(r["Counter_Value"]))
     summary = collections.defaultdict(dict)
     for (k, c), v in agg.items():
         if k.startswith("decds::"):
             summary[k][c] = sum(v) / len(v)
-    durations = {r["Name"].split("(")[0]: float(r["AverageNs"]) for r in csv.DictReader(open(stats))}
+    durations = {kname(r["Name"]): float(r["AverageNs"]) for r in csv.DictReader(open(stats))}
     for k in summary:
         summary[k]["avg_duration_ns"] = durations.get(k)
     with open(os.path.join(prof, "%s_pmc_summary.json" % tag), "w") as f:
