@@ -77,6 +77,44 @@ __global__ __launch_bounds__(WG, WAVES_PER_SIMD) void np_kernel(const uint8_t *_
     });
 }
 
+// MB blocks per lane: a wave covers MB consecutive KiB of every row per tile (lane block of
+// instruction m = base + 64m + lane) and stores all MB pieces of a row back to back, so
+// each row receives an MB-KiB contiguous burst from one wave at one time (contiguous tile ranges)
+template <int MB, bool ENC>
+__global__ __launch_bounds__(WG, WAVES_PER_SIMD) void mb_kernel(const uint8_t *__restrict__ src, size_t n,
+                                                               uint8_t *__restrict__ dst) {
+    constexpr int NOUT = ENC ? (int)N : (int)K;
+    constexpr uint32_t TPC = TILES_PER_CS / MB;  // tiles of MB*256 blocks
+    uint32_t ioff[K], ooff[NOUT];
+#pragma unroll
+    for (int i = 0; i < (int)K; i++) ioff[i] = ENC ? (uint32_t)(i * L) : (uint32_t)(i * F + K);
+#pragma unroll
+    for (int j = 0; j < NOUT; j++) ooff[j] = ENC ? (uint32_t)(j * F + K) : (uint32_t)(j * L);
+    const uint64_t total = (uint64_t)n * TPC;
+    const uint32_t t0 = (uint32_t)(total * blockIdx.x / gridDim.x), t1 = (uint32_t)(total * (blockIdx.x + 1) / gridDim.x);
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    for (uint32_t t = t0; t < t1; t++) {
+        const uint32_t cs = t / TPC, tile = t % TPC;
+        const uint8_t *ibase = src + (size_t)cs * (ENC ? CS : N * F);
+        uint8_t *obase = dst + (size_t)cs * (ENC ? N * F : CS);
+        uint4 x[MB][K];
+        uint32_t blk[MB];
+#pragma unroll
+        for (int m = 0; m < MB; m++) {
+            blk[m] = (tile * 4 + wave) * 64 * MB + m * 64 + lane;
+            if (blk[m] < MAIN_BLOCKS) load_block<EncTune, K>(x[m], ibase, ioff, blk[m] * COLS_PER_LANE);
+        }
+#pragma unroll
+        for (int j = 0; j < NOUT; j++)
+#pragma unroll
+            for (int m = 0; m < MB; m++) {
+                const uint4 a = x[m][j % K], b = x[m][(j + 3) % K];
+                if (blk[m] < MAIN_BLOCKS)
+                    strow<-1>(obase, ooff[j] + blk[m] * COLS_PER_LANE, make_uint4(a.x ^ b.y, a.y ^ b.z, a.z ^ b.w, a.w ^ b.x));
+            }
+    }
+}
+
 __global__ void random_fill(uint64_t *p, size_t nw) {
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < nw; i += (size_t)gridDim.x * blockDim.x) {
         uint64_t z = (i + 1) * 0x9E3779B97F4A7C15ull;
@@ -120,6 +158,8 @@ int main(int argc, char **argv) {
         CASE(2, true, 0, "enc_map2"),       CASE(32, true, 0, "enc_map32"),
         CASESY(0, true, "enc_map0_sync"),   CASESY(MAP_BAND, true, "enc_band_sync"), CASESY(8, true, "enc_map8_sync"),
         CASESY(8, false, "dec_map8_sync"),  CASESY(MAP_BAND, false, "dec_band_sync"),
+        Case{"enc_mb2", true, mb_kernel<2, true>, false, {}}, Case{"enc_mb4", true, mb_kernel<4, true>, false, {}},
+        Case{"dec_mb2", false, mb_kernel<2, false>, false, {}}, Case{"dec_mb4", false, mb_kernel<4, false>, false, {}},
         CASE(0, false, 0, "dec_map0"),      CASE(8, false, 0, "dec_map8"),      CASE(MAP_BAND, false, 0, "dec_band"),
         CASE(8, false, 5, "dec_map8_g5"),   CASE(MAP_BAND, false, 5, "dec_band_g5"), CASE(MAP_BAND, false, 10, "dec_band_drain"),
     };
