@@ -20,6 +20,7 @@ sys.path.insert(0, ROOT)
 
 GIB = float(1 << 30)
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+SWEEP = (256, 1024, 1639)  # encode batch sweep: chunksets per launch (1639 = the 16 GiB blob of cfg3)
 
 CONFIGS = {
     # name: (blob bytes per GPU, description)
@@ -43,6 +44,7 @@ def parse():
     p.add_argument("--config", default="cfg2", choices=sorted(CONFIGS))
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-commit", action="store_true", help="skip timing the commitment kernels (row f1)")
+    p.add_argument("--no-sweep", action="store_true", help="skip the encode batch sweep (256..1639 chunksets)")
     p.add_argument("--cpu-sample", type=int, default=0, help="chunksets in the CPU sample (0 = auto)")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
     return p.parse_args()
@@ -184,6 +186,34 @@ def main():
                   "coded_GBps": round(n * N * F / (c_ms * 1e-3) / 1e9, 1),
                   "blob_GiBps": round(n * CS / GIB / (c_ms * 1e-3), 1), "bound": "valu (BLAKE3 rotates)"}
 
+    # encode batch sweep beside the headline step (north_star: "at batch >= 256"):
+    # one HBM-resident 16 GiB blob, encode-only launches of its first n chunksets, HIP events on the
+    # bench stream. Single-GPU runs only; never inside the timed step.
+    sweep = None
+    if world == 1 and not args.no_sweep:
+        del out, plan, verd, status
+        nmax = max(SWEEP)
+        with torch.cuda.stream(stream):
+            big = torch.empty(nmax * CS, dtype=torch.uint8, device=dev)
+            codec.fill_random_device(ctx, 0xDEC05003, big, stream=stream)
+            cbig = torch.from_numpy(codec.fill_random_host(0xC0EF0003, nmax * N * K)).to(dev)
+            obig = torch.empty(nmax * N * F, dtype=torch.uint8, device=dev)
+        sweep = []
+        for ns in SWEEP:
+            reps = 3 if ns >= 1024 else 5
+            codec.encode_batch(ctx, big, ns, cbig, obig, stream=stream)
+            sev = [torch.cuda.Event(enable_timing=True) for _ in range(reps + 1)]
+            sev[0].record(stream)
+            for r in range(reps):
+                codec.encode_batch(ctx, big, ns, cbig, obig, stream=stream)
+                sev[r + 1].record(stream)
+            stream.synchronize()
+            ms = sev[0].elapsed_time(sev[-1]) / reps
+            gbs = ns * (CS + N * F) / (ms * 1e-3) / 1e9
+            sweep.append({"chunksets": ns, "encode_ms": round(ms, 3), "encode_GBps": round(gbs, 1),
+                          "frac": round(gbs / HBM_PEAK_GBS, 4), "blob_GiBps": round(ns * CS / GIB / (ms * 1e-3), 1)})
+        del big, cbig, obig
+
     enc_bytes = n * (CS + N * F)            # algorithmic HBM bytes of one encode launch
     dec_bytes = n_ready * (K * F + CS)      # ... of one decode launch (ready chunksets only)
     enc_gbs = enc_bytes / (enc_ms * 1e-3) / 1e9
@@ -219,6 +249,7 @@ def main():
                           "repair_blob_GiBps": round(n * CS / GIB / ((plan_ms + dec_ms) * 1e-3), 1),
                           "ready_chunksets": n_ready, "not_ready_chunksets": n - n_ready},
             "commitment": commit,
+            "encode_batch_sweep": sweep,
         }
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args.cpu_sample, 0xDEC05002)
