@@ -338,6 +338,28 @@ def test_repair_pitch_and_repeated_candidates(ctx):
     assert st[0] == 0
 
 
+@pytest.mark.parametrize("blob_len", [1, 4093, CS - 1, CS, CS + 1, 3 * CS + 12345])
+def test_blob_all_chunks_shuffled_roundtrip(ctx, blob_len):
+    """tests.rs:4-57: build a blob, shuffle ALL 16*n chunks of all chunksets together, feed them to
+    the repairing blob in that order (each chunkset sees its own chunks in their global order), and
+    get the blob back; coded bytes equal the oracle's. Sizes: 1 B, odd, either side of one
+    chunkset, and a ragged multi-chunkset blob (the reference draws 1 B ... 256 MiB)."""
+    blob = o.fill_random(0xB10D + blob_len, blob_len)
+    n = -(-blob_len // CS)
+    coeffs = o.fill_random(0xC0F1 + blob_len, n * N * K)
+    coded = codec.blob_encode_host(ctx, blob, coeffs, batch=2)
+    assert np.array_equal(coded, o.blob_encode(blob, coeffs, nthreads=8))
+    order = np.random.default_rng(blob_len).permutation(n * N)   # global chunk ids c*16 + j
+    cand = np.full((n, N), 0xFF, np.uint8)
+    fill = np.zeros(n, np.int64)
+    for gid in order:
+        c, j = divmod(int(gid), N)
+        cand[c, fill[c]] = j
+        fill[c] += 1
+    out, status = codec.blob_repair_host(ctx, coded, cand, blob_len, batch=2)
+    assert (status == 0).all() and np.array_equal(out, blob)
+
+
 def test_blob_host_not_ready_chunkset(ctx):
     blob_len = CS + 777
     blob = o.fill_random(0xB10C, blob_len)
