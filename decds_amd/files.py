@@ -18,6 +18,7 @@ the ones the reference would accept.
 import ctypes
 import os
 import time
+from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
 
@@ -46,13 +47,34 @@ def _merkle(leaves):
     return root.raw, proofs[:n * depth * 32].reshape(n, depth * 32) if depth else np.zeros((n, 0), np.uint8)
 
 
-def break_blob(ctx, blob, target_dir, batch=64, coeffs=None, timings=None):
+def _pinned(shape, torch):
+    return torch.empty(shape, dtype=torch.uint8, pin_memory=True)
+
+
+def _read_pinned(path, torch):
+    """the whole file into one page-locked buffer (DMA source for the H2D copies)"""
+    size = os.path.getsize(path)
+    t = _pinned(max(size, 1), torch)[:size]
+    with open(path, "rb") as f:
+        if size and f.readinto(memoryview(t.numpy())) != size:
+            raise OSError("short read of %s" % path)
+    return t
+
+
+def break_blob(ctx, blob, target_dir, batch=64, coeffs=None, timings=None, threads=16):
     """Blob::new + handle_break: `blob` is a path or a uint8 array. coeffs: n x 16 x 10 coding vectors
-    or None (drawn from os.urandom, as the reference draws from rand::rng()). Returns the header."""
+    or None (drawn from os.urandom, as the reference draws from rand::rng()). Returns the header.
+    The blob is read into page-locked memory; per batch the H2D copy, encode, commitment and the
+    D2H copies into page-locked outputs are queued on one stream without host round trips; the
+    share files are serialised and written by `threads` workers (one chunkset each)."""
     import torch
     t = {} if timings is None else timings
     t0 = time.perf_counter()
-    data = np.fromfile(blob, dtype=np.uint8) if isinstance(blob, (str, os.PathLike)) else np.ascontiguousarray(blob)
+    if isinstance(blob, (str, os.PathLike)):
+        data_t = _read_pinned(blob, torch)
+    else:
+        data_t = torch.from_numpy(np.ascontiguousarray(blob).reshape(-1))
+    data = data_t.numpy()
     if data.size == 0:
         raise DecdsError(8, "empty data for blob")
     t["read_s"] = time.perf_counter() - t0
@@ -61,35 +83,38 @@ def break_blob(ctx, blob, target_dir, batch=64, coeffs=None, timings=None):
         coeffs = np.frombuffer(os.urandom(n * N * K), np.uint8)
     coeffs = np.ascontiguousarray(coeffs, dtype=np.uint8).reshape(-1)
     t0 = time.perf_counter()
-    digest = _blake3(data)                                             # blob.rs:249
+    digest = _blake3(data, threads)                                    # blob.rs:249
     t["digest_s"] = time.perf_counter() - t0
     t0 = time.perf_counter()
     dev = torch.device("cuda", ctx.device)
-    coded_h = np.empty((n * N, F), np.uint8)
-    roots_h = np.empty((n, 32), np.uint8)
-    proofs_h = np.empty((n * N, PROOF_SIZE * 32), np.uint8)
+    coded_h = _pinned((n * N, F), torch)
+    roots_h = _pinned((n, 32), torch)
+    proofs_h = _pinned((n * N, PROOF_SIZE * 32), torch)
     bmax = min(batch, n)
-    src = torch.empty(bmax * CS, dtype=torch.uint8, device=dev)
-    coded = torch.empty(bmax * N * F, dtype=torch.uint8, device=dev)
-    dig = torch.empty(bmax * N * 32, dtype=torch.uint8, device=dev)
-    roots = torch.empty(bmax * 32, dtype=torch.uint8, device=dev)
-    proofs = torch.empty(bmax * N * 128, dtype=torch.uint8, device=dev)
-    for c0 in range(0, n, bmax):
-        b = min(bmax, n - c0)
-        lo, hi = c0 * CS, min(data.size, (c0 + b) * CS)
-        src[:hi - lo].copy_(torch.from_numpy(data[lo:hi]))
-        if hi - lo < b * CS:
-            src[hi - lo:b * CS].zero_()                               # blob.rs:252-254 zero padding
-        cv = torch.from_numpy(coeffs[c0 * N * K:(c0 + b) * N * K].copy()).to(dev)
-        codec.encode_batch(ctx, src, b, cv, coded)
-        codec.commit_batch(ctx, coded, b, dig, roots, proofs, first_chunkset_id=c0)
-        coded_h[c0 * N:(c0 + b) * N] = coded[:b * N * F].view(b * N, F).cpu().numpy()
-        roots_h[c0:c0 + b] = roots[:b * 32].view(b, 32).cpu().numpy()
-        proofs_h[c0 * N:(c0 + b) * N] = proofs[:b * N * 128].view(b * N, 128).cpu().numpy()
-    torch.cuda.synchronize()
+    stream = torch.cuda.Stream(dev)
+    with torch.cuda.stream(stream):
+        cv = torch.from_numpy(coeffs).to(dev, non_blocking=False)
+        src = torch.empty(bmax * CS, dtype=torch.uint8, device=dev)
+        coded = torch.empty(bmax * N * F, dtype=torch.uint8, device=dev)
+        dig = torch.empty(bmax * N * 32, dtype=torch.uint8, device=dev)
+        roots = torch.empty(bmax * 32, dtype=torch.uint8, device=dev)
+        proofs = torch.empty(bmax * N * 128, dtype=torch.uint8, device=dev)
+        for c0 in range(0, n, bmax):                                   # stream-ordered buffer reuse
+            b = min(bmax, n - c0)
+            lo, hi = c0 * CS, min(data.size, (c0 + b) * CS)
+            src[:hi - lo].copy_(data_t[lo:hi], non_blocking=True)
+            if hi - lo < b * CS:
+                src[hi - lo:b * CS].zero_()                           # blob.rs:252-254 zero padding
+            codec.encode_batch(ctx, src, b, cv[c0 * N * K:], coded, stream=stream)
+            codec.commit_batch(ctx, coded, b, dig, roots, proofs, first_chunkset_id=c0, stream=stream)
+            coded_h[c0 * N:(c0 + b) * N].view(-1).copy_(coded[:b * N * F], non_blocking=True)
+            roots_h[c0:c0 + b].view(-1).copy_(roots[:b * 32], non_blocking=True)
+            proofs_h[c0 * N:(c0 + b) * N].view(-1).copy_(proofs[:b * N * 128], non_blocking=True)
+    stream.synchronize()
     t["device_s"] = time.perf_counter() - t0
     t0 = time.perf_counter()
-    cs_roots = [roots_h[c].tobytes() for c in range(n)]
+    coded_np, roots_np, proofs_np = coded_h.numpy(), roots_h.numpy(), proofs_h.numpy()
+    cs_roots = [roots_np[c].tobytes() for c in range(n)]
     blob_root, blob_proofs = _merkle(cs_roots)                         # blob.rs:266-273
     header = wire.BlobHeader(data.size, n, digest, blob_root, cs_roots)
     os.makedirs(target_dir, exist_ok=True)
@@ -98,20 +123,24 @@ def break_blob(ctx, blob, target_dir, batch=64, coeffs=None, timings=None):
     depth = blob_proofs.shape[1] // 32
     plen = PROOF_SIZE + depth
     cap = lib().decds_pcc_encoded_len(n, n * N, F, plen)
-    out = ctypes.create_string_buffer(cap)
-    w = ctypes.c_size_t()
-    pf = np.empty(plen * 32, np.uint8)
-    for c in range(n):                                                 # handle_break.rs:66-106
+
+    def write_chunkset(c):                                             # handle_break.rs:66-106
         d = os.path.join(target_dir, "chunkset.%d" % c)
         os.makedirs(d, exist_ok=True)
+        out = ctypes.create_string_buffer(cap)
+        w = ctypes.c_size_t()
+        pf = np.empty(plen * 32, np.uint8)
         pf[PROOF_SIZE * 32:] = blob_proofs[c]
         for j in range(N):
             r = c * N + j
-            pf[:PROOF_SIZE * 32] = proofs_h[r]
-            check(lib().decds_pcc_to_bytes(c, r, coded_h[r].ctypes.data_as(ctypes.c_void_p), F,
+            pf[:PROOF_SIZE * 32] = proofs_np[r]
+            check(lib().decds_pcc_to_bytes(c, r, coded_np[r].ctypes.data_as(ctypes.c_void_p), F,
                                            pf.ctypes.data_as(ctypes.c_void_p), plen, out, cap, ctypes.byref(w)))
             with open(os.path.join(d, "share%02d.data" % j), "wb") as f:
                 f.write(memoryview(out)[:w.value])
+
+    with ThreadPoolExecutor(max_workers=max(1, threads)) as pool:
+        list(pool.map(write_chunkset, range(n)))
     t["write_s"] = time.perf_counter() - t0
     return header
 
@@ -125,92 +154,114 @@ def read_blob_metadata(chunk_dir):
     return h
 
 
-def repair_blob(ctx, chunk_dir, target_dir, batch=64, timings=None):
+def repair_blob(ctx, chunk_dir, target_dir, batch=64, timings=None, threads=16):
     """handle_repair over device batches. Returns the repaired bytes' path; raises DecdsError if a
-    chunkset cannot be repaired or the repaired digest differs (handle_repair.rs:79-84, 129-151)."""
+    chunkset cannot be repaired or the repaired digest differs (handle_repair.rs:79-84, 129-151).
+    Share files are read and parsed by `threads` workers straight into a page-locked staging
+    buffer laid out as the chunksets' 16 coded-row slots (share j of chunkset slot s at row
+    s*16 + j), so validation, plan and decode run on it in place after one H2D copy."""
     import torch
     t = {} if timings is None else timings
     header = read_blob_metadata(chunk_dir)
     n = header.get_num_chunksets()
+    blob_size = header.get_blob_size()
     dev = torch.device("cuda", ctx.device)
     roots_d = torch.from_numpy(np.frombuffer(b"".join(header.chunkset_root_commitments), np.uint8).copy()).to(dev)
     broot_d = torch.from_numpy(np.frombuffer(header.root_commitment, np.uint8).copy()).to(dev)
     os.makedirs(target_dir, exist_ok=True)
     out_path = os.path.join(target_dir, "repaired.data")
-    repaired = np.empty(n * CS, np.uint8)
-    t_read = t_dev = 0.0
+    plen = PROOF_SIZE + max(0, (n - 1).bit_length())                   # 4 chunkset + blob-level hashes
+    repaired_h = _pinned(n * CS, torch)
     bmax = min(batch, n)
-    for c0 in range(0, n, bmax):
-        b = min(bmax, n - c0)
+    rows_h = _pinned((bmax * N, F), torch)
+    prf_h = _pinned((bmax * N, plen * 32), torch)
+    rows_np, prf_np = rows_h.numpy(), prf_h.numpy()
+    ids_np = np.empty((bmax * N, 2), np.int64)
+    filled = np.zeros(bmax * N, bool)
+    stream = torch.cuda.Stream(dev)
+    with torch.cuda.stream(stream):
+        rows_d = torch.empty(bmax * N * F, dtype=torch.uint8, device=dev)
+        prf_d = torch.empty(bmax * N * plen * 32, dtype=torch.uint8, device=dev)
+        ids_d = torch.empty(bmax * N * 2, dtype=torch.int64, device=dev)
+        dig = torch.empty(bmax * N * 32, dtype=torch.uint8, device=dev)
+        valid = torch.empty(bmax * N, dtype=torch.uint8, device=dev)
+        plan = torch.empty(bmax * 128, dtype=torch.uint8, device=dev)
+        verd = torch.empty(bmax * N, dtype=torch.int8, device=dev)
+        status = torch.empty(bmax, dtype=torch.int32, device=dev)
+    t_read = t_dev = 0.0
+
+    def read_chunkset(c0, s):                                          # handle_repair.rs:53-76
+        cs, ch = ctypes.c_uint64(), ctypes.c_uint64()
+        dp, pp = ctypes.c_void_p(), ctypes.c_void_p()
+        dl, pl, used = ctypes.c_size_t(), ctypes.c_size_t(), ctypes.c_size_t()
+        for j in range(N):
+            r = s * N + j
+            filled[r] = False
+            ids_np[r] = (n, 0)                                         # never valid unless overwritten
+            try:
+                with open(os.path.join(chunk_dir, "chunkset.%d" % (c0 + s), "share%02d.data" % j), "rb") as f:
+                    raw = bytearray(f.read())
+            except OSError:
+                continue                                               # missing share: skipped
+            src = (ctypes.c_char * len(raw)).from_buffer(raw)
+            st = lib().decds_pcc_from_bytes(src, len(raw), ctypes.byref(cs), ctypes.byref(ch), ctypes.byref(dp),
+                                            ctypes.byref(dl), ctypes.byref(pp), ctypes.byref(pl), ctypes.byref(used))
+            if st != 0 or used.value != len(raw) or dl.value != F or pl.value != plen:
+                continue                                               # unreadable / malformed: skipped
+            base = ctypes.addressof(src)
+            mv = memoryview(raw)
+            rows_np[r] = np.frombuffer(mv[dp.value - base:dp.value - base + F], np.uint8)
+            prf_np[r] = np.frombuffer(mv[pp.value - base:pp.value - base + plen * 32], np.uint8)
+            ids_np[r] = (cs.value, ch.value)
+            filled[r] = True
+
+    with ThreadPoolExecutor(max_workers=max(1, threads)) as pool:
+        for c0 in range(0, n, bmax):
+            b = min(bmax, n - c0)
+            t0 = time.perf_counter()
+            list(pool.map(lambda s: read_chunkset(c0, s), range(b)))
+            t_read += time.perf_counter() - t0
+            t0 = time.perf_counter()
+            m = b * N
+            with torch.cuda.stream(stream):
+                rows_d[:m * F].copy_(rows_h[:m].view(-1), non_blocking=True)
+                prf_d[:m * plen * 32].copy_(prf_h[:m].view(-1), non_blocking=True)
+                ids_d[:m * 2].copy_(torch.from_numpy(ids_np[:m].reshape(-1)), non_blocking=False)
+                codec.validate_batch(ctx, rows_d, m, ids_d, prf_d, plen, roots_d, n, dig, valid, blob_root=broot_d,
+                                     stream=stream)
+                v = valid[:m].cpu().numpy().astype(bool)
+                # RepairingBlob::add_chunk routes by the chunk's own chunkset id (blob.rs:374-379): a
+                # valid chunk in another chunkset's directory is kept only in its own directory
+                cand = np.full((b, N), NO_CANDIDATE, np.uint8)
+                for s in range(b):
+                    ok = np.nonzero(filled[s * N:(s + 1) * N] & v[s * N:(s + 1) * N]
+                                    & (ids_np[s * N:(s + 1) * N, 0] == c0 + s))[0]
+                    cand[s, :ok.size] = ok
+                dst = torch.empty(b * CS, dtype=torch.uint8, device=dev)
+                codec.repair_batch(ctx, rows_d, b, torch.from_numpy(cand).to(dev), plan, verd, dst, status,
+                                   stream=stream)
+                st = status[:b].cpu().numpy()
+                bad = [c0 + s for s in range(b) if st[s] != 0]
+                if bad:
+                    raise DecdsError(6 if any(st[s] == 6 for s in range(b)) else 5,
+                                     "failed to repair chunkset(s) %s" % bad[:8])
+                repaired_h[c0 * CS:(c0 + b) * CS].copy_(dst, non_blocking=True)
+            stream.synchronize()
+            t_dev += time.perf_counter() - t0
         t0 = time.perf_counter()
-        rows, ids, prf, owner = [], [], [], []                          # owner: (chunkset slot, share id)
-        plen = None
-        for c in range(c0, c0 + b):
-            for j in range(N):
-                p = os.path.join(chunk_dir, "chunkset.%d" % c, "share%02d.data" % j)
-                if not os.path.isfile(p):
-                    continue
-                raw = open(p, "rb").read()
-                try:
-                    ch, used = wire.pcc_from_bytes(raw)
-                except DecdsError:
-                    continue                                           # unreadable share: skipped
-                if used != len(raw) or len(ch.erasure_coded_data) != F:
-                    continue
-                if plen is None:
-                    plen = len(ch.proof)
-                if len(ch.proof) != plen:
-                    continue
-                rows.append(ch.erasure_coded_data)
-                ids.append((ch.chunkset_id, ch.chunk_id))
-                prf.append(b"".join(ch.proof))
-                owner.append((c - c0, j))
-        t_read += time.perf_counter() - t0
-        t0 = time.perf_counter()
-        m = len(rows)
-        cand = np.full((b, N), NO_CANDIDATE, np.uint8)
-        if m:
-            rows_d = torch.from_numpy(np.frombuffer(b"".join(rows), np.uint8).copy()).to(dev)
-            ids_d = torch.tensor(ids, dtype=torch.int64, device=dev)
-            prf_d = torch.from_numpy(np.frombuffer(b"".join(prf), np.uint8).copy()).to(dev)
-            dig = torch.empty(m * 32, dtype=torch.uint8, device=dev)
-            valid = torch.empty(m, dtype=torch.uint8, device=dev)
-            codec.validate_batch(ctx, rows_d, m, ids_d, prf_d, plen, roots_d, n, dig, valid, blob_root=broot_d)
-            v = valid.cpu().numpy()
-            # RepairingBlob::add_chunk routes by the chunk's own chunkset id (blob.rs:374-379): a valid
-            # chunk in another chunkset's directory belongs to that chunkset, which the reference
-            # would repair from it only if it were read there; keep it only in its own directory
-            fill = [0] * b
-            coded = torch.empty(b * N * F, dtype=torch.uint8, device=dev)
-            for k in range(m):
-                s, j = owner[k]
-                if v[k] and ids[k][0] == c0 + s and fill[s] < N:
-                    coded[(s * N + fill[s]) * F:(s * N + fill[s] + 1) * F].copy_(rows_d[k * F:(k + 1) * F])
-                    cand[s, fill[s]] = fill[s]
-                    fill[s] += 1
-        else:
-            coded = torch.empty(b * N * F, dtype=torch.uint8, device=dev)
-        plan = torch.empty(b * 128, dtype=torch.uint8, device=dev)
-        verd = torch.empty(b * N, dtype=torch.int8, device=dev)
-        status = torch.empty(b, dtype=torch.int32, device=dev)
-        dst = torch.empty(b * CS, dtype=torch.uint8, device=dev)
-        codec.repair_batch(ctx, coded, b, torch.from_numpy(cand).to(dev), plan, verd, dst, status)
-        st = status.cpu().numpy()
-        bad = [c0 + s for s in range(b) if st[s] != 0]
-        if bad:
-            raise DecdsError(6 if any(st[s] == 6 for s in range(b)) else 5,
-                             "failed to repair chunkset(s) %s" % bad[:8])
-        repaired[c0 * CS:(c0 + b) * CS] = dst.cpu().numpy()
-        t_dev += time.perf_counter() - t0
+        blob = repaired_h.numpy()[:blob_size]
+
+        def write_part(c):                                             # handle_repair.rs:86-96
+            lo, hi = c * CS, min(blob_size, (c + 1) * CS)
+            with open(os.path.join(target_dir, "chunkset.%d.data" % c), "wb") as f:
+                f.write(memoryview(blob[lo:hi]))
+
+        list(pool.map(write_part, range(n)))
+        with open(out_path, "wb") as f:
+            f.write(memoryview(blob))
+        t["write_s"] = time.perf_counter() - t0
     t0 = time.perf_counter()
-    blob = repaired[:header.get_blob_size()]
-    for c in range(n):                                                  # handle_repair.rs:86-96
-        lo, hi = c * CS, min(header.get_blob_size(), (c + 1) * CS)
-        blob[lo:hi].tofile(os.path.join(target_dir, "chunkset.%d.data" % c))
-    blob.tofile(out_path)
-    t["write_s"] = time.perf_counter() - t0
-    t0 = time.perf_counter()
-    ok = _blake3(blob) == header.get_blob_digest()                      # handle_repair.rs:129-151
+    ok = _blake3(blob, threads) == header.get_blob_digest()             # handle_repair.rs:129-151
     t["digest_s"] = time.perf_counter() - t0
     t["read_s"], t["device_s"] = t_read, t_dev
     if not ok:
