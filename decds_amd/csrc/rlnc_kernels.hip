@@ -350,6 +350,9 @@ __device__ __forceinline__ void combine_block(const uint8_t *lds, uint32_t laneo
 // MAP > 0: super-tiles of MAP consecutive tiles of one chunkset dealt round-robin to the
 //   workgroups, so the resident workgroups sweep a few whole chunksets side by side, at the price
 //   of a table rebuild per super-tile.
+// MAP < MAP_BAND: non-persistent — workgroup b takes the T = -MAP consecutive tiles from b*T and
+//   exits; the dispatcher sweeps the batch in order and refills a CU as soon as one of its
+//   workgroups finishes (decode default, T = 8: -3 % / -5 % at 103 / 1639 chunksets).
 // MAP == MAP_BAND: XCD bands. The dispatcher deals workgroups round-robin over the 8 XCDs
 //   (workgroup b runs on XCD b % 8, cdna_hip_programming.md T1), so the P = grid / 8 workgroups of
 //   XCD x sweep chunksets x, x + 8, x + 16, ... one at a time, workgroup q = b / 8 taking tiles
@@ -362,7 +365,7 @@ constexpr uint32_t NXCD = 8;
 #define DECDS_ENC_MAP 0
 #endif
 #ifndef DECDS_DEC_MAP
-#define DECDS_DEC_MAP 8
+#define DECDS_DEC_MAP -8
 #endif
 #ifndef DECDS_ENC_SHARE
 #define DECDS_ENC_SHARE 500
@@ -415,6 +418,16 @@ __device__ __forceinline__ void walk_tiles(size_t n, Fn &&f) {
             const uint32_t cs = st / SPC, tb = (st % SPC) * MAP;
             const uint32_t ncs = st + gridDim.x < total ? (st + gridDim.x) / SPC : 0xFFFFFFFFu;
             for (uint32_t k = 0; k < (uint32_t)MAP; k++) f(cs, tb + k, 1u, k + 1 < (uint32_t)MAP, ncs);
+        }
+    } else if constexpr (MAP < MAP_BAND) {
+        // non-persistent: workgroup b takes tiles [b*T, (b+1)*T) and exits (grid = tiles / T), so
+        // the dispatcher sweeps the batch in order and refills CUs as workgroups finish
+        constexpr uint32_t T = (uint32_t)(-MAP);
+        const uint64_t total = (uint64_t)n * TILES_PER_CS;
+        const uint32_t t0 = blockIdx.x * T, t1 = (uint32_t)(t0 + T < total ? t0 + T : total);
+        for (uint32_t t = t0; t < t1; t++) {
+            const uint32_t cs = t / TILES_PER_CS, tile = t % TILES_PER_CS;
+            f(cs, tile, 1u, t + 1 < t1 && tile + 1 < TILES_PER_CS, 0xFFFFFFFFu);
         }
     } else {
         static_assert(MAP == MAP_BAND, "work map");
@@ -975,6 +988,7 @@ hipError_t launch_encode(const LaunchGeom &g, const uint8_t *src, size_t n, cons
         return hipGetLastError();
     }
     uint32_t grid = stream_grid(g, n);
+    if (DECDS_ENC_MAP < MAP_BAND) grid = (uint32_t)(((uint64_t)n * TILES_PER_CS + (-DECDS_ENC_MAP) - 1) / (-DECDS_ENC_MAP));
     if (DECDS_ENC_MAP == MAP_BAND && band_ok(grid & ~(NXCD - 1), n)) {
         grid &= ~(NXCD - 1);
         hipLaunchKernelGGL(rlnc_encode_kernel<DECDS_ENC_MAP>, dim3(grid), dim3(WG), LDS_BYTES, stream, src, n,
@@ -1009,6 +1023,7 @@ hipError_t launch_decode(const LaunchGeom &g, const uint8_t *coded, size_t pitch
         return hipGetLastError();
     }
     uint32_t grid = stream_grid(g, n);
+    if (DECDS_DEC_MAP < MAP_BAND) grid = (uint32_t)(((uint64_t)n * TILES_PER_CS + (-DECDS_DEC_MAP) - 1) / (-DECDS_DEC_MAP));
     if (DECDS_DEC_MAP == MAP_BAND && band_ok(grid & ~(NXCD - 1), n)) {
         grid &= ~(NXCD - 1);
         hipLaunchKernelGGL(rlnc_decode_kernel<DECDS_DEC_MAP>, dim3(grid), dim3(WG), LDS_BYTES, stream, coded, pitch,
