@@ -344,7 +344,7 @@ __device__ __forceinline__ void combine_block(const uint8_t *lds, uint32_t laneo
 }
 
 // ---- work split ---------------------------------------------------------------------------------
-// The n*256 tiles (256 lane blocks = 4096 columns each) are walked in one of three orders:
+// The n*256 tiles (256 lane blocks = 4096 columns each) are walked in one of four orders:
 // MAP == 0: equal contiguous ranges, one per resident workgroup (each workgroup rebuilds its LDS
 //   tables only when its range crosses into the next chunkset).
 // MAP > 0: super-tiles of MAP consecutive tiles of one chunkset dealt round-robin to the
@@ -397,9 +397,8 @@ __device__ __forceinline__ void tile_range(size_t n, uint32_t &t0, uint32_t &t1)
     }
 }
 
-// Calls f(chunkset, tile, step, next, next_chunkset) for this workgroup's tiles in order: when
-// `next`, the workgroup's following tile is tile + step of the same chunkset; next_chunkset is the
-// chunkset it visits after the current one (>= n: none), for loading its coefficients early.
+// Calls f(chunkset, tile, step, next) for this workgroup's tiles in order: when `next`, the
+// workgroup's following tile is tile + step of the same chunkset (the ROLL prefetch target).
 template <int MAP, uint32_t SHARE = 500, class Fn>
 __device__ __forceinline__ void walk_tiles(size_t n, Fn &&f) {
     if constexpr (MAP == 0) {
@@ -407,8 +406,7 @@ __device__ __forceinline__ void walk_tiles(size_t n, Fn &&f) {
         tile_range<SHARE>(n, t0, t1);
         for (uint32_t t = t0; t < t1; t++) {
             const uint32_t cs = t / TILES_PER_CS, tile = t % TILES_PER_CS;
-            f(cs, tile, 1u, t + 1 < t1 && tile + 1 < TILES_PER_CS,
-              (cs + 1) * TILES_PER_CS < t1 ? cs + 1 : 0xFFFFFFFFu);
+            f(cs, tile, 1u, t + 1 < t1 && tile + 1 < TILES_PER_CS);
         }
     } else if constexpr (MAP > 0) {
         static_assert(TILES_PER_CS % MAP == 0, "super-tile size");
@@ -416,8 +414,7 @@ __device__ __forceinline__ void walk_tiles(size_t n, Fn &&f) {
         const uint32_t total = (uint32_t)n * SPC;
         for (uint32_t st = blockIdx.x; st < total; st += gridDim.x) {
             const uint32_t cs = st / SPC, tb = (st % SPC) * MAP;
-            const uint32_t ncs = st + gridDim.x < total ? (st + gridDim.x) / SPC : 0xFFFFFFFFu;
-            for (uint32_t k = 0; k < (uint32_t)MAP; k++) f(cs, tb + k, 1u, k + 1 < (uint32_t)MAP, ncs);
+            for (uint32_t k = 0; k < (uint32_t)MAP; k++) f(cs, tb + k, 1u, k + 1 < (uint32_t)MAP);
         }
     } else if constexpr (MAP < MAP_BAND) {
         // non-persistent: workgroup b takes tiles [b*T, (b+1)*T) and exits (grid = tiles / T), so
@@ -427,14 +424,14 @@ __device__ __forceinline__ void walk_tiles(size_t n, Fn &&f) {
         const uint32_t t0 = blockIdx.x * T, t1 = (uint32_t)(t0 + T < total ? t0 + T : total);
         for (uint32_t t = t0; t < t1; t++) {
             const uint32_t cs = t / TILES_PER_CS, tile = t % TILES_PER_CS;
-            f(cs, tile, 1u, t + 1 < t1 && tile + 1 < TILES_PER_CS, 0xFFFFFFFFu);
+            f(cs, tile, 1u, t + 1 < t1 && tile + 1 < TILES_PER_CS);
         }
     } else {
         static_assert(MAP == MAP_BAND, "work map");
         const uint32_t P = gridDim.x / NXCD, x = blockIdx.x % NXCD, q = blockIdx.x / NXCD;
         if (q >= P) return;
         for (uint32_t cs = x; cs < n; cs += NXCD)
-            for (uint32_t tile = q; tile < TILES_PER_CS; tile += P) f(cs, tile, P, tile + P < TILES_PER_CS, cs + NXCD);
+            for (uint32_t tile = q; tile < TILES_PER_CS; tile += P) f(cs, tile, P, tile + P < TILES_PER_CS);
     }
 }
 
@@ -491,7 +488,7 @@ void rlnc_encode_kernel(const uint8_t *__restrict__ src, size_t n, const uint8_t
     uint4 x[K];
     bool have = false;
     [[maybe_unused]] bool built = false;
-    walk_tiles<MAP, DECDS_ENC_SHARE>(n, [&](uint32_t cs, uint32_t tile, uint32_t step, bool next, uint32_t) {
+    walk_tiles<MAP, DECDS_ENC_SHARE>(n, [&](uint32_t cs, uint32_t tile, uint32_t step, bool next) {
         if (cs != cur) {
             cur = cs;
             have = false;
@@ -550,7 +547,7 @@ void rlnc_decode_kernel(const uint8_t *__restrict__ coded, size_t pitch, size_t 
     uint4 x[K];
     bool have = false;
     [[maybe_unused]] bool built = false;
-    walk_tiles<MAP, DECDS_DEC_SHARE>(n, [&](uint32_t cs, uint32_t tile, uint32_t step, bool next, uint32_t) {
+    walk_tiles<MAP, DECDS_DEC_SHARE>(n, [&](uint32_t cs, uint32_t tile, uint32_t step, bool next) {
         if (cs != cur) {
             cur = cs;
             have = false;

@@ -28,7 +28,7 @@ __global__ __launch_bounds__(WG, WAVES_PER_SIMD) void pat_kernel(const uint8_t *
     for (int i = 0; i < (int)K; i++) ioff[i] = ENC ? (uint32_t)(i * L) : (uint32_t)(i * F + K);
 #pragma unroll
     for (int j = 0; j < NOUT; j++) ooff[j] = ENC ? (uint32_t)(j * F + K) : (uint32_t)(j * L);
-    walk_tiles<MAP>(n, [&](uint32_t cs, uint32_t tile, uint32_t, bool, uint32_t) {
+    walk_tiles<MAP>(n, [&](uint32_t cs, uint32_t tile, uint32_t, bool) {
         if (SY) __builtin_amdgcn_s_barrier();
         const uint8_t *ibase = src + (size_t)cs * (ENC ? CS : N * F);
         uint8_t *obase = dst + (size_t)cs * (ENC ? N * F : CS);
@@ -56,7 +56,7 @@ __global__ __launch_bounds__(WG, WAVES_PER_SIMD) void np_kernel(const uint8_t *_
     for (int i = 0; i < (int)K; i++) ioff[i] = (uint32_t)(i * L);
 #pragma unroll
     for (int j = 0; j < (int)N; j++) ooff[j] = (uint32_t)(j * F + K);
-    walk_tiles<0>(n, [&](uint32_t cs, uint32_t tile, uint32_t, bool, uint32_t) {
+    walk_tiles<0>(n, [&](uint32_t cs, uint32_t tile, uint32_t, bool) {
         const uint8_t *ibase = src + (size_t)cs * CS;
         uint8_t *obase = dst + (size_t)cs * N * F;
         const uint32_t block = tile * TILE_BLOCKS + threadIdx.x;
