@@ -130,6 +130,8 @@ struct Case {
     void (*fn)(const uint8_t *, size_t, uint8_t *);
     bool band;
     std::vector<float> ms;
+    uint32_t gmul = 1;  // grid multiplier (occupancy study; contiguous map only)
+    uint32_t np = 0;    // non-persistent: T tiles per workgroup (grid = tiles / T)
 };
 
 #define CASE(MAP, ENC, G, NAME) Case{NAME, ENC, pat_kernel<MAP, ENC, G>, MAP == MAP_BAND, {}}
@@ -160,6 +162,12 @@ int main(int argc, char **argv) {
         CASESY(8, false, "dec_map8_sync"),  CASESY(MAP_BAND, false, "dec_band_sync"),
         Case{"enc_mb2", true, mb_kernel<2, true>, false, {}}, Case{"enc_mb4", true, mb_kernel<4, true>, false, {}},
         Case{"dec_mb2", false, mb_kernel<2, false>, false, {}}, Case{"dec_mb4", false, mb_kernel<4, false>, false, {}},
+        Case{"enc_map0_x2", true, pat_kernel<0, true, 0>, false, {}, 2},
+        Case{"enc_map0_x4", true, pat_kernel<0, true, 0>, false, {}, 4},
+        Case{"enc_np2", true, pat_kernel<-2, true, 0>, false, {}, 1, 2},
+        Case{"enc_np8", true, pat_kernel<-8, true, 0>, false, {}, 1, 8},
+        Case{"dec_map0_x4", false, pat_kernel<0, false, 0>, false, {}, 4},
+        Case{"dec_np8", false, pat_kernel<-8, false, 0>, false, {}, 1, 8},
         CASE(0, false, 0, "dec_map0"),      CASE(8, false, 0, "dec_map8"),      CASE(MAP_BAND, false, 0, "dec_band"),
         CASE(8, false, 5, "dec_map8_g5"),   CASE(MAP_BAND, false, 5, "dec_band_g5"), CASE(MAP_BAND, false, 10, "dec_band_drain"),
     };
@@ -167,7 +175,8 @@ int main(int argc, char **argv) {
     hipEventCreate(&e0);
     hipEventCreate(&e1);
     auto launch = [&](Case &c) {
-        const uint32_t g = c.band ? grid & ~7u : grid;
+        uint32_t g = c.band ? grid & ~7u : grid * c.gmul;
+        if (c.np) g = (uint32_t)((n * TILES_PER_CS + c.np - 1) / c.np);
         if (c.enc)
             hipLaunchKernelGGL(c.fn, dim3(g), dim3(WG), 0, 0, b, n, a);
         else
