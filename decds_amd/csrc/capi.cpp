@@ -129,7 +129,7 @@ int decds_ctx_get_field(const decds_ctx *ctx, uint32_t *poly, uint8_t *marker) {
 static int check_pitch(size_t pitch) {
     if (pitch < F)
         return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "coded pitch %zu < %llu", pitch, (unsigned long long)F);
-    if ((N - 1) * (uint64_t)pitch + F >= (1ull << 32))
+    if ((N - 1) * (uint64_t)pitch + F >= (1ull << 31))  // row offsets stay inside a 2 GiB buffer descriptor
         return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "coded pitch %zu too large", pitch);
     return DECDS_OK;
 }

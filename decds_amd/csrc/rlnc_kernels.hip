@@ -60,7 +60,14 @@ struct Tune {
 #ifndef DECDS_DEC_SYNC
 #define DECDS_DEC_SYNC 0
 #endif
+#ifndef DECDS_ENC_BF
+#define DECDS_ENC_BF 1
+#endif
+#ifndef DECDS_ENC_BF_TUNE
+#define DECDS_ENC_BF_TUNE true, true, 0, 0
+#endif
 using EncTune = Tune<DECDS_ENC_TUNE, DECDS_ENC_SYNC>;
+using EncBfTune = Tune<DECDS_ENC_BF_TUNE>;  // DECDS_ENC_BF: per-chunkset branch-free segments
 using DecTune = Tune<DECDS_DEC_TUNE, DECDS_DEC_SYNC>;
 
 // ---- GF(2^8) ----------------------------------------------------------------------------------
@@ -161,12 +168,19 @@ __device__ __forceinline__ uint32_t tbl_mul(const uint8_t *lds, uint32_t i, uint
 // rlnc layout itself; gfx9 vector memory accepts unaligned 16-B accesses.
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
+// Buffer descriptors cover 2 GiB from the row base (the launchers keep every row offset below). A
+// lane with nothing to do passes column OOB_COL: its buffer loads return zeros and its buffer
+// stores are dropped by the range check, so a streaming loop needs no per-lane branch (see the
+// decode kernel's non-persistent path for why that matters).
+constexpr uint32_t BUF_RECORDS = 0x80000000u;
+constexpr uint32_t OOB_COL = 0x80000000u;
+
 template <int AUX>
 __device__ __forceinline__ uint4 ldrow(const uint8_t *base, uint32_t off) {
     u32x4 v;
     if constexpr (AUX >= 0) {
         const __amdgpu_buffer_rsrc_t r =
-            __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(base), 0, 0xFFFFFFFFu, 0x00020000);
+            __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(base), 0, BUF_RECORDS, 0x00020000);
         v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, AUX);
     } else {
         v = *reinterpret_cast<const u32x4 *>(base + off);
@@ -178,7 +192,7 @@ template <int AUX>
 __device__ __forceinline__ void strow(uint8_t *base, uint32_t off, uint4 v) {
     const u32x4 w = {v.x, v.y, v.z, v.w};
     if constexpr (AUX >= 0) {
-        const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, 0, 0xFFFFFFFFu, 0x00020000);
+        const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, 0, BUF_RECORDS, 0x00020000);
         __builtin_amdgcn_raw_buffer_store_b128(w, r, off, 0, AUX);
     } else {
         *reinterpret_cast<u32x4 *>(base + off) = w;
@@ -352,7 +366,8 @@ __device__ __forceinline__ void combine_block(const uint8_t *lds, uint32_t laneo
 //   of a table rebuild per super-tile.
 // MAP < MAP_BAND: non-persistent — workgroup b takes the T = -MAP consecutive tiles from b*T and
 //   exits; the dispatcher sweeps the batch in order and refills a CU as soon as one of its
-//   workgroups finishes (decode default, T = 8: -3 % / -5 % at 103 / 1639 chunksets).
+//   workgroups finishes (encode and decode default, T = 8; both stream their 8 tiles branch-free
+//   with stream_range instead of walking them here).
 // MAP == MAP_BAND: XCD bands. The dispatcher deals workgroups round-robin over the 8 XCDs
 //   (workgroup b runs on XCD b % 8, cdna_hip_programming.md T1), so the P = grid / 8 workgroups of
 //   XCD x sweep chunksets x, x + 8, x + 16, ... one at a time, workgroup q = b / 8 taking tiles
@@ -362,7 +377,7 @@ __device__ __forceinline__ void combine_block(const uint8_t *lds, uint32_t laneo
 constexpr int MAP_BAND = -1;
 constexpr uint32_t NXCD = 8;
 #ifndef DECDS_ENC_MAP
-#define DECDS_ENC_MAP 0
+#define DECDS_ENC_MAP -8
 #endif
 #ifndef DECDS_DEC_MAP
 #define DECDS_DEC_MAP -8
@@ -453,6 +468,30 @@ __device__ __forceinline__ void stream_tile(const uint8_t *lds, uint32_t laneoff
     if (active) combine_block<T, NIN, NOUT>(lds, laneoff, x, obase, ooff, block * COLS_PER_LANE, ibase, ioff, ncol0);
 }
 
+// Tiles [ta, tb) of one chunkset, branch-free (ROLL builds only): lanes past the last block use
+// OOB_COL, so no lane branches. The loop is entered after the first tile's loads AND NOUT dropped
+// stores, the same memory-counter picture as every later tile (NIN prefetched loads, then NOUT
+// stores). With a branch around the streaming code, or a reload path inside the loop, hipcc's
+// wait-count pass merges paths that issued no stores and waits with vmcnt(NIN-1) for the next
+// tile's first input: every tile then waited for the previous tile's stores as well; here it waits
+// for the inputs only.
+template <class T, int NIN, int NOUT>
+__device__ __forceinline__ void stream_range(const uint8_t *lds, uint32_t laneoff, uint32_t ta, uint32_t tb,
+                                             const uint8_t *ibase, const uint32_t (&ioff)[NIN], uint8_t *obase,
+                                             const uint32_t (&ooff)[NOUT], uint4 (&x)[NIN]) {
+    static_assert(T::ROLL && T::LAUX >= 0 && T::SAUX >= 0, "branch-free streaming needs prefetch and buffer ops");
+    uint32_t block = ta * TILE_BLOCKS + threadIdx.x;
+    load_block<T, NIN>(x, ibase, ioff, block < MAIN_BLOCKS ? block * COLS_PER_LANE : OOB_COL);
+#pragma unroll
+    for (int j = 0; j < NOUT; j++) strow<T::SAUX>(obase, OOB_COL + ooff[j], make_uint4(0, 0, 0, 0));
+    for (uint32_t t = ta; t < tb; t++, block += TILE_BLOCKS) {
+        const uint32_t nblock = block + TILE_BLOCKS;
+        const uint32_t col0 = block < MAIN_BLOCKS ? block * COLS_PER_LANE : OOB_COL;
+        const uint32_t ncol0 = t + 1 < tb && nblock < MAIN_BLOCKS ? nblock * COLS_PER_LANE : OOB_COL;
+        combine_block<T, NIN, NOUT>(lds, laneoff, x, obase, ooff, col0, ibase, ioff, ncol0);
+    }
+}
+
 // Timing-study builds only (DECDS_TIMING_TRACE): every wave stamps its start and end with the
 // 100 MHz real-time counter; decds_debug_trace copies the stamps out (kernel 0 encode, 1 decode).
 #ifdef DECDS_TIMING_TRACE
@@ -486,6 +525,47 @@ void rlnc_encode_kernel(const uint8_t *__restrict__ src, size_t n, const uint8_t
     uint8_t *obase = dst;
     const uint8_t *M = coeffs;
     uint4 x[K];
+    if constexpr (DECDS_ENC_BF && (MAP == 0 || MAP < MAP_BAND)) {
+        // this workgroup's tile range, walked one chunkset segment at a time: rebuild the tables,
+        // then stream the segment branch-free
+        uint32_t t0, t1;
+        if constexpr (MAP == 0) {
+            tile_range<DECDS_ENC_SHARE>(n, t0, t1);
+        } else {
+            const uint64_t total = (uint64_t)n * TILES_PER_CS;
+            t0 = blockIdx.x * (uint32_t)(-MAP);
+            t1 = (uint32_t)(t0 - MAP < total ? t0 - MAP : total);
+        }
+        while (t0 < t1) {
+            const uint32_t cs = t0 / TILES_PER_CS, tile0 = t0 % TILES_PER_CS;
+            const uint32_t te = (cs + 1) * TILES_PER_CS < t1 ? (cs + 1) * TILES_PER_CS : t1;
+            M = coeffs + (size_t)cs * N * K;
+            const uint32_t cw = table_coeffs<K, N>(M, K);
+            lds_barrier();
+            build_tables<K, N>(lds, cw, poly);
+            lds_barrier();
+            ibase = src + (size_t)cs * CS;
+            obase = dst + (size_t)cs * N * pitch;
+            if (tile0 == 0 && threadIdx.x < 64) {
+                for (uint32_t idx = lane; idx < N * K; idx += 64) obase[(idx / K) * pitch + idx % K] = M[idx];
+                for (uint32_t idx = lane; idx < TAIL_COLS * N; idx += 64) {
+                    const uint32_t j = idx % N, col = MAIN_COLS + idx / N;
+                    uint32_t y = 0;
+#pragma unroll
+                    for (uint32_t i = 0; i < K; i++) {
+                        const uint64_t p = (uint64_t)i * L + col;
+                        const uint32_t xv = p < CS ? ibase[p] : (p == CS ? marker : 0u);
+                        y ^= tbl_mul(lds, i, j, xv);
+                    }
+                    obase[j * pitch + K + col] = (uint8_t)y;
+                }
+            }
+            stream_range<EncBfTune, K, N>(lds, laneoff, tile0, te - cs * TILES_PER_CS, ibase, ioff, obase, ooff, x);
+            t0 = te;
+        }
+        TRACE_END(0);
+        return;
+    }
     bool have = false;
     [[maybe_unused]] bool built = false;
     walk_tiles<MAP, DECDS_ENC_SHARE>(n, [&](uint32_t cs, uint32_t tile, uint32_t step, bool next) {
@@ -545,6 +625,48 @@ void rlnc_decode_kernel(const uint8_t *__restrict__ coded, size_t pitch, size_t 
     const uint8_t *ibase = coded;
     uint8_t *obase = dst;
     uint4 x[K];
+    if constexpr (MAP < MAP_BAND) {
+        // Non-persistent: this workgroup's T tiles lie in one chunkset, streamed branch-free
+        constexpr uint32_t T = (uint32_t)(-MAP);
+        static_assert(TILES_PER_CS % T == 0, "a workgroup's tiles stay in one chunkset");
+        using DT = Tune<DecTune::ASM, true, DecTune::LAUX < 0 ? 0 : DecTune::LAUX, DecTune::SAUX < 0 ? 0 : DecTune::SAUX>;
+        const uint32_t t0 = blockIdx.x * T, cs = t0 / TILES_PER_CS, tile0 = t0 % TILES_PER_CS;
+        if (cs >= n) return;
+        const uint32_t *pw = reinterpret_cast<const uint32_t *>(plan + cs);
+        const uint32_t w0 = __builtin_amdgcn_readfirstlane(pw[0]);
+        const uint32_t w1 = __builtin_amdgcn_readfirstlane(pw[1]);
+        const uint32_t w2 = __builtin_amdgcn_readfirstlane(pw[2]);
+        if (((w2 >> 16) & 0xFFu) != K) return;  // RepairPlan::rank at byte 10: not ready
+        build_tables<K, K>(lds, table_coeffs<K, K>(plan[cs].inv, K), poly);
+        lds_barrier();
+        const uint32_t sel[K] = {w0 & 0xFFu, (w0 >> 8) & 0xFFu, (w0 >> 16) & 0xFFu, w0 >> 24,
+                                 w1 & 0xFFu, (w1 >> 8) & 0xFFu, (w1 >> 16) & 0xFFu, w1 >> 24,
+                                 w2 & 0xFFu, (w2 >> 8) & 0xFFu};
+#pragma unroll
+        for (int k = 0; k < (int)K; k++) ioff[k] = (uint32_t)(sel[k] * pitch + K);
+        ibase = coded + (size_t)cs * N * pitch;
+        obase = dst + (size_t)cs * CS;
+        if (tile0 == 0 && threadIdx.x < 64) {
+            // last 17 columns; piece 9's must decode to marker || zeros (rlnc
+            // get_decoded_data strips them; a mismatch is a repairing failure)
+            bool ok = true;
+            for (uint32_t idx = lane; idx < TAIL_COLS * K; idx += 64) {
+                const uint32_t i = idx % K, col = MAIN_COLS + idx / K;
+                uint32_t z = 0;
+#pragma unroll
+                for (uint32_t k = 0; k < K; k++) z ^= tbl_mul(lds, k, i, ibase[ioff[k] + col]);
+                const uint64_t p = (uint64_t)i * L + col;
+                if (p < CS)
+                    obase[p] = (uint8_t)z;
+                else
+                    ok &= z == (p == CS ? marker : 0u);
+            }
+            if (__any(!ok) && lane == 0) status[cs] = 6;  // DECDS_ERR_CHUNKSET_REPAIRING_FAILED
+        }
+        stream_range<DT, K, K>(lds, laneoff, tile0, tile0 + T, ibase, ioff, obase, ooff, x);
+        TRACE_END(1);
+        return;
+    }
     bool have = false;
     [[maybe_unused]] bool built = false;
     walk_tiles<MAP, DECDS_DEC_SHARE>(n, [&](uint32_t cs, uint32_t tile, uint32_t step, bool next) {

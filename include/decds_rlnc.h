@@ -79,7 +79,9 @@ int decds_device_count(void);
  *   src    : n x DECDS_CHUNKSET_BYTES (chunkset c at src + c*CS)
  *   coeffs : n x 16 x 10 coding vectors (row j of chunkset c at coeffs + (c*16+j)*10)
  *   dst    : n*16 coded rows; row r = c*16+j at dst + r*dst_pitch, laid out exactly like rlnc's
- *            full coded piece: coding vector (10 B) || payload (L B). dst_pitch >= 1,048,587. */
+ *            full coded piece: coding vector (10 B) || payload (L B). dst_pitch >= 1,048,587 and
+ *            15*dst_pitch + 1,048,587 < 2^31 (every pitch argument below: a chunkset's rows sit in
+ *            one 2 GiB buffer descriptor). */
 int decds_encode_batch(decds_ctx *ctx, const uint8_t *src, size_t n_chunksets,
                        const uint8_t *coeffs, uint8_t *dst, size_t dst_pitch, void *stream);
 

@@ -60,6 +60,29 @@ def test_encode_batch_bitexact_and_pitch(ctx):
             assert np.array_equal(coded[c * N:(c + 1) * N], ref), (pitch, c)
 
 
+def test_encode_decode_at_the_largest_pitch(ctx):
+    # a chunkset's 16 rows must fit one 2 GiB buffer descriptor (include/decds_rlnc.h): the largest
+    # pitch is bit-exact through encode and repair (lanes past the last block use out-of-range
+    # offsets, which must stay out of range there too); one byte more is refused
+    pmax = ((1 << 31) - 1 - F) // (N - 1)
+    data = o.fill_random(0xDEC05003, CS)
+    coeffs = o.fill_random(0xC0EF0003, N * K)
+    dst = torch.zeros((N - 1) * (pmax + 1) + F, dtype=torch.uint8, device="cuda")
+    codec.encode_batch(ctx, dev(data), 1, dev(coeffs), dst, pmax)
+    rows = host(dst.as_strided((N, F), (pmax, 1)))
+    assert np.array_equal(rows, o.chunkset_encode(data, coeffs, nthreads=8))
+    cand = np.array([15, 3, 8, 0, 12, 5, 9, 1, 14, 6, 2, 4, 7, 10, 11, 13], np.uint8)
+    plan = torch.empty(128, dtype=torch.uint8, device="cuda")
+    verd = torch.empty(N, dtype=torch.int8, device="cuda")
+    status = torch.empty(1, dtype=torch.int32, device="cuda")
+    out = torch.zeros(CS, dtype=torch.uint8, device="cuda")
+    codec.repair_batch(ctx, dst, 1, dev(cand), plan, verd, out, status, pitch=pmax)
+    assert host(status)[0] == 0 and np.array_equal(host(out), data)
+    with pytest.raises(decds_amd.DecdsError) as e:
+        codec.encode_batch(ctx, dev(data), 1, dev(coeffs), dst, pmax + 1)
+    assert e.value.kind == "InvalidArgument"
+
+
 def test_encode_zero_and_edge_coefficients(ctx):
     # zero coding vectors, identity rows (systematic pieces) and 0xFF everywhere
     data = o.fill_random(31, CS)
