@@ -412,6 +412,39 @@ __device__ __forceinline__ void tile_range(size_t n, uint32_t &t0, uint32_t &t1)
     }
 }
 
+// Non-persistent workgroup -> position in the batch. The dispatcher deals workgroups round-robin
+// over the 8 XCDs (b runs on XCD b % 8). With REMAP each XCD takes its own part of the batch
+// instead: DECDS_XCD_CHUNK = 0 one contiguous eighth (its q-th workgroup the q-th of that eighth,
+// rotated by SKEW x x workgroups); C > 0 runs of C consecutive workgroups dealt to the XCDs in turn
+// (C = 32: one chunkset per XCD at a time, the XCDs on neighbouring chunksets).
+#ifndef DECDS_ENC_XCD_REMAP
+#define DECDS_ENC_XCD_REMAP 1
+#endif
+#ifndef DECDS_DEC_XCD_REMAP
+#define DECDS_DEC_XCD_REMAP 0
+#endif
+#ifndef DECDS_XCD_SKEW
+#define DECDS_XCD_SKEW 0
+#endif
+#ifndef DECDS_XCD_CHUNK
+#define DECDS_XCD_CHUNK 0
+#endif
+template <bool REMAP>
+__device__ __forceinline__ uint32_t np_block() {
+    const uint32_t g = gridDim.x, b = blockIdx.x, x = b % NXCD, q = b / NXCD;
+    if constexpr (!REMAP) {
+        return b;
+    } else if constexpr (DECDS_XCD_CHUNK > 0) {
+        constexpr uint32_t C = DECDS_XCD_CHUNK;
+        if (b >= g - g % (NXCD * C)) return b;  // the ragged end keeps the dispatcher's order
+        return ((q / C) * NXCD + x) * C + q % C;
+    } else {
+        const uint32_t per = g / NXCD, rem = g % NXCD, cnt = per + (x < rem);
+        const uint32_t r = DECDS_XCD_SKEW ? (q + x * DECDS_XCD_SKEW) % cnt : q;
+        return x * per + (x < rem ? x : rem) + r;
+    }
+}
+
 // Calls f(chunkset, tile, step, next) for this workgroup's tiles in order: when `next`, the
 // workgroup's following tile is tile + step of the same chunkset (the ROLL prefetch target).
 template <int MAP, uint32_t SHARE = 500, class Fn>
@@ -533,7 +566,7 @@ void rlnc_encode_kernel(const uint8_t *__restrict__ src, size_t n, const uint8_t
             tile_range<DECDS_ENC_SHARE>(n, t0, t1);
         } else {
             const uint64_t total = (uint64_t)n * TILES_PER_CS;
-            t0 = blockIdx.x * (uint32_t)(-MAP);
+            t0 = np_block<DECDS_ENC_XCD_REMAP>() * (uint32_t)(-MAP);
             t1 = (uint32_t)(t0 - MAP < total ? t0 - MAP : total);
         }
         while (t0 < t1) {
@@ -630,7 +663,7 @@ void rlnc_decode_kernel(const uint8_t *__restrict__ coded, size_t pitch, size_t 
         constexpr uint32_t T = (uint32_t)(-MAP);
         static_assert(TILES_PER_CS % T == 0, "a workgroup's tiles stay in one chunkset");
         using DT = Tune<DecTune::ASM, true, DecTune::LAUX < 0 ? 0 : DecTune::LAUX, DecTune::SAUX < 0 ? 0 : DecTune::SAUX>;
-        const uint32_t t0 = blockIdx.x * T, cs = t0 / TILES_PER_CS, tile0 = t0 % TILES_PER_CS;
+        const uint32_t t0 = np_block<DECDS_DEC_XCD_REMAP>() * T, cs = t0 / TILES_PER_CS, tile0 = t0 % TILES_PER_CS;
         if (cs >= n) return;
         const uint32_t *pw = reinterpret_cast<const uint32_t *>(plan + cs);
         const uint32_t w0 = __builtin_amdgcn_readfirstlane(pw[0]);
