@@ -483,22 +483,31 @@ __device__ __forceinline__ void walk_tiles(size_t n, Fn &&f) {
     }
 }
 
+// Column phase: lane blocks cover payload columns [phase, phase + MAIN_COLS) (phase < 16, chosen by
+// the launcher so that rows with a 16-byte-aligned pitch are read / written on 16-byte boundaries);
+// the wave owning tile 0 does the 17 edge columns byte by byte: e < phase is column e, the rest the
+// columns after the last block.
+__device__ __forceinline__ uint32_t edge_col(uint32_t e, uint32_t phase) {
+    return e < phase ? e : MAIN_COLS + e;
+}
+
 // One tile for this lane: inputs were prefetched by the previous tile when `have` (ROLL), else
 // they are loaded now; `next` says whether the following tile is tile + step of this chunkset.
 template <class T, int NIN, int NOUT>
 __device__ __forceinline__ void stream_tile(const uint8_t *lds, uint32_t laneoff, uint32_t tile, uint32_t step,
-                                            bool next, const uint8_t *ibase, const uint32_t (&ioff)[NIN],
+                                            bool next, uint32_t phase, const uint8_t *ibase, const uint32_t (&ioff)[NIN],
                                             uint8_t *obase, const uint32_t (&ooff)[NOUT], uint4 (&x)[NIN],
                                             bool &have) {
     if constexpr (T::SYNC == 1) __builtin_amdgcn_s_barrier();  // the 4 waves start the tile together
     const uint32_t block = tile * TILE_BLOCKS + threadIdx.x;
     const bool active = block < MAIN_BLOCKS;
-    if (!(T::ROLL && have) && active) load_block<T, NIN>(x, ibase, ioff, block * COLS_PER_LANE);
+    if (!(T::ROLL && have) && active) load_block<T, NIN>(x, ibase, ioff, block * COLS_PER_LANE + phase);
     have = next;
     const uint32_t nblock = block + step * TILE_BLOCKS;
     // branch-free prefetch: lanes with no next block re-load their own block (an L2 hit)
-    const uint32_t ncol0 = (have && nblock < MAIN_BLOCKS ? nblock : block) * COLS_PER_LANE;
-    if (active) combine_block<T, NIN, NOUT>(lds, laneoff, x, obase, ooff, block * COLS_PER_LANE, ibase, ioff, ncol0);
+    const uint32_t ncol0 = (have && nblock < MAIN_BLOCKS ? nblock : block) * COLS_PER_LANE + phase;
+    if (active)
+        combine_block<T, NIN, NOUT>(lds, laneoff, x, obase, ooff, block * COLS_PER_LANE + phase, ibase, ioff, ncol0);
 }
 
 // Tiles [ta, tb) of one chunkset, branch-free (ROLL builds only): lanes past the last block use
@@ -510,17 +519,17 @@ __device__ __forceinline__ void stream_tile(const uint8_t *lds, uint32_t laneoff
 // for the inputs only.
 template <class T, int NIN, int NOUT>
 __device__ __forceinline__ void stream_range(const uint8_t *lds, uint32_t laneoff, uint32_t ta, uint32_t tb,
-                                             const uint8_t *ibase, const uint32_t (&ioff)[NIN], uint8_t *obase,
-                                             const uint32_t (&ooff)[NOUT], uint4 (&x)[NIN]) {
+                                             uint32_t phase, const uint8_t *ibase, const uint32_t (&ioff)[NIN],
+                                             uint8_t *obase, const uint32_t (&ooff)[NOUT], uint4 (&x)[NIN]) {
     static_assert(T::ROLL && T::LAUX >= 0 && T::SAUX >= 0, "branch-free streaming needs prefetch and buffer ops");
     uint32_t block = ta * TILE_BLOCKS + threadIdx.x;
-    load_block<T, NIN>(x, ibase, ioff, block < MAIN_BLOCKS ? block * COLS_PER_LANE : OOB_COL);
+    load_block<T, NIN>(x, ibase, ioff, block < MAIN_BLOCKS ? block * COLS_PER_LANE + phase : OOB_COL);
 #pragma unroll
     for (int j = 0; j < NOUT; j++) strow<T::SAUX>(obase, OOB_COL + ooff[j], make_uint4(0, 0, 0, 0));
     for (uint32_t t = ta; t < tb; t++, block += TILE_BLOCKS) {
         const uint32_t nblock = block + TILE_BLOCKS;
-        const uint32_t col0 = block < MAIN_BLOCKS ? block * COLS_PER_LANE : OOB_COL;
-        const uint32_t ncol0 = t + 1 < tb && nblock < MAIN_BLOCKS ? nblock * COLS_PER_LANE : OOB_COL;
+        const uint32_t col0 = block < MAIN_BLOCKS ? block * COLS_PER_LANE + phase : OOB_COL;
+        const uint32_t ncol0 = t + 1 < tb && nblock < MAIN_BLOCKS ? nblock * COLS_PER_LANE + phase : OOB_COL;
         combine_block<T, NIN, NOUT>(lds, laneoff, x, obase, ooff, col0, ibase, ioff, ncol0);
     }
 }
@@ -543,7 +552,7 @@ __device__ uint64_t g_trace[2][2 * TRACE_WAVES];
 template <int MAP>
 __global__ __launch_bounds__(WG, WAVES_PER_SIMD) __attribute__((amdgpu_waves_per_eu(WAVES_PER_SIMD, WAVES_PER_SIMD)))
 void rlnc_encode_kernel(const uint8_t *__restrict__ src, size_t n, const uint8_t *__restrict__ coeffs,
-                        uint8_t *__restrict__ dst, size_t pitch, uint32_t poly, uint32_t marker) {
+                        uint8_t *__restrict__ dst, size_t pitch, uint32_t phase, uint32_t poly, uint32_t marker) {
     TRACE_BEGIN(0);
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const uint32_t lane = threadIdx.x & 63u;
@@ -582,7 +591,7 @@ void rlnc_encode_kernel(const uint8_t *__restrict__ src, size_t n, const uint8_t
             if (tile0 == 0 && threadIdx.x < 64) {
                 for (uint32_t idx = lane; idx < N * K; idx += 64) obase[(idx / K) * pitch + idx % K] = M[idx];
                 for (uint32_t idx = lane; idx < TAIL_COLS * N; idx += 64) {
-                    const uint32_t j = idx % N, col = MAIN_COLS + idx / N;
+                    const uint32_t j = idx % N, col = edge_col(idx / N, phase);
                     uint32_t y = 0;
 #pragma unroll
                     for (uint32_t i = 0; i < K; i++) {
@@ -593,7 +602,8 @@ void rlnc_encode_kernel(const uint8_t *__restrict__ src, size_t n, const uint8_t
                     obase[j * pitch + K + col] = (uint8_t)y;
                 }
             }
-            stream_range<EncBfTune, K, N>(lds, laneoff, tile0, te - cs * TILES_PER_CS, ibase, ioff, obase, ooff, x);
+            stream_range<EncBfTune, K, N>(lds, laneoff, tile0, te - cs * TILES_PER_CS, phase, ibase, ioff, obase, ooff,
+                                          x);
             t0 = te;
         }
         TRACE_END(0);
@@ -622,9 +632,9 @@ void rlnc_encode_kernel(const uint8_t *__restrict__ src, size_t n, const uint8_t
         if (tile == 0 && threadIdx.x < 64) {
             // coding-vector prefix of the 16 full coded pieces (rlnc layout: cv || payload)
             for (uint32_t idx = lane; idx < N * K; idx += 64) obase[(idx / K) * pitch + idx % K] = M[idx];
-            // last 17 columns: piece 9 carries the boundary marker, then zero padding
+            // the 17 edge columns (edge_col): piece 9 carries the boundary marker, then zero padding
             for (uint32_t idx = lane; idx < TAIL_COLS * N; idx += 64) {
-                const uint32_t j = idx % N, col = MAIN_COLS + idx / N;
+                const uint32_t j = idx % N, col = edge_col(idx / N, phase);
                 uint32_t y = 0;
 #pragma unroll
                 for (uint32_t i = 0; i < K; i++) {
@@ -635,7 +645,7 @@ void rlnc_encode_kernel(const uint8_t *__restrict__ src, size_t n, const uint8_t
                 obase[j * pitch + K + col] = (uint8_t)y;
             }
         }
-        stream_tile<EncTune, K, N>(lds, laneoff, tile, step, next, ibase, ioff, obase, ooff, x, have);
+        stream_tile<EncTune, K, N>(lds, laneoff, tile, step, next, phase, ibase, ioff, obase, ooff, x, have);
     });
     TRACE_END(0);
 }
@@ -643,7 +653,8 @@ void rlnc_encode_kernel(const uint8_t *__restrict__ src, size_t n, const uint8_t
 template <int MAP>
 __global__ __launch_bounds__(WG, WAVES_PER_SIMD) __attribute__((amdgpu_waves_per_eu(WAVES_PER_SIMD, WAVES_PER_SIMD)))
 void rlnc_decode_kernel(const uint8_t *__restrict__ coded, size_t pitch, size_t n, const RepairPlan *__restrict__ plan,
-                        uint8_t *__restrict__ dst, int32_t *__restrict__ status, uint32_t poly, uint32_t marker) {
+                        uint8_t *__restrict__ dst, int32_t *__restrict__ status, uint32_t phase, uint32_t poly,
+                        uint32_t marker) {
     TRACE_BEGIN(1);
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const uint32_t lane = threadIdx.x & 63u;
@@ -680,11 +691,11 @@ void rlnc_decode_kernel(const uint8_t *__restrict__ coded, size_t pitch, size_t 
         ibase = coded + (size_t)cs * N * pitch;
         obase = dst + (size_t)cs * CS;
         if (tile0 == 0 && threadIdx.x < 64) {
-            // last 17 columns; piece 9's must decode to marker || zeros (rlnc
+            // the 17 edge columns (edge_col); piece 9's must decode to marker || zeros (rlnc
             // get_decoded_data strips them; a mismatch is a repairing failure)
             bool ok = true;
             for (uint32_t idx = lane; idx < TAIL_COLS * K; idx += 64) {
-                const uint32_t i = idx % K, col = MAIN_COLS + idx / K;
+                const uint32_t i = idx % K, col = edge_col(idx / K, phase);
                 uint32_t z = 0;
 #pragma unroll
                 for (uint32_t k = 0; k < K; k++) z ^= tbl_mul(lds, k, i, ibase[ioff[k] + col]);
@@ -696,7 +707,7 @@ void rlnc_decode_kernel(const uint8_t *__restrict__ coded, size_t pitch, size_t 
             }
             if (__any(!ok) && lane == 0) status[cs] = 6;  // DECDS_ERR_CHUNKSET_REPAIRING_FAILED
         }
-        stream_range<DT, K, K>(lds, laneoff, tile0, tile0 + T, ibase, ioff, obase, ooff, x);
+        stream_range<DT, K, K>(lds, laneoff, tile0, tile0 + T, phase, ibase, ioff, obase, ooff, x);
         TRACE_END(1);
         return;
     }
@@ -734,11 +745,11 @@ void rlnc_decode_kernel(const uint8_t *__restrict__ coded, size_t pitch, size_t 
         }
         if (!ready) return;
         if (tile == 0 && threadIdx.x < 64) {
-            // last 17 columns; piece 9's must decode to marker || zeros (rlnc
+            // the 17 edge columns (edge_col); piece 9's must decode to marker || zeros (rlnc
             // get_decoded_data strips them; a mismatch is a repairing failure)
             bool ok = true;
             for (uint32_t idx = lane; idx < TAIL_COLS * K; idx += 64) {
-                const uint32_t i = idx % K, col = MAIN_COLS + idx / K;
+                const uint32_t i = idx % K, col = edge_col(idx / K, phase);
                 uint32_t z = 0;
 #pragma unroll
                 for (uint32_t k = 0; k < K; k++) z ^= tbl_mul(lds, k, i, ibase[ioff[k] + col]);
@@ -750,7 +761,7 @@ void rlnc_decode_kernel(const uint8_t *__restrict__ coded, size_t pitch, size_t 
             }
             if (__any(!ok) && lane == 0) status[cs] = 6;  // DECDS_ERR_CHUNKSET_REPAIRING_FAILED
         }
-        stream_tile<DecTune, K, K>(lds, laneoff, tile, step, next, ibase, ioff, obase, ooff, x, have);
+        stream_tile<DecTune, K, K>(lds, laneoff, tile, step, next, phase, ibase, ioff, obase, ooff, x, have);
     });
     TRACE_END(1);
 }
@@ -1103,6 +1114,21 @@ constexpr int ENC_MAP_FALLBACK = 0, DEC_MAP_FALLBACK = 8;
 #ifndef DECDS_DEC_WS
 #define DECDS_DEC_WS 0
 #endif
+// Column phase of the coded rows' payloads (edge_col): with a 16-byte-aligned pitch every row's
+// payload (row + 10) has the same alignment, and blocks starting `phase` columns in are 16-byte
+// aligned. Encode uses it (its 16 row stores aligned: -2..-3 %); decode measured slower with its 10
+// row loads aligned (+3..+5 %) and keeps phase 0. Other pitches keep phase 0.
+#ifndef DECDS_ENC_PHASE
+#define DECDS_ENC_PHASE 1
+#endif
+#ifndef DECDS_DEC_PHASE
+#define DECDS_DEC_PHASE 0
+#endif
+static uint32_t row_phase(bool on, const uint8_t *rows, size_t pitch) {
+    if (!on || pitch % 16) return 0;
+    return (uint32_t)((16 - ((uintptr_t)rows + K) % 16) % 16);
+}
+
 static uint32_t ws_grid(const LaunchGeom &g, size_t n) {  // one workgroup per CU
     const uint64_t tiles = (uint64_t)n * TILES_PER_CS;
     return (uint32_t)(tiles < (uint64_t)g.num_cus ? tiles : (uint64_t)g.num_cus);
@@ -1139,18 +1165,19 @@ hipError_t launch_encode(const LaunchGeom &g, const uint8_t *src, size_t n, cons
                            (const RepairPlan *)nullptr, dst, pitch, (int32_t *)nullptr, poly, marker);
         return hipGetLastError();
     }
+    const uint32_t phase = row_phase(DECDS_ENC_PHASE, dst, pitch);
     uint32_t grid = stream_grid(g, n);
     if (DECDS_ENC_MAP < MAP_BAND) grid = (uint32_t)(((uint64_t)n * TILES_PER_CS + (-DECDS_ENC_MAP) - 1) / (-DECDS_ENC_MAP));
     if (DECDS_ENC_MAP == MAP_BAND && band_ok(grid & ~(NXCD - 1), n)) {
         grid &= ~(NXCD - 1);
         hipLaunchKernelGGL(rlnc_encode_kernel<DECDS_ENC_MAP>, dim3(grid), dim3(WG), LDS_BYTES, stream, src, n,
-                           coeffs, dst, pitch, poly, marker);
+                           coeffs, dst, pitch, phase, poly, marker);
     } else if (DECDS_ENC_MAP != MAP_BAND) {
         hipLaunchKernelGGL(rlnc_encode_kernel<DECDS_ENC_MAP>, dim3(grid), dim3(WG), LDS_BYTES, stream, src, n,
-                           coeffs, dst, pitch, poly, marker);
+                           coeffs, dst, pitch, phase, poly, marker);
     } else {
         hipLaunchKernelGGL(rlnc_encode_kernel<ENC_MAP_FALLBACK>, dim3(grid), dim3(WG), LDS_BYTES, stream, src, n,
-                           coeffs, dst, pitch, poly, marker);
+                           coeffs, dst, pitch, phase, poly, marker);
     }
     return hipGetLastError();
 }
@@ -1174,18 +1201,19 @@ hipError_t launch_decode(const LaunchGeom &g, const uint8_t *coded, size_t pitch
                            (const uint8_t *)nullptr, pl, dst, pitch, status, poly, marker);
         return hipGetLastError();
     }
+    const uint32_t phase = row_phase(DECDS_DEC_PHASE, coded, pitch);
     uint32_t grid = stream_grid(g, n);
     if (DECDS_DEC_MAP < MAP_BAND) grid = (uint32_t)(((uint64_t)n * TILES_PER_CS + (-DECDS_DEC_MAP) - 1) / (-DECDS_DEC_MAP));
     if (DECDS_DEC_MAP == MAP_BAND && band_ok(grid & ~(NXCD - 1), n)) {
         grid &= ~(NXCD - 1);
         hipLaunchKernelGGL(rlnc_decode_kernel<DECDS_DEC_MAP>, dim3(grid), dim3(WG), LDS_BYTES, stream, coded, pitch,
-                           n, pl, dst, status, poly, marker);
+                           n, pl, dst, status, phase, poly, marker);
     } else if (DECDS_DEC_MAP != MAP_BAND) {
         hipLaunchKernelGGL(rlnc_decode_kernel<DECDS_DEC_MAP>, dim3(grid), dim3(WG), LDS_BYTES, stream, coded, pitch,
-                           n, pl, dst, status, poly, marker);
+                           n, pl, dst, status, phase, poly, marker);
     } else {
         hipLaunchKernelGGL(rlnc_decode_kernel<DEC_MAP_FALLBACK>, dim3(grid), dim3(WG), LDS_BYTES, stream, coded,
-                           pitch, n, pl, dst, status, poly, marker);
+                           pitch, n, pl, dst, status, phase, poly, marker);
     }
     return hipGetLastError();
 }

@@ -32,11 +32,12 @@ def host(t):
     return t.cpu().numpy()
 
 
-def gpu_encode(ctx, data, coeffs, n, pitch=F):
+def gpu_encode(ctx, data, coeffs, n, pitch=F, off=0):
+    # off: the coded rows start `off` bytes into the allocation (another column phase, edge_col)
     src, cv = dev(data), dev(coeffs)
-    dst = torch.zeros((n * N - 1) * pitch + F, dtype=torch.uint8, device="cuda")
-    codec.encode_batch(ctx, src, n, cv, dst, pitch)
-    out = host(dst)
+    dst = torch.zeros(off + (n * N - 1) * pitch + F, dtype=torch.uint8, device="cuda")
+    codec.encode_batch(ctx, src, n, cv, dst[off:], pitch)
+    out = host(dst)[off:]
     return np.stack([out[r * pitch: r * pitch + F] for r in range(n * N)])
 
 
@@ -53,11 +54,13 @@ def test_encode_batch_bitexact_and_pitch(ctx):
     n = 5
     data = o.fill_random(0xDEC05002, n * CS)
     coeffs = o.fill_random(0xC0EF0002, n * N * K)
-    for pitch in (F, F + 53, 1 << 21):
-        coded = gpu_encode(ctx, data, coeffs, n, pitch)
+    refs = {c: o.chunkset_encode(data[c * CS:(c + 1) * CS], coeffs[c * 160:(c + 1) * 160], nthreads=8)
+            for c in (0, 2, 4)}
+    # 16-byte-aligned pitches run the blocks at column phase (6 - off) mod 16: head columns too
+    for pitch, off in ((F, 0), (F + 53, 0), (1 << 21, 0), (F + 5, 0), (F + 5, 3), (F + 5, 6), (F + 117, 15)):
+        coded = gpu_encode(ctx, data, coeffs, n, pitch, off)
         for c in (0, 2, 4):
-            ref = o.chunkset_encode(data[c * CS:(c + 1) * CS], coeffs[c * 160:(c + 1) * 160], nthreads=8)
-            assert np.array_equal(coded[c * N:(c + 1) * N], ref), (pitch, c)
+            assert np.array_equal(coded[c * N:(c + 1) * N], refs[c]), (pitch, off, c)
 
 
 def test_encode_decode_at_the_largest_pitch(ctx):
@@ -332,12 +335,14 @@ def test_cfg2_one_gib_encode_repair_device_resident(ctx):
     assert torch.equal(out[ok], src[ok])
 
 
-def test_repair_pitch_and_repeated_candidates(ctx):
-    # decode from a padded coded layout; a candidate row repeated in the arrival order is not useful
-    n, pitch = 2, F + 4093
+@pytest.mark.parametrize("pitch,off", [(F + 4093, 0), (F + 5, 0), (F + 5, 9)])
+def test_repair_pitch_and_repeated_candidates(ctx, pitch, off):
+    # decode from a padded coded layout (16-byte-aligned pitches: block loads at a column phase);
+    # a candidate row repeated in the arrival order is not useful
+    n = 2
     data = o.fill_random(0xDEC05004, n * CS)
     coeffs = o.fill_random(0xC0EF0004, n * N * K)
-    coded = torch.empty((n * N - 1) * pitch + F, dtype=torch.uint8, device="cuda")
+    coded = torch.empty(off + (n * N - 1) * pitch + F, dtype=torch.uint8, device="cuda")[off:]
     codec.encode_batch(ctx, dev(data), n, dev(coeffs), coded, pitch)
     cand = np.full((n, N), 0xFF, np.uint8)
     cand[0, :12] = [3, 3, 7, 1, 0, 15, 2, 9, 11, 4, 5, 6]
