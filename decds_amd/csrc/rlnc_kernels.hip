@@ -483,12 +483,18 @@ __device__ __forceinline__ void walk_tiles(size_t n, Fn &&f) {
     }
 }
 
-// Column phase: lane blocks cover payload columns [phase, phase + MAIN_COLS) (phase < 16, chosen by
-// the launcher so that rows with a 16-byte-aligned pitch are read / written on 16-byte boundaries);
-// the wave owning tile 0 does the 17 edge columns byte by byte: e < phase is column e, the rest the
-// columns after the last block.
+// Column phase: lane blocks cover payload columns from `phase` on (phase < 16, chosen by the
+// launcher so that rows with a 16-byte-aligned pitch are read / written on 16-byte boundaries); the
+// wave owning tile 0 does the edge columns byte by byte: e < phase is column e, the rest the columns
+// after the last block.
+// Piece 9's main columns must stay below CS - 9L (its marker and padding are edge columns), so a
+// phase above 7 gives up one block: 33 edge columns instead of 17.
+constexpr uint32_t MAX_FULL_PHASE = (uint32_t)(CS - (K - 1) * L) - MAIN_COLS;
+static_assert(MAX_FULL_PHASE == 7, "layout");
+__device__ __forceinline__ uint32_t main_blocks(uint32_t phase) { return MAIN_BLOCKS - (phase > MAX_FULL_PHASE); }
+__device__ __forceinline__ uint32_t edge_cols(uint32_t phase) { return (uint32_t)L - main_blocks(phase) * COLS_PER_LANE; }
 __device__ __forceinline__ uint32_t edge_col(uint32_t e, uint32_t phase) {
-    return e < phase ? e : MAIN_COLS + e;
+    return e < phase ? e : main_blocks(phase) * COLS_PER_LANE + e;
 }
 
 // One tile for this lane: inputs were prefetched by the previous tile when `have` (ROLL), else
@@ -500,12 +506,13 @@ __device__ __forceinline__ void stream_tile(const uint8_t *lds, uint32_t laneoff
                                             bool &have) {
     if constexpr (T::SYNC == 1) __builtin_amdgcn_s_barrier();  // the 4 waves start the tile together
     const uint32_t block = tile * TILE_BLOCKS + threadIdx.x;
-    const bool active = block < MAIN_BLOCKS;
+    const uint32_t nmain = main_blocks(phase);
+    const bool active = block < nmain;
     if (!(T::ROLL && have) && active) load_block<T, NIN>(x, ibase, ioff, block * COLS_PER_LANE + phase);
     have = next;
     const uint32_t nblock = block + step * TILE_BLOCKS;
     // branch-free prefetch: lanes with no next block re-load their own block (an L2 hit)
-    const uint32_t ncol0 = (have && nblock < MAIN_BLOCKS ? nblock : block) * COLS_PER_LANE + phase;
+    const uint32_t ncol0 = (have && nblock < nmain ? nblock : block) * COLS_PER_LANE + phase;
     if (active)
         combine_block<T, NIN, NOUT>(lds, laneoff, x, obase, ooff, block * COLS_PER_LANE + phase, ibase, ioff, ncol0);
 }
@@ -523,21 +530,28 @@ __device__ __forceinline__ void stream_range(const uint8_t *lds, uint32_t laneof
                                              uint8_t *obase, const uint32_t (&ooff)[NOUT], uint4 (&x)[NIN]) {
     static_assert(T::ROLL && T::LAUX >= 0 && T::SAUX >= 0, "branch-free streaming needs prefetch and buffer ops");
     uint32_t block = ta * TILE_BLOCKS + threadIdx.x;
-    load_block<T, NIN>(x, ibase, ioff, block < MAIN_BLOCKS ? block * COLS_PER_LANE + phase : OOB_COL);
+    const uint32_t nmain = main_blocks(phase);
+    load_block<T, NIN>(x, ibase, ioff, block < nmain ? block * COLS_PER_LANE + phase : OOB_COL);
+    asm volatile("" ::: "memory");  // keep the dropped stores after the loads, as in the loop
 #pragma unroll
     for (int j = 0; j < NOUT; j++) strow<T::SAUX>(obase, OOB_COL + ooff[j], make_uint4(0, 0, 0, 0));
-    for (uint32_t t = ta; t < tb; t++, block += TILE_BLOCKS) {
+    // ta < tb (callers): a do-while, so no zero-trip guard lets hipcc sink the prologue loads
+    // below the dropped stores
+    uint32_t t = ta;
+#pragma unroll 1
+    do {
         const uint32_t nblock = block + TILE_BLOCKS;
-        const uint32_t col0 = block < MAIN_BLOCKS ? block * COLS_PER_LANE + phase : OOB_COL;
-        const uint32_t ncol0 = t + 1 < tb && nblock < MAIN_BLOCKS ? nblock * COLS_PER_LANE + phase : OOB_COL;
+        const uint32_t col0 = block < nmain ? block * COLS_PER_LANE + phase : OOB_COL;
+        const uint32_t ncol0 = t + 1 < tb && nblock < nmain ? nblock * COLS_PER_LANE + phase : OOB_COL;
         combine_block<T, NIN, NOUT>(lds, laneoff, x, obase, ooff, col0, ibase, ioff, ncol0);
-    }
+        block += TILE_BLOCKS;
+    } while (++t < tb);
 }
 
 // Timing-study builds only (DECDS_TIMING_TRACE): every wave stamps its start and end with the
 // 100 MHz real-time counter; decds_debug_trace copies the stamps out (kernel 0 encode, 1 decode).
 #ifdef DECDS_TIMING_TRACE
-constexpr uint32_t TRACE_WAVES = 4096;
+constexpr uint32_t TRACE_WAVES = 65536;  // non-persistent launches: 128 waves per chunkset
 __device__ uint64_t g_trace[2][2 * TRACE_WAVES];
 #define TRACE_BEGIN(k)                                                                              \
     const uint32_t trace_w_ = blockIdx.x * (WG / 64) + threadIdx.x / 64;                            \
@@ -568,19 +582,9 @@ void rlnc_encode_kernel(const uint8_t *__restrict__ src, size_t n, const uint8_t
     const uint8_t *M = coeffs;
     uint4 x[K];
     if constexpr (DECDS_ENC_BF && (MAP == 0 || MAP < MAP_BAND)) {
-        // this workgroup's tile range, walked one chunkset segment at a time: rebuild the tables,
-        // then stream the segment branch-free
-        uint32_t t0, t1;
-        if constexpr (MAP == 0) {
-            tile_range<DECDS_ENC_SHARE>(n, t0, t1);
-        } else {
-            const uint64_t total = (uint64_t)n * TILES_PER_CS;
-            t0 = np_block<DECDS_ENC_XCD_REMAP>() * (uint32_t)(-MAP);
-            t1 = (uint32_t)(t0 - MAP < total ? t0 - MAP : total);
-        }
-        while (t0 < t1) {
+        // one chunkset segment [t0, te): rebuild the tables, then stream it branch-free
+        auto segment = [&](uint32_t t0, uint32_t te) {
             const uint32_t cs = t0 / TILES_PER_CS, tile0 = t0 % TILES_PER_CS;
-            const uint32_t te = (cs + 1) * TILES_PER_CS < t1 ? (cs + 1) * TILES_PER_CS : t1;
             M = coeffs + (size_t)cs * N * K;
             const uint32_t cw = table_coeffs<K, N>(M, K);
             lds_barrier();
@@ -590,7 +594,7 @@ void rlnc_encode_kernel(const uint8_t *__restrict__ src, size_t n, const uint8_t
             obase = dst + (size_t)cs * N * pitch;
             if (tile0 == 0 && threadIdx.x < 64) {
                 for (uint32_t idx = lane; idx < N * K; idx += 64) obase[(idx / K) * pitch + idx % K] = M[idx];
-                for (uint32_t idx = lane; idx < TAIL_COLS * N; idx += 64) {
+                for (uint32_t idx = lane; idx < edge_cols(phase) * N; idx += 64) {
                     const uint32_t j = idx % N, col = edge_col(idx / N, phase);
                     uint32_t y = 0;
 #pragma unroll
@@ -604,7 +608,24 @@ void rlnc_encode_kernel(const uint8_t *__restrict__ src, size_t n, const uint8_t
             }
             stream_range<EncBfTune, K, N>(lds, laneoff, tile0, te - cs * TILES_PER_CS, phase, ibase, ioff, obase, ooff,
                                           x);
-            t0 = te;
+        };
+        auto walk_range = [&](uint32_t t0, uint32_t t1) {
+            while (t0 < t1) {
+                const uint32_t cs_end = (t0 / TILES_PER_CS + 1) * TILES_PER_CS;
+                const uint32_t te = cs_end < t1 ? cs_end : t1;
+                segment(t0, te);
+                t0 = te;
+            }
+        };
+        if constexpr (MAP == 0) {
+            uint32_t t0, t1;
+            tile_range<DECDS_ENC_SHARE>(n, t0, t1);
+            walk_range(t0, t1);
+        } else if constexpr (MAP < MAP_BAND) {
+            // non-persistent: T = -MAP tiles, then exit
+            const uint64_t total = (uint64_t)n * TILES_PER_CS;
+            const uint32_t t0 = np_block<DECDS_ENC_XCD_REMAP>() * (uint32_t)(-MAP);
+            walk_range(t0, (uint32_t)(t0 - MAP < total ? t0 - MAP : total));
         }
         TRACE_END(0);
         return;
@@ -632,8 +653,8 @@ void rlnc_encode_kernel(const uint8_t *__restrict__ src, size_t n, const uint8_t
         if (tile == 0 && threadIdx.x < 64) {
             // coding-vector prefix of the 16 full coded pieces (rlnc layout: cv || payload)
             for (uint32_t idx = lane; idx < N * K; idx += 64) obase[(idx / K) * pitch + idx % K] = M[idx];
-            // the 17 edge columns (edge_col): piece 9 carries the boundary marker, then zero padding
-            for (uint32_t idx = lane; idx < TAIL_COLS * N; idx += 64) {
+            // the edge columns (edge_col): piece 9 carries the boundary marker, then zero padding
+            for (uint32_t idx = lane; idx < edge_cols(phase) * N; idx += 64) {
                 const uint32_t j = idx % N, col = edge_col(idx / N, phase);
                 uint32_t y = 0;
 #pragma unroll
@@ -691,10 +712,10 @@ void rlnc_decode_kernel(const uint8_t *__restrict__ coded, size_t pitch, size_t 
         ibase = coded + (size_t)cs * N * pitch;
         obase = dst + (size_t)cs * CS;
         if (tile0 == 0 && threadIdx.x < 64) {
-            // the 17 edge columns (edge_col); piece 9's must decode to marker || zeros (rlnc
+            // the edge columns (edge_col); piece 9's must decode to marker || zeros (rlnc
             // get_decoded_data strips them; a mismatch is a repairing failure)
             bool ok = true;
-            for (uint32_t idx = lane; idx < TAIL_COLS * K; idx += 64) {
+            for (uint32_t idx = lane; idx < edge_cols(phase) * K; idx += 64) {
                 const uint32_t i = idx % K, col = edge_col(idx / K, phase);
                 uint32_t z = 0;
 #pragma unroll
@@ -745,10 +766,10 @@ void rlnc_decode_kernel(const uint8_t *__restrict__ coded, size_t pitch, size_t 
         }
         if (!ready) return;
         if (tile == 0 && threadIdx.x < 64) {
-            // the 17 edge columns (edge_col); piece 9's must decode to marker || zeros (rlnc
+            // the edge columns (edge_col); piece 9's must decode to marker || zeros (rlnc
             // get_decoded_data strips them; a mismatch is a repairing failure)
             bool ok = true;
-            for (uint32_t idx = lane; idx < TAIL_COLS * K; idx += 64) {
+            for (uint32_t idx = lane; idx < edge_cols(phase) * K; idx += 64) {
                 const uint32_t i = idx % K, col = edge_col(idx / K, phase);
                 uint32_t z = 0;
 #pragma unroll

@@ -63,6 +63,20 @@ def test_encode_batch_bitexact_and_pitch(ctx):
             assert np.array_equal(coded[c * N:(c + 1) * N], refs[c]), (pitch, off, c)
 
 
+def test_encode_every_column_phase(ctx):
+    # a 16-byte-aligned pitch at each of the 16 base offsets runs the encode blocks at each column
+    # phase; above phase 7 the last block becomes edge columns (piece 9 must not read past the
+    # chunkset into its marker / padding), so 2 chunksets, the first one's neighbour readable
+    n, pitch = 2, F + 5
+    data = o.fill_random(0xDEC05005, n * CS)
+    coeffs = o.fill_random(0xC0EF0005, n * N * K)
+    refs = [o.chunkset_encode(data[c * CS:(c + 1) * CS], coeffs[c * 160:(c + 1) * 160], nthreads=8) for c in range(n)]
+    for off in range(16):
+        coded = gpu_encode(ctx, data, coeffs, n, pitch, off)
+        for c in range(n):
+            assert np.array_equal(coded[c * N:(c + 1) * N], refs[c]), (off, c)
+
+
 def test_encode_decode_at_the_largest_pitch(ctx):
     # a chunkset's 16 rows must fit one 2 GiB buffer descriptor (include/decds_rlnc.h): the largest
     # pitch is bit-exact through encode and repair (lanes past the last block use out-of-range

@@ -12,14 +12,28 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
+TRACE_WAVES = 65536
+
+
 def summarise(st, n_waves):
     import numpy as np
     s = st.reshape(-1, 2)[:n_waves].astype(np.int64)
+    s = s[(s[:, 0] > 0) & (s[:, 1] > 0)]
+    n_waves = len(s)
     t0 = s[:, 0].min()
     start, end = (s[:, 0] - t0) / 100.0, (s[:, 1] - t0) / 100.0   # microseconds
     q = np.percentile(end, [0, 10, 50, 90, 99, 100])
-    return {"start_max_us": round(float(start.max()), 2), "end_us_p0_p10_p50_p90_p99_p100": [round(float(v), 1) for v in q],
-            "tail_us": round(float(q[5] - q[2]), 1), "busy_frac": round(float((end - start).sum() / (n_waves * q[5])), 3)}
+    # resident waves over time (20 bins over the launch) and per-wave durations
+    bins = np.linspace(0, q[5], 21)
+    mid = (bins[:-1] + bins[1:]) / 2
+    resident = [int(((start <= t) & (end > t)).sum()) for t in mid]
+    dur = end - start
+    return {"waves": n_waves, "start_max_us": round(float(start.max()), 2),
+            "end_us_p0_p10_p50_p90_p99_p100": [round(float(v), 1) for v in q],
+            "tail_us": round(float(q[5] - q[2]), 1), "busy_frac": round(float(dur.sum() / (n_waves * q[5])), 3),
+            "wave_us_p10_p50_p90": [round(float(v), 1) for v in np.percentile(dur, [10, 50, 90])],
+            "first_end_us": round(float(end.min()), 1), "last_start_us": round(float(start.max()), 1),
+            "resident_20bins": resident}
 
 
 def main():
@@ -58,17 +72,17 @@ def main():
     for r in range(a.reps):
         assert L.decds_encode_batch(h, vp(src.data_ptr()), n, vp(coeffs.data_ptr()), vp(coded.data_ptr()), F, sp) == 0
         st.synchronize()
-        enc = np.zeros(2 * 4096, np.uint64)
+        enc = np.zeros(2 * TRACE_WAVES, np.uint64)
         assert L.decds_debug_trace(0, enc.ctypes.data) == 0
         assert L.decds_repair_plan_batch(h, vp(coded.data_ptr()), F, n, vp(cand.data_ptr()), vp(plan.data_ptr()),
                                          vp(verd.data_ptr()), vp(status.data_ptr()), sp) == 0
         assert L.decds_decode_batch(h, vp(coded.data_ptr()), F, n, vp(plan.data_ptr()), vp(out.data_ptr()),
                                     vp(status.data_ptr()), sp) == 0
         st.synchronize()
-        dec = np.zeros(2 * 4096, np.uint64)
+        dec = np.zeros(2 * TRACE_WAVES, np.uint64)
         assert L.decds_debug_trace(1, dec.ctypes.data) == 0
         if r >= 2:
-            res["runs"].append({"encode": summarise(enc, 2048), "decode": summarise(dec, 2048)})
+            res["runs"].append({"encode": summarise(enc, TRACE_WAVES), "decode": summarise(dec, TRACE_WAVES)})
     if a.dump:
         np.savez(a.dump, encode=enc, decode=dec)
     print(json.dumps(res), flush=True)
