@@ -52,7 +52,7 @@ struct Tune {
 #define DECDS_ENC_TUNE false, false, -1, -1
 #endif
 #ifndef DECDS_DEC_TUNE
-#define DECDS_DEC_TUNE true, true, -1, 2
+#define DECDS_DEC_TUNE true, true, -1, 0
 #endif
 #ifndef DECDS_ENC_SYNC
 #define DECDS_ENC_SYNC 0
