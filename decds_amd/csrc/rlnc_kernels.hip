@@ -379,6 +379,14 @@ constexpr uint32_t NXCD = 8;
 #ifndef DECDS_ENC_MAP
 #define DECDS_ENC_MAP -8
 #endif
+// batches of at most DECDS_ENC_SMALL_N chunksets encode in units of 4 tiles (finer-grained at the
+// end of a short launch: -3 % at 103 chunksets on two boxes; at 1639 units of 8 were -6 % / +1.5 %)
+#ifndef DECDS_ENC_MAP_SMALL
+#define DECDS_ENC_MAP_SMALL -4
+#endif
+#ifndef DECDS_ENC_SMALL_N
+#define DECDS_ENC_SMALL_N 512
+#endif
 #ifndef DECDS_DEC_MAP
 #define DECDS_DEC_MAP -8
 #endif
@@ -1157,6 +1165,7 @@ static uint32_t ws_grid(const LaunchGeom &g, size_t n) {  // one workgroup per C
 
 hipError_t configure_kernels() {
     const void *fns[] = {reinterpret_cast<const void *>(rlnc_encode_kernel<DECDS_ENC_MAP>),
+                         reinterpret_cast<const void *>(rlnc_encode_kernel<DECDS_ENC_MAP_SMALL>),
                          reinterpret_cast<const void *>(rlnc_encode_kernel<ENC_MAP_FALLBACK>),
                          reinterpret_cast<const void *>(rlnc_decode_kernel<DECDS_DEC_MAP>),
                          reinterpret_cast<const void *>(rlnc_decode_kernel<DEC_MAP_FALLBACK>)};
@@ -1187,6 +1196,12 @@ hipError_t launch_encode(const LaunchGeom &g, const uint8_t *src, size_t n, cons
         return hipGetLastError();
     }
     const uint32_t phase = row_phase(DECDS_ENC_PHASE, dst, pitch);
+    if (DECDS_ENC_MAP < MAP_BAND && DECDS_ENC_MAP_SMALL < MAP_BAND && n <= DECDS_ENC_SMALL_N) {
+        constexpr uint32_t T = (uint32_t)(-DECDS_ENC_MAP_SMALL);
+        hipLaunchKernelGGL(rlnc_encode_kernel<DECDS_ENC_MAP_SMALL>, dim3((uint32_t)((n * TILES_PER_CS + T - 1) / T)),
+                           dim3(WG), LDS_BYTES, stream, src, n, coeffs, dst, pitch, phase, poly, marker);
+        return hipGetLastError();
+    }
     uint32_t grid = stream_grid(g, n);
     if (DECDS_ENC_MAP < MAP_BAND) grid = (uint32_t)(((uint64_t)n * TILES_PER_CS + (-DECDS_ENC_MAP) - 1) / (-DECDS_ENC_MAP));
     if (DECDS_ENC_MAP == MAP_BAND && band_ok(grid & ~(NXCD - 1), n)) {
