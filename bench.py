@@ -20,6 +20,7 @@ sys.path.insert(0, ROOT)
 
 GIB = float(1 << 30)
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+HBM_COPY_GBS = 6290.0  # MI355X_MICROARCH.md: 6.29 TB/s measured float4 copy (SURVEY.md §8d second denominator)
 SWEEP = (256, 1024, 1639)  # encode batch sweep: chunksets per launch (1639 = the 16 GiB blob of cfg3)
 
 CONFIGS = {
@@ -242,7 +243,8 @@ def main():
                        "blob_bytes_per_gpu": blob_per_gpu, "survivors_per_chunkset": K,
                        "parallelism": "chunkset-index shards x%d, no collective" % world},
             "roofline": {"bound": "hbm", "kernel": dominant, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic},
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "copy_ceiling": HBM_COPY_GBS, "frac_of_copy": round(achieved / HBM_COPY_GBS, 4)},
             "breakdown": {"encode_ms": round(enc_ms, 4), "plan_ms": round(plan_ms, 4), "decode_ms": round(dec_ms, 4),
                           "encode_GBps": round(enc_gbs, 1), "decode_GBps": round(dec_gbs, 1),
                           "encode_blob_GiBps": round(n * CS / GIB / (enc_ms * 1e-3), 1),
