@@ -21,7 +21,7 @@ sys.path.insert(0, ROOT)
 GIB = float(1 << 30)
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 HBM_COPY_GBS = 6290.0  # MI355X_MICROARCH.md: 6.29 TB/s measured float4 copy (SURVEY.md §8d second denominator)
-SWEEP = (256, 1024, 1639)  # encode batch sweep: chunksets per launch (1639 = the 16 GiB blob of cfg3)
+SWEEP = (1, 16, 64, 256, 1024, 1639)  # encode batch sweep: chunksets per launch
 
 CONFIGS = {
     # name: (blob bytes per GPU, description)
@@ -201,7 +201,7 @@ def main():
             obig = torch.empty(nmax * N * F, dtype=torch.uint8, device=dev)
         sweep = []
         for ns in SWEEP:
-            reps = 3 if ns >= 1024 else 5
+            reps = 3 if ns >= 1024 else 5 if ns >= 256 else 20
             codec.encode_batch(ctx, big, ns, cbig, obig, stream=stream)
             sev = [torch.cuda.Event(enable_timing=True) for _ in range(reps + 1)]
             sev[0].record(stream)
