@@ -387,6 +387,12 @@ constexpr uint32_t NXCD = 8;
 #ifndef DECDS_ENC_SMALL_N
 #define DECDS_ENC_SMALL_N 512
 #endif
+// tiny decode batches (single RepairingChunkSet repairs): a chunkset is only 256 tiles, 32 workgroups
+// of 8; units of 2 / 4 tiles for n <= 2 / 4 keep about 256 workgroups (-7 % / -28 % at n = 2 / 4).
+// Encode measured slower with smaller units there (units of 1 / 2: +40…+90 % at n = 1 / 2).
+#ifndef DECDS_TINY_MAPS
+#define DECDS_TINY_MAPS 1
+#endif
 #ifndef DECDS_DEC_MAP
 #define DECDS_DEC_MAP -8
 #endif
@@ -600,9 +606,9 @@ void rlnc_encode_kernel(const uint8_t *__restrict__ src, size_t n, const uint8_t
             lds_barrier();
             ibase = src + (size_t)cs * CS;
             obase = dst + (size_t)cs * N * pitch;
-            if (tile0 == 0 && threadIdx.x < 64) {
-                for (uint32_t idx = lane; idx < N * K; idx += 64) obase[(idx / K) * pitch + idx % K] = M[idx];
-                for (uint32_t idx = lane; idx < edge_cols(phase) * N; idx += 64) {
+            if (tile0 == 0) {  // the whole workgroup: one pass over the edge columns
+                for (uint32_t idx = threadIdx.x; idx < N * K; idx += WG) obase[(idx / K) * pitch + idx % K] = M[idx];
+                for (uint32_t idx = threadIdx.x; idx < edge_cols(phase) * N; idx += WG) {
                     const uint32_t j = idx % N, col = edge_col(idx / N, phase);
                     uint32_t y = 0;
 #pragma unroll
@@ -658,11 +664,11 @@ void rlnc_encode_kernel(const uint8_t *__restrict__ src, size_t n, const uint8_t
             ibase = src + (size_t)cs * CS;
             obase = dst + (size_t)cs * N * pitch;
         }
-        if (tile == 0 && threadIdx.x < 64) {
+        if (tile == 0) {
             // coding-vector prefix of the 16 full coded pieces (rlnc layout: cv || payload)
-            for (uint32_t idx = lane; idx < N * K; idx += 64) obase[(idx / K) * pitch + idx % K] = M[idx];
+            for (uint32_t idx = threadIdx.x; idx < N * K; idx += WG) obase[(idx / K) * pitch + idx % K] = M[idx];
             // the edge columns (edge_col): piece 9 carries the boundary marker, then zero padding
-            for (uint32_t idx = lane; idx < edge_cols(phase) * N; idx += 64) {
+            for (uint32_t idx = threadIdx.x; idx < edge_cols(phase) * N; idx += WG) {
                 const uint32_t j = idx % N, col = edge_col(idx / N, phase);
                 uint32_t y = 0;
 #pragma unroll
@@ -719,11 +725,11 @@ void rlnc_decode_kernel(const uint8_t *__restrict__ coded, size_t pitch, size_t 
         for (int k = 0; k < (int)K; k++) ioff[k] = (uint32_t)(sel[k] * pitch + K);
         ibase = coded + (size_t)cs * N * pitch;
         obase = dst + (size_t)cs * CS;
-        if (tile0 == 0 && threadIdx.x < 64) {
+        if (tile0 == 0) {  // the whole workgroup: one pass over the edge columns
             // the edge columns (edge_col); piece 9's must decode to marker || zeros (rlnc
             // get_decoded_data strips them; a mismatch is a repairing failure)
             bool ok = true;
-            for (uint32_t idx = lane; idx < edge_cols(phase) * K; idx += 64) {
+            for (uint32_t idx = threadIdx.x; idx < edge_cols(phase) * K; idx += WG) {
                 const uint32_t i = idx % K, col = edge_col(idx / K, phase);
                 uint32_t z = 0;
 #pragma unroll
@@ -773,11 +779,11 @@ void rlnc_decode_kernel(const uint8_t *__restrict__ coded, size_t pitch, size_t 
             }
         }
         if (!ready) return;
-        if (tile == 0 && threadIdx.x < 64) {
+        if (tile == 0) {
             // the edge columns (edge_col); piece 9's must decode to marker || zeros (rlnc
             // get_decoded_data strips them; a mismatch is a repairing failure)
             bool ok = true;
-            for (uint32_t idx = lane; idx < edge_cols(phase) * K; idx += 64) {
+            for (uint32_t idx = threadIdx.x; idx < edge_cols(phase) * K; idx += WG) {
                 const uint32_t i = idx % K, col = edge_col(idx / K, phase);
                 uint32_t z = 0;
 #pragma unroll
@@ -1166,6 +1172,8 @@ static uint32_t ws_grid(const LaunchGeom &g, size_t n) {  // one workgroup per C
 hipError_t configure_kernels() {
     const void *fns[] = {reinterpret_cast<const void *>(rlnc_encode_kernel<DECDS_ENC_MAP>),
                          reinterpret_cast<const void *>(rlnc_encode_kernel<DECDS_ENC_MAP_SMALL>),
+                         reinterpret_cast<const void *>(rlnc_decode_kernel<-2>),
+                         reinterpret_cast<const void *>(rlnc_decode_kernel<-4>),
                          reinterpret_cast<const void *>(rlnc_encode_kernel<ENC_MAP_FALLBACK>),
                          reinterpret_cast<const void *>(rlnc_decode_kernel<DECDS_DEC_MAP>),
                          reinterpret_cast<const void *>(rlnc_decode_kernel<DEC_MAP_FALLBACK>)};
@@ -1196,12 +1204,15 @@ hipError_t launch_encode(const LaunchGeom &g, const uint8_t *src, size_t n, cons
         return hipGetLastError();
     }
     const uint32_t phase = row_phase(DECDS_ENC_PHASE, dst, pitch);
-    if (DECDS_ENC_MAP < MAP_BAND && DECDS_ENC_MAP_SMALL < MAP_BAND && n <= DECDS_ENC_SMALL_N) {
-        constexpr uint32_t T = (uint32_t)(-DECDS_ENC_MAP_SMALL);
-        hipLaunchKernelGGL(rlnc_encode_kernel<DECDS_ENC_MAP_SMALL>, dim3((uint32_t)((n * TILES_PER_CS + T - 1) / T)),
-                           dim3(WG), LDS_BYTES, stream, src, n, coeffs, dst, pitch, phase, poly, marker);
+    auto np = [&](auto map) {  // non-persistent launch, units of T = -MAP tiles
+        constexpr int MAP = decltype(map)::value;
+        constexpr uint32_t T = (uint32_t)(-MAP);
+        hipLaunchKernelGGL(rlnc_encode_kernel<MAP>, dim3((uint32_t)((n * TILES_PER_CS + T - 1) / T)), dim3(WG),
+                           LDS_BYTES, stream, src, n, coeffs, dst, pitch, phase, poly, marker);
         return hipGetLastError();
-    }
+    };
+    if (DECDS_ENC_MAP < MAP_BAND && DECDS_ENC_MAP_SMALL < MAP_BAND && n <= DECDS_ENC_SMALL_N)
+        return np(std::integral_constant<int, DECDS_ENC_MAP_SMALL>{});
     uint32_t grid = stream_grid(g, n);
     if (DECDS_ENC_MAP < MAP_BAND) grid = (uint32_t)(((uint64_t)n * TILES_PER_CS + (-DECDS_ENC_MAP) - 1) / (-DECDS_ENC_MAP));
     if (DECDS_ENC_MAP == MAP_BAND && band_ok(grid & ~(NXCD - 1), n)) {
@@ -1238,6 +1249,15 @@ hipError_t launch_decode(const LaunchGeom &g, const uint8_t *coded, size_t pitch
         return hipGetLastError();
     }
     const uint32_t phase = row_phase(DECDS_DEC_PHASE, coded, pitch);
+    auto np = [&](auto map) {  // non-persistent launch, units of T = -MAP tiles
+        constexpr int MAP = decltype(map)::value;
+        constexpr uint32_t T = (uint32_t)(-MAP);
+        hipLaunchKernelGGL(rlnc_decode_kernel<MAP>, dim3((uint32_t)((n * TILES_PER_CS + T - 1) / T)), dim3(WG),
+                           LDS_BYTES, stream, coded, pitch, n, pl, dst, status, phase, poly, marker);
+        return hipGetLastError();
+    };
+    if (DECDS_DEC_MAP < MAP_BAND && DECDS_TINY_MAPS && n <= 2) return np(std::integral_constant<int, -2>{});
+    if (DECDS_DEC_MAP < MAP_BAND && DECDS_TINY_MAPS && n <= 4) return np(std::integral_constant<int, -4>{});
     uint32_t grid = stream_grid(g, n);
     if (DECDS_DEC_MAP < MAP_BAND) grid = (uint32_t)(((uint64_t)n * TILES_PER_CS + (-DECDS_DEC_MAP) - 1) / (-DECDS_DEC_MAP));
     if (DECDS_DEC_MAP == MAP_BAND && band_ok(grid & ~(NXCD - 1), n)) {
