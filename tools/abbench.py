@@ -20,6 +20,8 @@ def main():
     ap.add_argument("--n", type=int, default=1639)
     ap.add_argument("--rounds", type=int, default=12)
     ap.add_argument("--warmup-s", type=float, default=3.0)
+    ap.add_argument("--alloc-n", type=int, default=0, help="size the buffers for this many chunksets (>= n)")
+    ap.add_argument("--at", type=int, default=0, help="run on chunksets [at, at + n) of the buffers")
     ap.add_argument("libs", nargs="+")
     a = ap.parse_args()
     import numpy as np
@@ -27,6 +29,7 @@ def main():
     from decds_amd._capi import CHUNKSET_BYTES as CS, CODED_PIECE_BYTES as F, K, N, _declare
 
     n = a.n
+    na = max(a.alloc_n, n + a.at)
     builds = []
     for spec in a.libs:
         path, _, pitch = spec.partition(":")
@@ -41,7 +44,8 @@ def main():
     maxpitch = max(b["pitch"] for b in builds)
     st = torch.cuda.Stream()
     vp = ctypes.c_void_p
-    src = torch.empty(n * maxcs + 64, dtype=torch.uint8, device="cuda")
+    src_all = torch.empty(na * maxcs + 64, dtype=torch.uint8, device="cuda")
+    src = src_all[a.at * maxcs:]
     builds[0]["lib"].decds_fill_random_device(builds[0]["ctx"], 1, 0, vp(src.data_ptr()), src.numel(), vp(st.cuda_stream))
     coeffs = torch.from_numpy(np.random.default_rng(2).integers(0, 256, n * N * K, dtype=np.uint8)).cuda()
     rng = np.random.default_rng(3)
@@ -49,11 +53,13 @@ def main():
     for c in range(n):
         cand[c, :K] = rng.permutation(N)[:K]
     cand = torch.from_numpy(cand).cuda()
-    coded = torch.empty(n * N * maxpitch + 64, dtype=torch.uint8, device="cuda")
+    coded_all = torch.empty(na * N * maxpitch + 64, dtype=torch.uint8, device="cuda")
+    coded = coded_all[a.at * N * maxpitch:]
     plan = torch.empty(n * 128, dtype=torch.uint8, device="cuda")
     verd = torch.empty(n * N, dtype=torch.int8, device="cuda")
     status = torch.empty(n, dtype=torch.int32, device="cuda")
-    out = torch.empty(n * maxcs + 64, dtype=torch.uint8, device="cuda")
+    out_all = torch.empty(na * maxcs + 64, dtype=torch.uint8, device="cuda")
+    out = out_all[a.at * maxcs:]
     torch.cuda.synchronize()
     sp = vp(st.cuda_stream)
 
@@ -87,7 +93,7 @@ def main():
     for b in builds:
         t = np.array(b["t"])
         med, mn = np.median(t, axis=0), t.min(axis=0)
-        print(json.dumps({"tag": b["tag"], "n": n, "pitch": b["pitch"], "encode_ms": round(med[0], 4),
+        print(json.dumps({"tag": b["tag"], "n": n, "alloc_n": na, "at": a.at, "pitch": b["pitch"], "encode_ms": round(med[0], 4),
                           "encode_min_ms": round(mn[0], 4), "plan_ms": round(med[1], 4), "decode_ms": round(med[2], 4),
                           "decode_min_ms": round(mn[2], 4), "encode_GBps": round(n * (CS + N * F) / med[0] / 1e6, 1),
                           "decode_GBps": round(n * (K * F + CS) / med[2] / 1e6, 1)}), flush=True)
