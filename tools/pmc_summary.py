@@ -49,6 +49,14 @@ def main():
             traffic["kernels"][name] = {"hbm_bytes_per_launch": round((2 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024),
                                         "fetch_bytes_corrected": round(2 * c["FETCH_SIZE"] * 1024),
                                         "write_bytes": round(c["WRITE_SIZE"] * 1024)}
+    # the bench line printed by the profiled run itself: its HIP-event averages are for the same
+    # launches as the kernel trace
+    tlog = os.path.join(src, "trace.log")
+    if os.path.exists(tlog):
+        for line in open(tlog):
+            if line.startswith("{") and '"metric"' in line:
+                with open(os.path.join(prof, "%s_bench_traced.json" % tag), "w") as f:
+                    f.write(line)
     with open(os.path.join(prof, "traffic.json"), "w") as f:
         json.dump(traffic, f, indent=1)
     print(json.dumps(traffic, indent=1))
