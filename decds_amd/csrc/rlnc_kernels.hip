@@ -543,22 +543,22 @@ __device__ __forceinline__ void stream_range(const uint8_t *lds, uint32_t laneof
                                              uint32_t phase, const uint8_t *ibase, const uint32_t (&ioff)[NIN],
                                              uint8_t *obase, const uint32_t (&ooff)[NOUT], uint4 (&x)[NIN]) {
     static_assert(T::ROLL && T::LAUX >= 0 && T::SAUX >= 0, "branch-free streaming needs prefetch and buffer ops");
-    uint32_t block = ta * TILE_BLOCKS + threadIdx.x;
     const uint32_t nmain = main_blocks(phase);
-    load_block<T, NIN>(x, ibase, ioff, block < nmain ? block * COLS_PER_LANE + phase : OOB_COL);
+    auto col = [&](uint32_t t) {  // this lane's first column of tile t, or out of range
+        const uint32_t block = t * TILE_BLOCKS + threadIdx.x;
+        return t < tb && block < nmain ? block * COLS_PER_LANE + phase : OOB_COL;
+    };
+    load_block<T, NIN>(x, ibase, ioff, col(ta));
     asm volatile("" ::: "memory");  // keep the dropped stores after the loads, as in the loop
 #pragma unroll
     for (int j = 0; j < NOUT; j++) strow<T::SAUX>(obase, OOB_COL + ooff[j], make_uint4(0, 0, 0, 0));
     // ta < tb (callers): a do-while, so no zero-trip guard lets hipcc sink the prologue loads
-    // below the dropped stores
+    // below the dropped stores. (Two tiles in flight — a second register set, swapped per tile —
+    // needs 256 VGPRs and spills in decode; measured not worth it)
     uint32_t t = ta;
 #pragma unroll 1
     do {
-        const uint32_t nblock = block + TILE_BLOCKS;
-        const uint32_t col0 = block < nmain ? block * COLS_PER_LANE + phase : OOB_COL;
-        const uint32_t ncol0 = t + 1 < tb && nblock < nmain ? nblock * COLS_PER_LANE + phase : OOB_COL;
-        combine_block<T, NIN, NOUT>(lds, laneoff, x, obase, ooff, col0, ibase, ioff, ncol0);
-        block += TILE_BLOCKS;
+        combine_block<T, NIN, NOUT>(lds, laneoff, x, obase, ooff, col(t), ibase, ioff, col(t + 1));
     } while (++t < tb);
 }
 
