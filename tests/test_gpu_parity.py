@@ -426,3 +426,38 @@ def test_encode_large_n_last_chunkset_bounds(ctx):
     c = n - 1
     ref = o.chunkset_encode(src[c * CS:].cpu().numpy(), coeffs[c * 160:], nthreads=8)
     assert np.array_equal(coded[c * N * F:].cpu().numpy().reshape(N, F), ref)
+
+
+@pytest.mark.parametrize("trial", range(6))
+def test_randomized_layouts_encode_repair(ctx, trial):
+    # seeded random batch shapes through both kernels: batch sizes that pick every unit size
+    # (encode 4 / decode 2 / 4 / 8 tiles), rlnc-pitch and 16-byte-aligned pitches at any base offset
+    # (column phases 0..15), survivor subsets of 10..16 rows in random arrival order
+    rng = np.random.default_rng(0x7A1A1 + trial)
+    n = int(rng.choice([1, 2, 3, 4, 5, 9, 17]))
+    pitch = int(rng.choice([F, F + 1, F + 5, F + 13, F + 117, F + 4096, 1 << 21]))
+    off = int(rng.integers(0, 16))
+    data = o.fill_random(0xDEC06000 + trial, n * CS)
+    coeffs = o.fill_random(0xC0EF6000 + trial, n * N * K)
+    coded = torch.zeros(off + (n * N - 1) * pitch + F, dtype=torch.uint8, device="cuda")[off:]
+    codec.encode_batch(ctx, dev(data), n, dev(coeffs), coded, pitch)
+    rows = host(coded.as_strided((n * N, F), (pitch, 1)))
+    for c in sorted({0, n - 1, int(rng.integers(0, n))}):
+        ref = o.chunkset_encode(data[c * CS:(c + 1) * CS], coeffs[c * 160:(c + 1) * 160], nthreads=8)
+        assert np.array_equal(rows[c * N:(c + 1) * N], ref), (trial, n, pitch, off, c)
+    cand = np.full((n, N), 0xFF, np.uint8)
+    for c in range(n):
+        m = int(rng.integers(K, N + 1))
+        cand[c, :m] = rng.permutation(N)[:m]
+    plan = torch.empty(n * 128, dtype=torch.uint8, device="cuda")
+    verd = torch.empty(n * N, dtype=torch.int8, device="cuda")
+    status = torch.full((n,), -7, dtype=torch.int32, device="cuda")
+    out = torch.zeros(n * CS, dtype=torch.uint8, device="cuda")
+    codec.repair_batch(ctx, coded, n, dev(cand), plan, verd, out, status, pitch=pitch)
+    st, v, res = host(status), host(verd).reshape(n, N), host(out)
+    for c in range(n):
+        ov, rank = _oracle_verdicts(rows[c * N:(c + 1) * N], cand[c])
+        assert list(v[c]) == ov, (trial, c)
+        assert st[c] == (0 if rank == K else 5), (trial, c)
+        if rank == K:
+            assert np.array_equal(res[c * CS:(c + 1) * CS], data[c * CS:(c + 1) * CS]), (trial, n, pitch, off, c)
