@@ -118,6 +118,9 @@ __device__ __forceinline__ uint32_t table_coeffs(const uint8_t *M, uint32_t ldm)
 // { C[4q+jj][i] * x^(4h+k) : jj < 4 } (xtime chains) and the 16 rows' dwords q by one XOR each
 // (nib & (nib-1) is nib minus its lowest bit), writing replica 0; a second pass copies each
 // 16-byte row into replicas 1..15. ~30 VALU per thread instead of 5120 bit-serial multiplies.
+#ifndef DECDS_REPLICA_FLAT
+#define DECDS_REPLICA_FLAT 1
+#endif
 template <int NIN, int NOUT>
 __device__ __forceinline__ void build_tables(uint8_t *lds, uint32_t cw, uint32_t poly) {
     const uint32_t p = threadIdx.x;
@@ -141,17 +144,33 @@ __device__ __forceinline__ void build_tables(uint8_t *lds, uint32_t cw, uint32_t
         w[0] = 0;
 #pragma unroll
         for (int nib = 1; nib < 16; nib++) w[nib] = w[nib & (nib - 1)] ^ bw[__builtin_ctz(nib)];
-        uint8_t *base = lds + (i * 2 + h) * TABLE_BYTES + 4 * q;
+        // first copy in replica (2i + h) mod 16 (flat builds): the 32 lanes of a write group then
+        // hit 32 distinct banks; replica 0 for all would be 8-way conflicts
+        uint8_t *base = lds + (i * 2 + h) * TABLE_BYTES + (DECDS_REPLICA_FLAT ? ((i * 2 + h) & 15u) * 16 : 0) + 4 * q;
 #pragma unroll
         for (int nib = 0; nib < 16; nib++) *reinterpret_cast<uint32_t *>(base + nib * ROW_BYTES) = w[nib];
     }
     lds_barrier();
+#if DECDS_REPLICA_FLAT
+    // the other 15 replicas of every row, one 16-byte slot per lane: consecutive lanes write
+    // consecutive slots (conflict-free ds_write_b128; the first copy is read as a broadcast). Row-per-thread copies
+    // put the 8 lanes of a write group 256 B apart, i.e. on the same banks: 8-way conflicts, ~18 %
+    // of the encode kernel's LDS cycles (SQ_LDS_BANK_CONFLICT, r01m).
+#pragma unroll 4
+    for (uint32_t s = threadIdx.x; s < NIN * 32 * 16; s += blockDim.x) {
+        const uint32_t src = (s >> 8) & 15u;  // table 2i + h = s >> 8 was written in replica (2i + h) mod 16
+        if ((s & 15u) == src) continue;
+        uint8_t *row = lds + (s >> 4) * ROW_BYTES;
+        *reinterpret_cast<uint4 *>(row + (s & 15u) * 16) = *reinterpret_cast<const uint4 *>(row + src * 16);
+    }
+#else
     for (uint32_t r = threadIdx.x; r < NIN * 32; r += blockDim.x) {
         uint8_t *row = lds + r * ROW_BYTES;
         const uint4 val = *reinterpret_cast<const uint4 *>(row);
 #pragma unroll
         for (int c = 1; c < 16; c++) *reinterpret_cast<uint4 *>(row + c * 16) = val;
     }
+#endif
 }
 
 // byte product M[j][i] * x read back from replica 0 of the tables (tail / scalar path)

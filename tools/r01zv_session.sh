@@ -1,0 +1,23 @@
+#!/bin/bash
+# Conflict-free table replica copies (one 16-byte slot per lane) against row-per-thread copies:
+# parity, kernel A/B, and the LDS bank-conflict counters of both builds.
+set -o pipefail
+out=${1:-gpurun_out/r01zv}
+mkdir -p $out
+export TMPDIR=/tmp
+DECDS_LIB=build/ab/lib_flat.so timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_fullsize.py -m gpu -x -q --timeout 300 --timeout-method thread > $out/flat_tests.log 2>&1 || { echo "TESTS FAILED"; tail -30 $out/flat_tests.log; exit 1; }
+tail -1 $out/flat_tests.log
+L="build/ab/lib_old.so build/ab/lib_flat.so"
+for n in 1 4 16 103 256 1639; do
+  r=12; [ $n -ge 1024 ] && r=5
+  timeout -k 10 300 python tools/abbench.py --n $n --rounds $r $L > $out/ab$n.jsonl 2>&1 || { echo "AB FAILED"; tail $out/ab$n.jsonl; exit 1; }
+done
+for n in 1 4 16 103 256 1639; do grep -h tag $out/ab$n.jsonl; done | python -c "
+import sys,json
+for l in sys.stdin:
+    d=json.loads(l); print(d['tag'], d['n'], d['encode_ms'], d['encode_min_ms'], d['decode_ms'], d['decode_min_ms'])"
+bcmd="python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-sweep --no-commit"
+for v in old flat; do
+  DECDS_LIB=build/ab/lib_$v.so timeout -k 10 300 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_WAVE_CYCLES --output-format csv -d $out/pmc_$v -o bench -- $bcmd > $out/pmc_$v.log 2>&1 || { echo "PMC $v FAILED"; tail -5 $out/pmc_$v.log; exit 1; }
+done
+echo session-ok
