@@ -1060,7 +1060,11 @@ __global__ __launch_bounds__(64) void rlnc_plan_kernel(const uint8_t *__restrict
     bool ended = false;
     int32_t my_verdict = -1;  // lane a < 16 keeps candidate a's verdict
 #pragma unroll
+#ifdef DECDS_TIMING_PLAN_SETUP  // timing study only: the setup without the candidate loop (wrong output)
+    for (uint32_t a = 0; a < 0; a++) {
+#else
     for (uint32_t a = 0; a < N; a++) {
+#endif
         const uint32_t r = __builtin_amdgcn_readlane(my_cand, a);
         int32_t v;
         if (ended || r >= N) {
