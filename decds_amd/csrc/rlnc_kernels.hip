@@ -67,7 +67,7 @@ struct Tune {
 #define DECDS_ENC_BF_TUNE true, true, 0, 0
 #endif
 using EncTune = Tune<DECDS_ENC_TUNE, DECDS_ENC_SYNC>;
-using EncBfTune = Tune<DECDS_ENC_BF_TUNE>;  // DECDS_ENC_BF: per-chunkset branch-free segments
+using EncBfTune = Tune<DECDS_ENC_BF_TUNE, DECDS_ENC_SYNC>;  // DECDS_ENC_BF: per-chunkset branch-free segments
 using DecTune = Tune<DECDS_DEC_TUNE, DECDS_DEC_SYNC>;
 
 // ---- GF(2^8) ----------------------------------------------------------------------------------
@@ -577,6 +577,7 @@ __device__ __forceinline__ void stream_range(const uint8_t *lds, uint32_t laneof
     uint32_t t = ta;
 #pragma unroll 1
     do {
+        if constexpr (T::SYNC == 1) __builtin_amdgcn_s_barrier();  // the 4 waves start each tile together
         combine_block<T, NIN, NOUT>(lds, laneoff, x, obase, ooff, col(t), ibase, ioff, col(t + 1));
     } while (++t < tb);
 }
@@ -727,7 +728,8 @@ void rlnc_decode_kernel(const uint8_t *__restrict__ coded, size_t pitch, size_t 
         // Non-persistent: this workgroup's T tiles lie in one chunkset, streamed branch-free
         constexpr uint32_t T = (uint32_t)(-MAP);
         static_assert(TILES_PER_CS % T == 0, "a workgroup's tiles stay in one chunkset");
-        using DT = Tune<DecTune::ASM, true, DecTune::LAUX < 0 ? 0 : DecTune::LAUX, DecTune::SAUX < 0 ? 0 : DecTune::SAUX>;
+        using DT = Tune<DecTune::ASM, true, DecTune::LAUX < 0 ? 0 : DecTune::LAUX, DecTune::SAUX < 0 ? 0 : DecTune::SAUX,
+                        DecTune::SYNC>;
         const uint32_t t0 = np_block<DECDS_DEC_XCD_REMAP>() * T, cs = t0 / TILES_PER_CS, tile0 = t0 % TILES_PER_CS;
         if (cs >= n) return;
         const uint32_t *pw = reinterpret_cast<const uint32_t *>(plan + cs);
