@@ -462,6 +462,9 @@ __device__ __forceinline__ void tile_range(size_t n, uint32_t &t0, uint32_t &t1)
 #ifndef DECDS_XCD_CHUNK
 #define DECDS_XCD_CHUNK 0
 #endif
+#ifndef DECDS_XCD_MODE
+#define DECDS_XCD_MODE 0  // study variants: 1 odd XCDs sweep their eighth backwards, 2 from its middle
+#endif
 template <bool REMAP>
 __device__ __forceinline__ uint32_t np_block() {
     const uint32_t g = gridDim.x, b = blockIdx.x, x = b % NXCD, q = b / NXCD;
@@ -473,7 +476,9 @@ __device__ __forceinline__ uint32_t np_block() {
         return ((q / C) * NXCD + x) * C + q % C;
     } else {
         const uint32_t per = g / NXCD, rem = g % NXCD, cnt = per + (x < rem);
-        const uint32_t r = DECDS_XCD_SKEW ? (q + x * DECDS_XCD_SKEW) % cnt : q;
+        uint32_t r = DECDS_XCD_SKEW ? (q + x * DECDS_XCD_SKEW) % cnt : q;
+        if constexpr (DECDS_XCD_MODE == 1) r = (x & 1u) ? cnt - 1 - r : r;       // odd XCDs walk backwards
+        if constexpr (DECDS_XCD_MODE == 2) r = (x & 1u) ? (r + cnt / 2) % cnt : r;  // odd XCDs start mid-range
         return x * per + (x < rem ? x : rem) + r;
     }
 }
