@@ -395,11 +395,16 @@ __device__ __forceinline__ void combine_block(const uint8_t *lds, uint32_t laneo
 //   512 x 26 narrow ones. Needs grid % 8 == 0 and n close to a multiple of 8 (launcher checks).
 constexpr int MAP_BAND = -1;
 constexpr uint32_t NXCD = 8;
+// Encode: units of 4 tiles at every batch size. Units of 8 above 512 chunksets (the round-1 default
+// until the tile loop went branch-free and the table builds conflict-free) measured +4.5 / +6 / +7 %
+// at 600 / 1024 / 1639 chunksets on three boxes (tools/sessions/r01zz9, in-process A/B), and inside
+// bench.py's buffers 4.61 vs 4.94-5.25 TB/s at 1639 — only in the DRAM's fast mode, which units of
+// 8 reach less often, were they ahead (5.38 vs 5.22-5.25; r01zz10).
 #ifndef DECDS_ENC_MAP
-#define DECDS_ENC_MAP -8
+#define DECDS_ENC_MAP -4
 #endif
-// batches of at most DECDS_ENC_SMALL_N chunksets encode in units of 4 tiles (finer-grained at the
-// end of a short launch: -3 % at 103 chunksets on two boxes; at 1639 units of 8 were -6 % / +1.5 %)
+// batches of at most DECDS_ENC_SMALL_N chunksets encode with DECDS_ENC_MAP_SMALL (finer-grained at
+// the end of a short launch: units of 4 against 8 were -3 % at 103 chunksets on two boxes)
 #ifndef DECDS_ENC_MAP_SMALL
 #define DECDS_ENC_MAP_SMALL -4
 #endif
