@@ -428,6 +428,22 @@ def test_encode_large_n_last_chunkset_bounds(ctx):
     assert np.array_equal(coded[c * N * F:].cpu().numpy().reshape(N, F), ref)
 
 
+def test_encode_batch_above_512_bitexact(ctx):
+    # a batch past the old units-of-8 threshold (512 chunksets): XCD eighths of 65 chunksets, last
+    # eighth shorter; first, middle and last chunksets bit-exact against the oracle
+    n = 520
+    src = torch.empty(n * CS, dtype=torch.uint8, device="cuda")
+    codec.fill_random_device(ctx, 0xABCE, src)
+    coeffs = o.fill_random(0xC0EF0006, n * N * K)
+    coded = torch.empty(n * N * F, dtype=torch.uint8, device="cuda")
+    codec.encode_batch(ctx, src, n, dev(coeffs), coded)
+    torch.cuda.synchronize()
+    for c in (0, 64, 65, 259, n - 1):
+        ref = o.chunkset_encode(src[c * CS:(c + 1) * CS].cpu().numpy(), coeffs[c * 160:(c + 1) * 160], nthreads=8)
+        assert np.array_equal(coded[c * N * F:(c + 1) * N * F].cpu().numpy().reshape(N, F), ref), c
+    del src, coded
+
+
 @pytest.mark.parametrize("trial", range(6))
 def test_randomized_layouts_encode_repair(ctx, trial):
     # seeded random batch shapes through both kernels: batch sizes that pick every unit size
