@@ -41,6 +41,7 @@ def lib():
         for name, res, args in [
             ("orc_gf256_mul", u8, [u8, u8, u32]),
             ("orc_gf256_inv", u8, [u8, u32]),
+            ("orc_set_simd", c.c_int, [c.c_int]),
             ("orc_gf256_mul_table", None, [u32, vp]),
             ("orc_splitmix64_word", u64, [u64, u64]),
             ("orc_fill_random", None, [u64, u64, vp, sz]),
@@ -71,6 +72,11 @@ def lib():
 
 def _p(a):
     return ctypes.c_void_p(a.ctypes.data)
+
+
+def set_simd(on):
+    """AVX2 nibble-table row kernels (same bytes as the scalar restatement); returns the mode in effect"""
+    return lib().orc_set_simd(int(bool(on)))
 
 
 def gf_mul(a, b, poly=POLY):

@@ -4,6 +4,7 @@
  */
 #include "rlnc_oracle.h"
 
+#include <immintrin.h>
 #include <pthread.h>
 #include <stdlib.h>
 #include <string.h>
@@ -76,16 +77,59 @@ int orc_encoder_pad(const uint8_t *data, size_t len, size_t k, uint8_t marker, u
     return ORC_OK;
 }
 
-/* multiply-accumulate a row by a constant through that constant's 256-entry product row
- * (the scalar table-driven form of rlnc 0.4.0's inner loop) */
+/* Row kernels. Default: the scalar table-driven form of rlnc 0.4.0's inner loop [recalled] — one
+ * 256-entry product row per constant, one lookup per byte. orc_set_simd(1) switches to the AVX2
+ * nibble-table form (c*x = T_lo[x & 15] ^ T_hi[x >> 4], 32 bytes per vpshufb pair) where the CPU has
+ * it: same products, so the same bytes; it only makes the CPU baseline a stronger one (bench.py
+ * reports both). */
+static int g_simd = 0;
+
+int orc_set_simd(int on) {
+    g_simd = on && __builtin_cpu_supports("avx2");
+    return g_simd;
+}
+
+__attribute__((target("avx2"))) static void mul_row_avx2(uint8_t *dst, const uint8_t *src, size_t len,
+                                                         uint8_t c, uint32_t poly, int acc) {
+    uint8_t lo[16], hi[16];
+    for (unsigned x = 0; x < 16; x++) {
+        lo[x] = orc_gf256_mul(c, (uint8_t)x, poly);
+        hi[x] = orc_gf256_mul(c, (uint8_t)(x << 4), poly);
+    }
+    const __m256i tl = _mm256_broadcastsi128_si256(_mm_loadu_si128((const __m128i *)lo));
+    const __m256i th = _mm256_broadcastsi128_si256(_mm_loadu_si128((const __m128i *)hi));
+    const __m256i m = _mm256_set1_epi8(0x0F);
+    size_t j = 0;
+    for (; j + 32 <= len; j += 32) {
+        const __m256i v = _mm256_loadu_si256((const __m256i *)(src + j));
+        __m256i r = _mm256_xor_si256(_mm256_shuffle_epi8(tl, _mm256_and_si256(v, m)),
+                                     _mm256_shuffle_epi8(th, _mm256_and_si256(_mm256_srli_epi16(v, 4), m)));
+        if (acc) r = _mm256_xor_si256(r, _mm256_loadu_si256((const __m256i *)(dst + j)));
+        _mm256_storeu_si256((__m256i *)(dst + j), r);
+    }
+    for (; j < len; j++) {
+        const uint8_t y = (uint8_t)(lo[src[j] & 15] ^ hi[src[j] >> 4]);
+        dst[j] = acc ? (uint8_t)(dst[j] ^ y) : y;
+    }
+}
+
+/* multiply-accumulate a row by a constant */
 static void mul_acc_row(uint8_t *dst, const uint8_t *src, size_t len, uint8_t c, uint32_t poly) {
     if (c == 0) return;
+    if (g_simd) {
+        mul_row_avx2(dst, src, len, c, poly, 1);
+        return;
+    }
     uint8_t t[256];
     for (unsigned x = 0; x < 256; x++) t[x] = orc_gf256_mul(c, (uint8_t)x, poly);
     for (size_t j = 0; j < len; j++) dst[j] ^= t[src[j]];
 }
 
 static void mul_row(uint8_t *row, size_t len, uint8_t c, uint32_t poly) {
+    if (g_simd) {
+        mul_row_avx2(row, row, len, c, poly, 0);
+        return;
+    }
     uint8_t t[256];
     for (unsigned x = 0; x < 256; x++) t[x] = orc_gf256_mul(c, (uint8_t)x, poly);
     for (size_t j = 0; j < len; j++) row[j] = t[row[j]];

@@ -57,6 +57,8 @@ extern "C" {
 #define ORC_ERR_ARGS 7
 
 uint8_t orc_gf256_mul(uint8_t a, uint8_t b, uint32_t poly);
+/* 1: AVX2 nibble-table row kernels where the CPU has AVX2 (same bytes); returns the mode in effect */
+int orc_set_simd(int on);
 uint8_t orc_gf256_inv(uint8_t a, uint32_t poly);
 /* full 256x256 product table, row-major: out[a*256+b] = a*b */
 void orc_gf256_mul_table(uint32_t poly, uint8_t *out);

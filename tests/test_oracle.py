@@ -167,3 +167,27 @@ def test_blob_encode_repair_partial_last_chunkset():
     cand = np.array([np.random.default_rng(c).permutation(16) for c in range(n)], np.uint8)
     out, status = o.blob_repair(coded, cand, blob_len, nthreads=4)
     assert (status == 0).all() and np.array_equal(out, blob)
+
+
+def test_simd_row_kernels_match_scalar():
+    # the AVX2 nibble-table row kernels (bench.py's stronger CPU baseline) produce the scalar
+    # restatement's bytes: encode of two chunksets (one partial) and the repair of both
+    blob = o.fill_random(0x51D0, o.CS + 12345)
+    coeffs = o.fill_random(0x51D1, 2 * o.N * o.K)
+    cand = np.full((2, o.N), 0xFF, np.uint8)
+    rng = np.random.default_rng(5)
+    for c in range(2):
+        cand[c, :o.K + 2] = rng.permutation(o.N)[:o.K + 2]
+    o.set_simd(0)
+    ref = o.blob_encode(blob, coeffs, nthreads=4)
+    ref_out, ref_st = o.blob_repair(ref, cand, blob.size, nthreads=4)
+    try:
+        if not o.set_simd(1):
+            pytest.skip("no AVX2 on this host")
+        got = o.blob_encode(blob, coeffs, nthreads=4)
+        out, st = o.blob_repair(got, cand, blob.size, nthreads=4)
+    finally:
+        o.set_simd(0)
+    assert np.array_equal(got, ref)
+    assert np.array_equal(st, ref_st) and np.array_equal(out, ref_out)
+    assert np.array_equal(out[:blob.size], blob)
