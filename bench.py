@@ -110,9 +110,17 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit("--gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
+    # DECDS_BENCH_BACKEND=gloo is a rehearsal mode for the N > 1 path on a box with fewer GPUs than
+    # ranks (ranks share devices round-robin, timing reduced over gloo); the real runs use RCCL.
+    backend = os.environ.get("DECDS_BENCH_BACKEND", "nccl")
+    if backend == "gloo":
+        local = local % torch.cuda.device_count()
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "gloo":
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     blob_per_gpu, desc = CONFIGS[args.config]
     n_total = -(-(blob_per_gpu * world) // CS)
@@ -177,7 +185,7 @@ def main():
     elapsed = time.perf_counter() - t0
     if world > 1:
         dist.barrier()
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if backend == "gloo" else dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
