@@ -2,7 +2,8 @@
 of two coded buffers while stream B plans and decodes step s (events order encode(s) -> plan(s) and
 decode(s-1) -> encode(s+1), the coded buffer's last reader). Full-size launches only, so the gain
 can only come from one kernel's ramp-up / drain overlapping the other's. Against the sequential
-one-stream step. Prints one JSON line per mode.
+one-stream step, and against S independent sub-batch streams (split2/3/4: each stream its own
+encode -> plan -> decode chain, as S processes sharing the card). Prints one JSON line per mode.
 
 usage: python tools/overlapbench.py --n 103 --steps 40 --rounds 5
 """
@@ -68,6 +69,25 @@ def main():
             dec_done[s].record(sb)
         sa.wait_stream(sb)
 
+    streams = [torch.cuda.Stream() for _ in range(4)]
+
+    def run_split(S, k):
+        # S independent sub-batches, each on its own stream with its own encode -> plan -> decode
+        # chain (as S processes sharing the card would issue them); no cross-stream waits
+        b = [n * j // S for j in range(S + 1)]
+        for st in streams[:S]:
+            st.wait_stream(sa)
+        for _ in range(k):
+            for j in range(S):
+                c0, m, st = b[j], b[j + 1] - b[j], streams[j]
+                codec.encode_batch(ctx, src[c0 * CS:], m, coeffs[c0 * N * K:], coded[0][c0 * N * F:], stream=st)
+                codec.repair_plan_batch(ctx, coded[0][c0 * N * F:], m, cand[c0:], plan[c0 * 128:], verd[c0 * N:],
+                                        status[c0:], stream=st)
+                codec.decode_batch(ctx, coded[0][c0 * N * F:], m, plan[c0 * 128:], out[c0 * CS:], status[c0:],
+                                   stream=st)
+        for st in streams[:S]:
+            sa.wait_stream(st)
+
     def timed(fn):
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -81,10 +101,15 @@ def main():
         run_seq(10)
         run_pipe(10)
     torch.cuda.synchronize()
-    res = {"seq": [], "pipe": []}
+    fns = {"seq": run_seq, "pipe": run_pipe, "split2": lambda k: run_split(2, k),
+           "split3": lambda k: run_split(3, k), "split4": lambda k: run_split(4, k)}
+    for _ in range(10):
+        for f in fns.values():
+            f(4)
+    res = {m: [] for m in fns}
     for r in range(a.rounds):
-        for m in (("seq", "pipe") if r % 2 == 0 else ("pipe", "seq")):
-            res[m].append(timed(run_seq if m == "seq" else run_pipe))
+        for m in (list(fns) if r % 2 == 0 else list(fns)[::-1]):
+            res[m].append(timed(fns[m]))
     st = status.cpu().numpy()
     ok = all(torch.equal(out[c * CS:(c + 1) * CS], src[c * CS:(c + 1) * CS]) for c in np.nonzero(st == 0)[0].tolist())
     for m, v in res.items():
