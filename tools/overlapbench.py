@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--n", type=int, default=103)
     ap.add_argument("--steps", type=int, default=40)
     ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--graph", action="store_true", help="sequential steps against one step captured as a HIP graph")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -101,8 +102,27 @@ def main():
         run_seq(10)
         run_pipe(10)
     torch.cuda.synchronize()
+    # one step captured as a HIP graph (the three launches), replayed per step
+    graph = None
+    if a.graph:
+        gs = torch.cuda.Stream()
+        gs.wait_stream(sa)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph, stream=gs):
+            codec.encode_batch(ctx, src, n, coeffs, coded[0], stream=gs)
+            codec.repair_plan_batch(ctx, coded[0], n, cand, plan, verd, status, stream=gs)
+            codec.decode_batch(ctx, coded[0], n, plan, out, status, stream=gs)
+        torch.cuda.synchronize()
+
+    def run_graph(k):
+        with torch.cuda.stream(sa):
+            for _ in range(k):
+                graph.replay()
+
     fns = {"seq": run_seq, "pipe": run_pipe, "split2": lambda k: run_split(2, k),
            "split3": lambda k: run_split(3, k), "split4": lambda k: run_split(4, k)}
+    if a.graph:
+        fns = {"seq": run_seq, "graph": run_graph}
     for _ in range(10):
         for f in fns.values():
             f(4)
