@@ -39,6 +39,19 @@ int decds_ctx_bind(const decds_ctx *ctx) {
     return e == hipSuccess ? DECDS_OK : decds_hip_error(e, "hipSetDevice");
 }
 
+hipError_t decds_ctx_scratch(decds_ctx *ctx, size_t bytes, uint8_t **out) {
+    if (ctx->host_scratch_cap < bytes) {
+        if (ctx->host_scratch) (void)hipFree(ctx->host_scratch);
+        ctx->host_scratch = nullptr;
+        ctx->host_scratch_cap = 0;
+        hipError_t e = hipMalloc(reinterpret_cast<void **>(&ctx->host_scratch), bytes);
+        if (e) return e;
+        ctx->host_scratch_cap = bytes;
+    }
+    *out = ctx->host_scratch;
+    return hipSuccess;
+}
+
 extern "C" {
 
 const char *decds_last_error(void) { return g_last_error.c_str(); }
@@ -103,6 +116,10 @@ int decds_ctx_create(int device, decds_ctx **out) {
 }
 
 int decds_ctx_destroy(decds_ctx *ctx) {
+    if (ctx && ctx->host_scratch) {
+        (void)hipSetDevice(ctx->device);
+        (void)hipFree(ctx->host_scratch);
+    }
     delete ctx;
     return DECDS_OK;
 }

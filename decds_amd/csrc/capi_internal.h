@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <mutex>
+
 #include "rlnc_kernels.h"
 
 struct decds_ctx {
@@ -11,7 +13,15 @@ struct decds_ctx {
     uint8_t marker;    // boundary marker appended by rlnc Encoder::new (0x81 [recalled])
     uint32_t gen;      // smallest generator of GF(2^8)* under poly (the plan kernel's log/exp tables)
     decds::LaunchGeom geom;
+    // device buffers of the host blob paths (decds_blob_*_host), kept across calls (grow-only) so a
+    // call does not pay hipMalloc / hipFree of its slot buffers; host_mu serialises those calls
+    std::mutex host_mu;
+    uint8_t *host_scratch = nullptr;
+    size_t host_scratch_cap = 0;
 };
+
+// at least `bytes` of the context's host-path scratch (caller holds ctx->host_mu)
+hipError_t decds_ctx_scratch(decds_ctx *ctx, size_t bytes, uint8_t **out);
 
 int decds_set_error(int code, const char *fmt, ...);
 int decds_hip_error(hipError_t e, const char *what);

@@ -259,6 +259,42 @@ struct HostReg {
 };
 }  // namespace
 
+// Copy / compute pipeline of the host blob paths: one stream per engine (H2D, kernels, D2H) and
+// SLOTS buffer sets, ordered by events, so the link carries H2D and D2H at the same time (PCIe is
+// full duplex: 53 + 57 GB/s alone, 98 GB/s together, tools/pciebench.py). Round 1's two streams,
+// each H2D -> kernel -> D2H in order, kept one direction busy at a time (60 GB/s in sum).
+constexpr int SLOTS = 3;
+inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+struct Pipe {
+    hipStream_t h2d = nullptr, comp = nullptr, d2h = nullptr;
+    hipEvent_t in_done[SLOTS] = {}, k_done[SLOTS] = {}, out_done[SLOTS] = {};
+    hipError_t init() {
+        hipError_t e;
+        for (hipStream_t *st : {&h2d, &comp, &d2h})
+            if ((e = hipStreamCreateWithFlags(st, hipStreamNonBlocking))) return e;
+        for (int i = 0; i < SLOTS; i++)
+            for (hipEvent_t *ev : {&in_done[i], &k_done[i], &out_done[i]}) {
+                if ((e = hipEventCreateWithFlags(ev, hipEventDisableTiming))) return e;
+                if ((e = hipEventRecord(*ev, comp))) return e;  // every slot starts free
+            }
+        return hipSuccess;
+    }
+    hipError_t drain() {
+        hipError_t e = hipSuccess, f;
+        for (hipStream_t st : {h2d, comp, d2h})
+            if (st && (f = hipStreamSynchronize(st)) && !e) e = f;
+        return e;
+    }
+    ~Pipe() {
+        (void)drain();
+        for (int i = 0; i < SLOTS; i++)
+            for (hipEvent_t ev : {in_done[i], k_done[i], out_done[i]})
+                if (ev) (void)hipEventDestroy(ev);
+        for (hipStream_t st : {h2d, comp, d2h})
+            if (st) (void)hipStreamDestroy(st);
+    }
+};
+
 int decds_blob_encode_host(decds_ctx *ctx, const uint8_t *blob, size_t blob_len, const uint8_t *coeffs_host,
                            uint8_t *coded_host, size_t batch) {
     if (blob_len == 0) return decds_set_error(DECDS_ERR_EMPTY_DATA_FOR_BLOB, "empty data for blob");  // blob.rs:245-247
@@ -269,39 +305,43 @@ int decds_blob_encode_host(decds_ctx *ctx, const uint8_t *blob, size_t blob_len,
     if (batch == 0) batch = 64;
     batch = std::min(batch, n);
     HostReg rin(blob, blob_len), rout(coded_host, n * N * F), rcv(coeffs_host, n * N * K);
-    hipStream_t st[2];
-    DevBuf din[2], dout[2], dcv[2];
+    std::lock_guard<std::mutex> lock(ctx->host_mu);
+    uint8_t *din[SLOTS], *dout[SLOTS], *dcv[SLOTS];
+    const size_t sz_in = align256(batch * CS), sz_out = align256(batch * N * F), sz_cv = align256(batch * N * K);
+    uint8_t *base;
     hipError_t e;
-    for (int i = 0; i < 2; i++) {
-        if ((e = hipStreamCreateWithFlags(&st[i], hipStreamNonBlocking))) return decds_hip_error(e, "hipStreamCreate");
-        if ((e = din[i].alloc(batch * CS)) || (e = dout[i].alloc(batch * N * F)) || (e = dcv[i].alloc(batch * N * K)))
-            return decds_hip_error(e, "hipMalloc");
-    }
+    if ((e = decds_ctx_scratch(ctx, SLOTS * (sz_in + sz_out + sz_cv), &base))) return decds_hip_error(e, "hipMalloc");
+    for (int i = 0; i < SLOTS; i++, base += sz_in + sz_out + sz_cv) din[i] = base, dout[i] = base + sz_in, dcv[i] = base + sz_in + sz_out;
+    Pipe pp;
+    if ((e = pp.init())) return decds_hip_error(e, "stream/event setup");
     int rc = DECDS_OK;
     for (size_t b0 = 0, it = 0; b0 < n && rc == DECDS_OK; b0 += batch, it++) {
-        const int k = (int)(it & 1);
+        const int k = (int)(it % SLOTS);
         const size_t nb = std::min(batch, n - b0);
         const size_t off = b0 * CS, have = std::min(blob_len - off, nb * CS);
-        if ((e = hipMemcpyAsync(din[k].p, blob + off, have, hipMemcpyHostToDevice, st[k]))) { rc = decds_hip_error(e, "H2D"); break; }
-        if (have < nb * CS && (e = hipMemsetAsync(din[k].p + have, 0, nb * CS - have, st[k]))) {  // blob.rs:254 zero pad
-            rc = decds_hip_error(e, "memset");
-            break;
-        }
-        if ((e = hipMemcpyAsync(dcv[k].p, coeffs_host + b0 * N * K, nb * N * K, hipMemcpyHostToDevice, st[k]))) {
+        // inputs of slot k: free once the slot's previous kernel has read them
+        if ((e = hipStreamWaitEvent(pp.h2d, pp.k_done[k], 0)) ||
+            (e = hipMemcpyAsync(din[k], blob + off, have, hipMemcpyHostToDevice, pp.h2d)) ||
+            (have < nb * CS && (e = hipMemsetAsync(din[k] + have, 0, nb * CS - have, pp.h2d))) ||  // blob.rs:254 zero pad
+            (e = hipMemcpyAsync(dcv[k], coeffs_host + b0 * N * K, nb * N * K, hipMemcpyHostToDevice, pp.h2d)) ||
+            (e = hipEventRecord(pp.in_done[k], pp.h2d))) {
             rc = decds_hip_error(e, "H2D");
             break;
         }
-        if ((rc = decds_encode_batch(ctx, din[k].p, nb, dcv[k].p, dout[k].p, F, st[k]))) break;
-        if ((e = hipMemcpyAsync(coded_host + b0 * N * F, dout[k].p, nb * N * F, hipMemcpyDeviceToHost, st[k]))) {
+        // coded rows of slot k: free once the slot's previous D2H has read them
+        if ((e = hipStreamWaitEvent(pp.comp, pp.in_done[k], 0)) || (e = hipStreamWaitEvent(pp.comp, pp.out_done[k], 0))) {
+            rc = decds_hip_error(e, "hipStreamWaitEvent");
+            break;
+        }
+        if ((rc = decds_encode_batch(ctx, din[k], nb, dcv[k], dout[k], F, pp.comp))) break;
+        if ((e = hipEventRecord(pp.k_done[k], pp.comp)) || (e = hipStreamWaitEvent(pp.d2h, pp.k_done[k], 0)) ||
+            (e = hipMemcpyAsync(coded_host + b0 * N * F, dout[k], nb * N * F, hipMemcpyDeviceToHost, pp.d2h)) ||
+            (e = hipEventRecord(pp.out_done[k], pp.d2h))) {
             rc = decds_hip_error(e, "D2H");
             break;
         }
     }
-    for (int i = 0; i < 2; i++) {
-        e = hipStreamSynchronize(st[i]);
-        if (e && rc == DECDS_OK) rc = decds_hip_error(e, "hipStreamSynchronize");
-        (void)hipStreamDestroy(st[i]);
-    }
+    if ((e = pp.drain()) && rc == DECDS_OK) rc = decds_hip_error(e, "hipStreamSynchronize");
     return rc;
 }
 
@@ -328,25 +368,31 @@ int decds_blob_repair_host(decds_ctx *ctx, const uint8_t *coded_host, size_t n, 
         }
         status_host[c] = rank == K ? DECDS_OK : DECDS_ERR_CHUNKSET_NOT_YET_READY;
     }
-    hipStream_t st[2];
-    DevBuf dcoded[2], dcand[2], dplan[2], dverd[2], dstat[2], ddst[2];
-    std::vector<std::vector<uint8_t>> cand_h(2, std::vector<uint8_t>(batch * N));
-    hipError_t e;
-    for (int i = 0; i < 2; i++) {
-        if ((e = hipStreamCreateWithFlags(&st[i], hipStreamNonBlocking))) return decds_hip_error(e, "hipStreamCreate");
-        if ((e = dcoded[i].alloc(batch * N * F)) || (e = dplan[i].alloc(batch * DECDS_REPAIR_PLAN_BYTES)) ||
-            (e = dverd[i].alloc(batch * N)) || (e = dstat[i].alloc(batch * sizeof(int32_t))) ||
-            (e = ddst[i].alloc(batch * CS)) || (e = dcand[i].alloc(batch * N)))
-            return decds_hip_error(e, "hipMalloc");
-    }
+    std::vector<std::vector<uint8_t>> cand_h(SLOTS, std::vector<uint8_t>(batch * N));
+    std::vector<std::vector<int32_t>> stat_h(SLOTS, std::vector<int32_t>(batch));
     HostReg rout(out, blob_len), rin(coded_host, n * N * F);
+    std::lock_guard<std::mutex> lock(ctx->host_mu);
+    uint8_t *dcoded[SLOTS], *dcand[SLOTS], *dplan[SLOTS], *dverd[SLOTS], *dstat[SLOTS], *ddst[SLOTS];
+    const size_t sz[6] = {align256(batch * N * F), align256(batch * N), align256(batch * DECDS_REPAIR_PLAN_BYTES),
+                          align256(batch * N), align256(batch * sizeof(int32_t)), align256(batch * CS)};
+    const size_t per = sz[0] + sz[1] + sz[2] + sz[3] + sz[4] + sz[5];
+    uint8_t *base;
+    hipError_t e;
+    if ((e = decds_ctx_scratch(ctx, SLOTS * per, &base))) return decds_hip_error(e, "hipMalloc");
+    for (int i = 0; i < SLOTS; i++) {
+        uint8_t **dst[6] = {&dcoded[i], &dcand[i], &dplan[i], &dverd[i], &dstat[i], &ddst[i]};
+        for (int j = 0; j < 6; j++) *dst[j] = base, base += sz[j];
+    }
+    Pipe pp;
+    if ((e = pp.init())) return decds_hip_error(e, "stream/event setup");
     int rc = DECDS_OK;
-    std::vector<std::vector<int32_t>> stat_h(2, std::vector<int32_t>(batch));
-    size_t pending_b0[2] = {(size_t)-1, (size_t)-1}, pending_nb[2] = {0, 0};
+    size_t pending_b0[SLOTS], pending_nb[SLOTS] = {};
+    for (int i = 0; i < SLOTS; i++) pending_b0[i] = (size_t)-1;
+    // host side of slot k once its D2H is done: device statuses, zeroed output of unrepaired chunksets
     auto finish = [&](int k) -> int {
         if (pending_b0[k] == (size_t)-1) return DECDS_OK;
-        hipError_t ee = hipStreamSynchronize(st[k]);
-        if (ee) return decds_hip_error(ee, "hipStreamSynchronize");
+        hipError_t ee = hipEventSynchronize(pp.out_done[k]);
+        if (ee) return decds_hip_error(ee, "hipEventSynchronize");
         for (size_t c = 0; c < pending_nb[k]; c++) {
             const size_t cs = pending_b0[k] + c;
             int32_t &hs = status_host[cs];
@@ -360,48 +406,48 @@ int decds_blob_repair_host(decds_ctx *ctx, const uint8_t *coded_host, size_t n, 
         return DECDS_OK;
     };
     for (size_t b0 = 0, it = 0; b0 < n && rc == DECDS_OK; b0 += batch, it++) {
-        const int k = (int)(it & 1);
-        if ((rc = finish(k))) break;
+        const int k = (int)(it % SLOTS);
+        if ((rc = finish(k))) break;  // slot k's previous batch fully done: all its buffers are free
         const size_t nb = std::min(batch, n - b0);
-        for (size_t c = 0; c < nb; c++) {
+        for (size_t c = 0; c < nb && rc == DECDS_OK; c++) {
             const bool ready = status_host[b0 + c] == DECDS_OK;
             for (uint32_t a = 0; a < N; a++) cand_h[k][c * N + a] = ready && a < K ? (uint8_t)a : (uint8_t)DECDS_NO_CANDIDATE;
             if (!ready) continue;
             for (uint32_t r = 0; r < K; r++) {
                 const uint8_t row = sel[(b0 + c) * K + r];
-                if ((e = hipMemcpyAsync(dcoded[k].p + (c * N + r) * F, coded_host + ((b0 + c) * N + row) * F, F,
-                                        hipMemcpyHostToDevice, st[k]))) {
+                if ((e = hipMemcpyAsync(dcoded[k] + (c * N + r) * F, coded_host + ((b0 + c) * N + row) * F, F,
+                                        hipMemcpyHostToDevice, pp.h2d))) {
                     rc = decds_hip_error(e, "H2D");
                     break;
                 }
             }
         }
         if (rc) break;
-        if ((e = hipMemcpyAsync(dcand[k].p, cand_h[k].data(), nb * N, hipMemcpyHostToDevice, st[k]))) {
+        if ((e = hipMemcpyAsync(dcand[k], cand_h[k].data(), nb * N, hipMemcpyHostToDevice, pp.h2d)) ||
+            (e = hipEventRecord(pp.in_done[k], pp.h2d)) || (e = hipStreamWaitEvent(pp.comp, pp.in_done[k], 0))) {
             rc = decds_hip_error(e, "H2D");
             break;
         }
-        if ((rc = decds_repair_batch(ctx, dcoded[k].p, F, nb, dcand[k].p, dplan[k].p, reinterpret_cast<int8_t *>(dverd[k].p),
-                                     ddst[k].p, reinterpret_cast<int32_t *>(dstat[k].p), st[k])))
+        if ((rc = decds_repair_batch(ctx, dcoded[k], F, nb, dcand[k], dplan[k], reinterpret_cast<int8_t *>(dverd[k]),
+                                     ddst[k], reinterpret_cast<int32_t *>(dstat[k]), pp.comp)))
             break;
-        if ((e = hipMemcpyAsync(stat_h[k].data(), dstat[k].p, nb * sizeof(int32_t), hipMemcpyDeviceToHost, st[k]))) {
-            rc = decds_hip_error(e, "D2H");
-            break;
-        }
         // blob.rs:464: truncate the last chunkset to its real size
         const size_t off = b0 * CS, keep = std::min(blob_len - off, nb * CS);
-        if ((e = hipMemcpyAsync(out + off, ddst[k].p, keep, hipMemcpyDeviceToHost, st[k]))) {
+        if ((e = hipEventRecord(pp.k_done[k], pp.comp)) || (e = hipStreamWaitEvent(pp.d2h, pp.k_done[k], 0)) ||
+            (e = hipMemcpyAsync(stat_h[k].data(), dstat[k], nb * sizeof(int32_t), hipMemcpyDeviceToHost, pp.d2h)) ||
+            (e = hipMemcpyAsync(out + off, ddst[k], keep, hipMemcpyDeviceToHost, pp.d2h)) ||
+            (e = hipEventRecord(pp.out_done[k], pp.d2h))) {
             rc = decds_hip_error(e, "D2H");
             break;
         }
         pending_b0[k] = b0;
         pending_nb[k] = nb;
     }
-    for (int i = 0; i < 2; i++) {
-        int r2 = finish(i);
+    for (size_t j = 0; j < SLOTS; j++) {  // oldest pending slot first
+        int r2 = finish((int)(j % SLOTS));
         if (r2 && rc == DECDS_OK) rc = r2;
-        (void)hipStreamDestroy(st[i]);
     }
+    if ((e = pp.drain()) && rc == DECDS_OK) rc = decds_hip_error(e, "hipStreamSynchronize");
     return rc;
 }
 
