@@ -368,8 +368,25 @@ int decds_blob_repair_host(decds_ctx *ctx, const uint8_t *coded_host, size_t n, 
         }
         status_host[c] = rank == K ? DECDS_OK : DECDS_ERR_CHUNKSET_NOT_YET_READY;
     }
-    std::vector<std::vector<uint8_t>> cand_h(SLOTS, std::vector<uint8_t>(batch * N));
-    std::vector<std::vector<int32_t>> stat_h(SLOTS, std::vector<int32_t>(batch));
+    // per-slot candidate lists and device statuses in page-locked memory: a pageable source or
+    // target would make hipMemcpyAsync a staged copy that blocks this thread until its stream
+    // reaches it, stalling the issue of the next slot
+    struct Pinned {
+        void *p = nullptr;
+        ~Pinned() {
+            if (p) (void)hipHostFree(p);
+        }
+    } pin;
+    {
+        hipError_t pe = hipHostMalloc(&pin.p, SLOTS * batch * (N + sizeof(int32_t)), hipHostMallocDefault);
+        if (pe) return decds_hip_error(pe, "hipHostMalloc");
+    }
+    uint8_t *cand_h[SLOTS];
+    int32_t *stat_h[SLOTS];
+    for (int i = 0; i < SLOTS; i++) {
+        stat_h[i] = reinterpret_cast<int32_t *>(pin.p) + i * batch;
+        cand_h[i] = reinterpret_cast<uint8_t *>(pin.p) + SLOTS * batch * sizeof(int32_t) + i * batch * N;
+    }
     HostReg rout(out, blob_len), rin(coded_host, n * N * F);
     std::lock_guard<std::mutex> lock(ctx->host_mu);
     uint8_t *dcoded[SLOTS], *dcand[SLOTS], *dplan[SLOTS], *dverd[SLOTS], *dstat[SLOTS], *ddst[SLOTS];
@@ -409,21 +426,31 @@ int decds_blob_repair_host(decds_ctx *ctx, const uint8_t *coded_host, size_t n, 
         const int k = (int)(it % SLOTS);
         if ((rc = finish(k))) break;  // slot k's previous batch fully done: all its buffers are free
         const size_t nb = std::min(batch, n - b0);
-        for (size_t c = 0; c < nb && rc == DECDS_OK; c++) {
+        // the accepted rows keep their own row slots on the device (slot layout = host layout less
+        // b0 chunksets), so runs of consecutive accepted rows — across chunkset boundaries too —
+        // cross the link as one copy each instead of one copy per row
+        std::vector<uint8_t> take(nb * N, 0);
+        for (size_t c = 0; c < nb; c++) {
             const bool ready = status_host[b0 + c] == DECDS_OK;
-            for (uint32_t a = 0; a < N; a++) cand_h[k][c * N + a] = ready && a < K ? (uint8_t)a : (uint8_t)DECDS_NO_CANDIDATE;
-            if (!ready) continue;
-            for (uint32_t r = 0; r < K; r++) {
-                const uint8_t row = sel[(b0 + c) * K + r];
-                if ((e = hipMemcpyAsync(dcoded[k] + (c * N + r) * F, coded_host + ((b0 + c) * N + row) * F, F,
-                                        hipMemcpyHostToDevice, pp.h2d))) {
-                    rc = decds_hip_error(e, "H2D");
-                    break;
-                }
+            for (uint32_t a = 0; a < N; a++)
+                cand_h[k][c * N + a] = ready && a < K ? sel[(b0 + c) * K + a] : (uint8_t)DECDS_NO_CANDIDATE;
+            if (ready)
+                for (uint32_t a = 0; a < K; a++) take[c * N + sel[(b0 + c) * K + a]] = 1;
+        }
+        for (size_t r0 = 0; r0 < nb * N && rc == DECDS_OK;) {
+            if (!take[r0]) {
+                r0++;
+                continue;
             }
+            size_t r1 = r0 + 1;
+            while (r1 < nb * N && take[r1]) r1++;
+            if ((e = hipMemcpyAsync(dcoded[k] + r0 * F, coded_host + (b0 * N + r0) * F, (r1 - r0) * F,
+                                    hipMemcpyHostToDevice, pp.h2d)))
+                rc = decds_hip_error(e, "H2D");
+            r0 = r1;
         }
         if (rc) break;
-        if ((e = hipMemcpyAsync(dcand[k], cand_h[k].data(), nb * N, hipMemcpyHostToDevice, pp.h2d)) ||
+        if ((e = hipMemcpyAsync(dcand[k], cand_h[k], nb * N, hipMemcpyHostToDevice, pp.h2d)) ||
             (e = hipEventRecord(pp.in_done[k], pp.h2d)) || (e = hipStreamWaitEvent(pp.comp, pp.in_done[k], 0))) {
             rc = decds_hip_error(e, "H2D");
             break;
@@ -434,7 +461,7 @@ int decds_blob_repair_host(decds_ctx *ctx, const uint8_t *coded_host, size_t n, 
         // blob.rs:464: truncate the last chunkset to its real size
         const size_t off = b0 * CS, keep = std::min(blob_len - off, nb * CS);
         if ((e = hipEventRecord(pp.k_done[k], pp.comp)) || (e = hipStreamWaitEvent(pp.d2h, pp.k_done[k], 0)) ||
-            (e = hipMemcpyAsync(stat_h[k].data(), dstat[k], nb * sizeof(int32_t), hipMemcpyDeviceToHost, pp.d2h)) ||
+            (e = hipMemcpyAsync(stat_h[k], dstat[k], nb * sizeof(int32_t), hipMemcpyDeviceToHost, pp.d2h)) ||
             (e = hipMemcpyAsync(out + off, ddst[k], keep, hipMemcpyDeviceToHost, pp.d2h)) ||
             (e = hipEventRecord(pp.out_done[k], pp.d2h))) {
             rc = decds_hip_error(e, "D2H");
