@@ -172,8 +172,11 @@ void decds_repairing_chunkset_free(decds_repairing_chunkset *rcs);
 
 /* ---- blob-level batching (decds-lib/src/blob.rs), host buffers, pinned-staged -------------- */
 /* Blob::new's chunkset loop (blob.rs:252-264): zero-pads blob to n = ceil(len/CS) chunksets and
- * encodes them in device batches of `batch` chunksets with H2D / kernel / D2H overlapped on two
- * streams. coded_host: n*16 rows of 1,048,587 bytes. coeffs_host: n x 16 x 10. */
+ * encodes them in device batches of `batch` chunksets (0 = 64; 8-32 measured best) with H2D,
+ * kernels and D2H on one stream each over three slots, so PCIe carries both directions at once;
+ * the slot buffers stay in ctx across calls (calls on one ctx are serialised). Page-lock the
+ * caller buffers once (decds_host_register) for the full rate. coded_host: n*16 rows of
+ * 1,048,587 bytes. coeffs_host: n x 16 x 10. */
 int decds_blob_encode_host(decds_ctx *ctx, const uint8_t *blob, size_t blob_len,
                            const uint8_t *coeffs_host, uint8_t *coded_host, size_t batch);
 /* RepairingBlob add_chunk/get_repaired_chunkset over all chunksets (blob.rs:373-394, 451-473):
