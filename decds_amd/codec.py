@@ -104,7 +104,7 @@ def fill_random_host(seed, nbytes, byte_offset=0):
     return out
 
 
-def blob_encode_host(ctx, blob, coeffs, batch=64, out=None):
+def blob_encode_host(ctx, blob, coeffs, batch=16, out=None):
     """Blob::new's chunkset loop (blob.rs:252-264) on host buffers. Returns (n*16, F) uint8."""
     blob = np.ascontiguousarray(np.frombuffer(blob, dtype=np.uint8) if isinstance(blob, (bytes, bytearray)) else blob)
     n = -(-blob.size // CHUNKSET_BYTES)
@@ -119,7 +119,7 @@ def blob_encode_host(ctx, blob, coeffs, batch=64, out=None):
     return out
 
 
-def blob_repair_host(ctx, coded, cand, blob_len, batch=64, out=None):
+def blob_repair_host(ctx, coded, cand, blob_len, batch=16, out=None):
     """RepairingBlob add_chunk/get_repaired_chunkset (blob.rs:373-473). Returns (blob, status)."""
     coded = np.ascontiguousarray(coded, dtype=np.uint8)
     n = coded.shape[0] // N

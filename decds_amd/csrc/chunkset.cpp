@@ -302,7 +302,7 @@ int decds_blob_encode_host(decds_ctx *ctx, const uint8_t *blob, size_t blob_len,
     int s = decds_ctx_bind(ctx);
     if (s) return s;
     const size_t n = (blob_len + CS - 1) / CS;  // blob.rs:252
-    if (batch == 0) batch = 64;
+    if (batch == 0) batch = 16;  // 8-32 measured best
     batch = std::min(batch, n);
     HostReg rin(blob, blob_len), rout(coded_host, n * N * F), rcv(coeffs_host, n * N * K);
     std::lock_guard<std::mutex> lock(ctx->host_mu);
@@ -353,7 +353,7 @@ int decds_blob_repair_host(decds_ctx *ctx, const uint8_t *coded_host, size_t n, 
         return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "blob length %zu inconsistent with %zu chunksets", blob_len, n);
     int s = decds_ctx_bind(ctx);
     if (s) return s;
-    if (batch == 0) batch = 64;
+    if (batch == 0) batch = 16;  // 8-32 measured best
     batch = std::min(batch, n);
     // RepairingBlob::add_chunk over the arrival order (blob.rs:373-394): the rank test runs on the
     // 10-byte coding vectors on the host, so only the 10 accepted rows of each chunkset cross PCIe

@@ -172,7 +172,7 @@ void decds_repairing_chunkset_free(decds_repairing_chunkset *rcs);
 
 /* ---- blob-level batching (decds-lib/src/blob.rs), host buffers, pinned-staged -------------- */
 /* Blob::new's chunkset loop (blob.rs:252-264): zero-pads blob to n = ceil(len/CS) chunksets and
- * encodes them in device batches of `batch` chunksets (0 = 64; 8-32 measured best) with H2D,
+ * encodes them in device batches of `batch` chunksets (0 = 16; 8-32 measured best) with H2D,
  * kernels and D2H on one stream each over three slots, so PCIe carries both directions at once;
  * the slot buffers stay in ctx across calls (calls on one ctx are serialised). Page-lock the
  * caller buffers once (decds_host_register) for the full rate. coded_host: n*16 rows of
