@@ -6,7 +6,10 @@ C-ABI in include/decds_rlnc.h. This package is the Python-side binding used by t
 """
 from ._capi import (CHUNKSET_BYTES, CODED_PIECE_BYTES, K, N, NO_CANDIDATE, PIECE_BYTES, REPAIR_PLAN_BYTES,
                     STATUS, STATUS_NAMES, DecdsError)
+from .blob import Blob, HostBuffer, RepairingBlob
 from .chunkset import Chunk, ChunkSet, Context, RepairingChunkSet
+from .wire import BlobHeader
 
-__all__ = ["Context", "Chunk", "ChunkSet", "RepairingChunkSet", "DecdsError", "K", "N", "CHUNKSET_BYTES",
-           "PIECE_BYTES", "CODED_PIECE_BYTES", "REPAIR_PLAN_BYTES", "NO_CANDIDATE", "STATUS", "STATUS_NAMES"]
+__all__ = ["Context", "Chunk", "ChunkSet", "RepairingChunkSet", "Blob", "RepairingBlob", "BlobHeader", "HostBuffer",
+           "DecdsError", "K", "N", "CHUNKSET_BYTES", "PIECE_BYTES", "CODED_PIECE_BYTES", "REPAIR_PLAN_BYTES",
+           "NO_CANDIDATE", "STATUS", "STATUS_NAMES"]

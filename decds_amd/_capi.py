@@ -119,6 +119,26 @@ def _declare(L):
         "decds_merkle_tree": (c.c_int, [VP, SZ, VP, VP]),
         "decds_merkle_verify": (c.c_int, [SZ, VP, VP, SZ, VP]),
         "decds_host_unregister": (c.c_int, [VP]),
+        "decds_host_alloc": (c.c_int, [SZ, c.POINTER(c.c_void_p)]),
+        "decds_host_free": (c.c_int, [VP]),
+        "decds_host_is_registered": (c.c_int, [VP, SZ]),
+        "decds_device_status": (c.c_int, [P]),
+        "decds_blob_encode_host_multi": (c.c_int, [VP, SZ, VP, SZ, VP, VP, SZ]),
+        "decds_blob_repair_host_multi": (c.c_int, [VP, SZ, VP, SZ, VP, SZ, VP, VP, SZ]),
+        "decds_blob_new": (c.c_int, [VP, SZ, VP, SZ, VP, c.POINTER(c.c_void_p)]),
+        "decds_blob_get_header": (c.c_int, [P, c.POINTER(c.c_uint64), c.POINTER(c.c_uint64), VP, VP,
+                                            c.POINTER(c.c_void_p)]),
+        "decds_blob_proof_len": (SZ, [P]),
+        "decds_blob_get_chunk": (c.c_int, [P, SZ, SZ, c.POINTER(c.c_void_p), VP, SZ]),
+        "decds_blob_get_share": (c.c_int, [P, SZ, VP, SZ, VP, SZ]),
+        "decds_blob_free": (None, [P]),
+        "decds_repairing_blob_new": (c.c_int, [P, c.c_uint64, c.c_uint64, VP, VP, c.POINTER(c.c_void_p)]),
+        "decds_repairing_blob_add_chunk": (c.c_int, [P, c.c_uint64, c.c_uint64, VP, SZ, VP, SZ]),
+        "decds_repairing_blob_add_chunks": (c.c_int, [P, SZ, VP, VP, VP, SZ, VP]),
+        "decds_repairing_blob_is_chunkset_ready_to_repair": (c.c_int, [P, SZ, c.POINTER(c.c_int)]),
+        "decds_repairing_blob_is_chunkset_already_repaired": (c.c_int, [P, SZ, c.POINTER(c.c_int)]),
+        "decds_repairing_blob_get_repaired_chunkset": (c.c_int, [P, SZ, VP, SZ, c.POINTER(SZ)]),
+        "decds_repairing_blob_free": (None, [P]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -141,6 +161,12 @@ EXPORTED = [
     "decds_chunkset_append_blob_inclusion_proof", "decds_repairing_chunkset_add_chunk",
     "decds_blake3_parallel", "decds_pcc_encoded_len", "decds_pcc_to_bytes", "decds_pcc_from_bytes",
     "decds_blob_header_encoded_len", "decds_blob_header_to_bytes", "decds_blob_header_from_bytes",
+    "decds_host_alloc", "decds_host_free", "decds_host_is_registered", "decds_device_status",
+    "decds_blob_encode_host_multi", "decds_blob_repair_host_multi", "decds_blob_new", "decds_blob_get_header",
+    "decds_blob_proof_len", "decds_blob_get_chunk", "decds_blob_get_share", "decds_blob_free",
+    "decds_repairing_blob_new", "decds_repairing_blob_add_chunk", "decds_repairing_blob_add_chunks",
+    "decds_repairing_blob_is_chunkset_ready_to_repair", "decds_repairing_blob_is_chunkset_already_repaired",
+    "decds_repairing_blob_get_repaired_chunkset", "decds_repairing_blob_free",
 ]
 
 

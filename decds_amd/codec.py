@@ -133,6 +133,40 @@ def blob_repair_host(ctx, coded, cand, blob_len, batch=16, out=None):
     return out, status
 
 
+def _ctxs(ctxs):
+    arr = (ctypes.c_void_p * len(ctxs))(*[c.handle.value for c in ctxs])
+    return arr, len(ctxs)
+
+
+def blob_encode_host_multi(ctxs, blob, coeffs, batch=16, out=None):
+    """blob_encode_host sharded over several contexts (devices) by contiguous chunkset range."""
+    blob = np.ascontiguousarray(np.frombuffer(blob, dtype=np.uint8) if isinstance(blob, (bytes, bytearray)) else blob)
+    n = -(-blob.size // CHUNKSET_BYTES)
+    coeffs = np.ascontiguousarray(coeffs, dtype=np.uint8)
+    if out is None:
+        out = np.empty((n * N, CODED_PIECE_BYTES), dtype=np.uint8)
+    arr, k = _ctxs(ctxs)
+    vp = ctypes.c_void_p
+    check(lib().decds_blob_encode_host_multi(arr, k, vp(blob.ctypes.data), blob.size, vp(coeffs.ctypes.data),
+                                             vp(out.ctypes.data), batch))
+    return out
+
+
+def blob_repair_host_multi(ctxs, coded, cand, blob_len, batch=16, out=None):
+    """blob_repair_host sharded over several contexts (devices) by contiguous chunkset range."""
+    coded = np.ascontiguousarray(coded, dtype=np.uint8)
+    n = coded.shape[0] // N
+    cand = np.ascontiguousarray(cand, dtype=np.uint8).reshape(n, N)
+    if out is None:
+        out = np.empty(blob_len, dtype=np.uint8)
+    status = np.empty(n, dtype=np.int32)
+    arr, k = _ctxs(ctxs)
+    vp = ctypes.c_void_p
+    check(lib().decds_blob_repair_host_multi(arr, k, vp(coded.ctypes.data), n, vp(cand.ctypes.data), blob_len,
+                                             vp(out.ctypes.data), vp(status.ctypes.data), batch))
+    return out, status
+
+
 def host_register(arr):
     """page-lock a numpy buffer for repeated host-path calls (decds_host_register)"""
     check(lib().decds_host_register(ctypes.c_void_p(arr.ctypes.data), arr.nbytes))
@@ -143,5 +177,6 @@ def host_unregister(arr):
 
 
 __all__ = ["commit_batch", "encode_batch", "repair_plan_batch", "decode_batch", "repair_batch", "fill_random_device",
-           "fill_random_host", "blob_encode_host", "blob_repair_host", "host_register", "host_unregister",
+           "fill_random_host", "blob_encode_host", "blob_repair_host", "blob_encode_host_multi",
+           "blob_repair_host_multi", "host_register", "host_unregister",
            "NO_CANDIDATE"]

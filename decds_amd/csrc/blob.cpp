@@ -1,0 +1,815 @@
+// blob.cpp — decds-lib's blob level (decds-lib/src/blob.rs) over the batch kernels:
+//
+//   decds_blob_encode_host[_multi]     Blob::new chunkset loop          blob.rs:244-264
+//   decds_blob_repair_host[_multi]     RepairingBlob over all chunks    blob.rs:373-394, 451-473
+//   decds_blob_*                       Blob (new, header, get_share)    blob.rs:227-318
+//   decds_repairing_blob_*             RepairingBlob                    blob.rs:321-473
+//
+// Host paths stream batches of chunksets through one HIP stream per engine (H2D, kernels, D2H)
+// over three event-ordered buffer slots, so PCIe carries both directions at once. Caller buffers
+// registered with the library (decds_host_register / decds_host_alloc) are DMA'd directly; any
+// other host memory goes through the context's pinned bounce rings (host_mem.h). The _multi forms
+// shard chunksets by contiguous index range over several contexts (devices), one host thread each,
+// with no collective: chunksets are independent (blob.rs:256-264).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <mutex>
+#include <random>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/decds_rlnc.h"
+#include "capi_internal.h"
+#include "commit_kernels.h"
+#include "rlnc_kernels.h"
+#include "rlnc_layout.h"
+
+using namespace decds;
+
+namespace {
+
+constexpr int SLOTS = 3;
+inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+struct Pipe {
+    hipStream_t h2d = nullptr, comp = nullptr, d2h = nullptr;
+    hipEvent_t in_done[SLOTS] = {}, k_done[SLOTS] = {}, out_done[SLOTS] = {};
+    hipError_t init() {
+        hipError_t e;
+        for (hipStream_t *st : {&h2d, &comp, &d2h})
+            if ((e = hipStreamCreateWithFlags(st, hipStreamNonBlocking))) return e;
+        for (int i = 0; i < SLOTS; i++)
+            for (hipEvent_t *ev : {&in_done[i], &k_done[i], &out_done[i]}) {
+                if ((e = hipEventCreateWithFlags(ev, hipEventDisableTiming))) return e;
+                if ((e = hipEventRecord(*ev, comp))) return e;  // every slot starts free
+            }
+        return hipSuccess;
+    }
+    hipError_t drain() {
+        hipError_t e = hipSuccess, f;
+        for (hipStream_t st : {h2d, comp, d2h})
+            if (st && (f = hipStreamSynchronize(st)) && !e) e = f;
+        return e;
+    }
+    ~Pipe() {
+        (void)drain();
+        for (int i = 0; i < SLOTS; i++)
+            for (hipEvent_t ev : {in_done[i], k_done[i], out_done[i]})
+                if (ev) (void)hipEventDestroy(ev);
+        for (hipStream_t st : {h2d, comp, d2h})
+            if (st) (void)hipStreamDestroy(st);
+    }
+};
+
+// commitment outputs of the encode pipeline (Blob::new: chunkset.rs:54-63 per chunkset)
+struct CommitOut {
+    uint8_t *roots;   // n x 32
+    uint8_t *proofs;  // n x 16 x PROOF_SIZE x 32
+    uint64_t first_id;
+};
+
+// End of a host-path call: complete the deferred copy-outs, drain every stream; after a failure
+// the rings drop whatever they still hold for this call.
+int finish_call(decds_ctx *ctx, Pipe &pp, int rc) {
+    hipError_t e;
+    if (rc == DECDS_OK && (e = ctx->out_ring.flush())) rc = decds_hip_error(e, "D2H (staged)");
+    if ((e = pp.drain()) && rc == DECDS_OK) rc = decds_hip_error(e, "hipStreamSynchronize");
+    if (rc != DECDS_OK) {
+        ctx->out_ring.abandon();
+        ctx->in_ring.abandon();
+    }
+    return rc;
+}
+
+// Blob::new's chunkset loop over chunksets [0, ceil(blob_len / CS)) of `blob` (a shard's slice)
+int encode_range(decds_ctx *ctx, const uint8_t *blob, size_t blob_len, const uint8_t *coeffs, uint8_t *coded,
+                 size_t batch, const CommitOut *cm) {
+    int s = decds_ctx_bind(ctx);
+    if (s) return s;
+    const size_t n = (blob_len + CS - 1) / CS;  // blob.rs:252
+    if (batch == 0) batch = 16;                 // 8-32 measured best
+    batch = std::min(batch, n);
+    const size_t PRF = N * PROOF_SIZE * 32;
+    HostUse uin(blob, blob_len), ucv(coeffs, n * N * K), uout(coded, n * N * F);
+    HostUse urt(cm ? cm->roots : nullptr, n * 32), uprf(cm ? cm->proofs : nullptr, n * PRF);
+    std::lock_guard<std::mutex> lock(ctx->host_mu);
+    const size_t sz[6] = {align256(batch * CS), align256(batch * N * F), align256(batch * N * K),
+                          cm ? align256(batch * N * 32) : 0, cm ? align256(batch * 32) : 0, cm ? align256(batch * PRF) : 0};
+    const size_t per = sz[0] + sz[1] + sz[2] + sz[3] + sz[4] + sz[5];
+    uint8_t *base, *din[SLOTS], *dout[SLOTS], *dcv[SLOTS], *ddig[SLOTS], *drt[SLOTS], *dprf[SLOTS];
+    hipError_t e;
+    if ((e = decds_ctx_scratch(ctx, SLOTS * per, &base))) return decds_hip_error(e, "hipMalloc");
+    for (int i = 0; i < SLOTS; i++) {
+        uint8_t **dst[6] = {&din[i], &dout[i], &dcv[i], &ddig[i], &drt[i], &dprf[i]};
+        for (int j = 0; j < 6; j++) *dst[j] = base, base += sz[j];
+    }
+    Pipe pp;
+    if ((e = pp.init())) return decds_hip_error(e, "stream/event setup");
+    auto issue_d2h = [&](int k, size_t b0, size_t nb) -> int {
+        if ((e = hipStreamWaitEvent(pp.d2h, pp.k_done[k], 0)) ||
+            (e = copy_d2h(coded + b0 * N * F, dout[k], nb * N * F, uout.pinned(), ctx->out_ring, pp.d2h)) ||
+            (cm && (e = copy_d2h(cm->roots + b0 * 32, drt[k], nb * 32, urt.pinned(), ctx->out_ring, pp.d2h))) ||
+            (cm && (e = copy_d2h(cm->proofs + b0 * PRF, dprf[k], nb * PRF, uprf.pinned(), ctx->out_ring, pp.d2h))) ||
+            (e = hipEventRecord(pp.out_done[k], pp.d2h)))
+            return decds_hip_error(e, "D2H");
+        return DECDS_OK;
+    };
+    int rc = DECDS_OK, pend = -1;
+    size_t pend_b0 = 0, pend_nb = 0;
+    for (size_t b0 = 0, it = 0; b0 < n && rc == DECDS_OK; b0 += batch, it++) {
+        const int k = (int)(it % SLOTS);
+        const size_t nb = std::min(batch, n - b0);
+        const size_t off = b0 * CS, have = std::min(blob_len - off, nb * CS);
+        // inputs of slot k: free once the slot's previous kernel has read them
+        if ((e = hipStreamWaitEvent(pp.h2d, pp.k_done[k], 0)) ||
+            (e = copy_h2d(din[k], blob + off, have, uin.pinned(), ctx->in_ring, pp.h2d)) ||
+            (have < nb * CS && (e = hipMemsetAsync(din[k] + have, 0, nb * CS - have, pp.h2d))) ||  // blob.rs:254 zero pad
+            (e = copy_h2d(dcv[k], coeffs + b0 * N * K, nb * N * K, ucv.pinned(), ctx->in_ring, pp.h2d)) ||
+            (e = hipEventRecord(pp.in_done[k], pp.h2d))) {
+            rc = decds_hip_error(e, "H2D");
+            break;
+        }
+        // outputs of slot k: free once the slot's previous D2H has read them
+        if ((e = hipStreamWaitEvent(pp.comp, pp.in_done[k], 0)) || (e = hipStreamWaitEvent(pp.comp, pp.out_done[k], 0))) {
+            rc = decds_hip_error(e, "hipStreamWaitEvent");
+            break;
+        }
+        if ((rc = decds_encode_batch(ctx, din[k], nb, dcv[k], dout[k], F, pp.comp))) break;
+        if (cm && (rc = decds_commit_batch(ctx, dout[k], F, nb, cm->first_id + b0, ddig[k], drt[k], dprf[k], pp.comp)))
+            break;
+        if ((e = hipEventRecord(pp.k_done[k], pp.comp))) {
+            rc = decds_hip_error(e, "hipEventRecord");
+            break;
+        }
+        // the previous batch's D2H goes out after this batch's inputs: on the staged path the host
+        // then fills batch b+1's inputs while batch b-1's outputs drain
+        if (pend >= 0 && (rc = issue_d2h(pend, pend_b0, pend_nb))) break;
+        pend = k, pend_b0 = b0, pend_nb = nb;
+    }
+    if (rc == DECDS_OK && pend >= 0) rc = issue_d2h(pend, pend_b0, pend_nb);
+    return finish_call(ctx, pp, rc);
+}
+
+// RepairingBlob::add_chunk over every arrival + get_repaired_chunkset for chunksets [0, n) of a
+// shard: coded / cand / out / status point at the shard's first chunkset, blob_len is its length
+int repair_range(decds_ctx *ctx, const uint8_t *coded_host, size_t n, const uint8_t *cand_host, size_t blob_len,
+                 uint8_t *out, int32_t *status_host, size_t batch) {
+    int s = decds_ctx_bind(ctx);
+    if (s) return s;
+    if (batch == 0) batch = 16;  // 8-32 measured best
+    batch = std::min(batch, n);
+    // RepairingBlob::add_chunk over the arrival order (blob.rs:373-394): the rank test runs on the
+    // 10-byte coding vectors on the host, so only the 10 accepted rows of each chunkset cross PCIe
+    std::vector<uint8_t> sel(n * K, 0);
+    for (size_t c = 0; c < n; c++) {
+        uint8_t basis[K * K], piv[K];
+        uint32_t rank = 0;
+        for (uint32_t a = 0; a < N && rank < K; a++) {
+            const uint8_t row = cand_host[c * N + a];
+            if (row >= N) break;
+            if (decds_rank_push(basis, piv, &rank, coded_host + (c * N + row) * F, ctx->poly)) sel[c * K + rank - 1] = row;
+        }
+        status_host[c] = rank == K ? DECDS_OK : DECDS_ERR_CHUNKSET_NOT_YET_READY;
+    }
+    // per-slot candidate lists and device statuses in page-locked memory (tiny, per call)
+    struct Pinned {
+        void *p = nullptr;
+        ~Pinned() {
+            if (p) (void)hipHostFree(p);
+        }
+    } pin;
+    {
+        hipError_t pe = hipHostMalloc(&pin.p, SLOTS * batch * (N + sizeof(int32_t)), hipHostMallocDefault);
+        if (pe) return decds_hip_error(pe, "hipHostMalloc");
+    }
+    uint8_t *cand_h[SLOTS];
+    int32_t *stat_h[SLOTS];
+    for (int i = 0; i < SLOTS; i++) {
+        stat_h[i] = reinterpret_cast<int32_t *>(pin.p) + i * batch;
+        cand_h[i] = reinterpret_cast<uint8_t *>(pin.p) + SLOTS * batch * sizeof(int32_t) + i * batch * N;
+    }
+    HostUse uout(out, blob_len), uin(coded_host, n * N * F);
+    std::lock_guard<std::mutex> lock(ctx->host_mu);
+    uint8_t *dcoded[SLOTS], *dcand[SLOTS], *dplan[SLOTS], *dverd[SLOTS], *dstat[SLOTS], *ddst[SLOTS];
+    const size_t sz[6] = {align256(batch * N * F), align256(batch * N), align256(batch * DECDS_REPAIR_PLAN_BYTES),
+                          align256(batch * N), align256(batch * sizeof(int32_t)), align256(batch * CS)};
+    const size_t per = sz[0] + sz[1] + sz[2] + sz[3] + sz[4] + sz[5];
+    uint8_t *base;
+    hipError_t e;
+    if ((e = decds_ctx_scratch(ctx, SLOTS * per, &base))) return decds_hip_error(e, "hipMalloc");
+    for (int i = 0; i < SLOTS; i++) {
+        uint8_t **dst[6] = {&dcoded[i], &dcand[i], &dplan[i], &dverd[i], &dstat[i], &ddst[i]};
+        for (int j = 0; j < 6; j++) *dst[j] = base, base += sz[j];
+    }
+    Pipe pp;
+    if ((e = pp.init())) return decds_hip_error(e, "stream/event setup");
+    int rc = DECDS_OK;
+    size_t pending_b0[SLOTS], pending_nb[SLOTS] = {};
+    for (int i = 0; i < SLOTS; i++) pending_b0[i] = (size_t)-1;
+    // host side of slot k once its D2H is done: a ready chunkset whose decoded tail is not marker
+    // || zeros is ChunksetRepairingFailed and gets no data (its region was written: clear it)
+    auto finish = [&](int k) -> int {
+        if (pending_b0[k] == (size_t)-1) return DECDS_OK;
+        hipError_t ee = hipEventSynchronize(pp.out_done[k]);
+        if (ee) return decds_hip_error(ee, "hipEventSynchronize");
+        for (size_t c = 0; c < pending_nb[k]; c++) {
+            const size_t cs = pending_b0[k] + c;
+            if (status_host[cs] == DECDS_OK && stat_h[k][c] != DECDS_OK) {
+                status_host[cs] = DECDS_ERR_CHUNKSET_REPAIRING_FAILED;
+                if (!uout.pinned() && (ee = ctx->out_ring.flush())) return decds_hip_error(ee, "D2H (staged)");
+                const size_t off = cs * CS;
+                std::memset(out + off, 0, std::min(blob_len - off, (size_t)CS));
+            }
+        }
+        pending_b0[k] = (size_t)-1;
+        return DECDS_OK;
+    };
+    for (size_t b0 = 0, it = 0; b0 < n && rc == DECDS_OK; b0 += batch, it++) {
+        const int k = (int)(it % SLOTS);
+        if ((rc = finish(k))) break;  // slot k's previous batch fully done: all its buffers are free
+        const size_t nb = std::min(batch, n - b0);
+        // the accepted rows keep their own row slots on the device (slot layout = host layout less
+        // b0 chunksets), so runs of consecutive accepted rows — across chunkset boundaries too —
+        // cross the link as one copy each instead of one copy per row
+        std::vector<uint8_t> take(nb * N, 0);
+        for (size_t c = 0; c < nb; c++) {
+            const bool ready = status_host[b0 + c] == DECDS_OK;
+            for (uint32_t a = 0; a < N; a++)
+                cand_h[k][c * N + a] = ready && a < K ? sel[(b0 + c) * K + a] : (uint8_t)DECDS_NO_CANDIDATE;
+            if (ready)
+                for (uint32_t a = 0; a < K; a++) take[c * N + sel[(b0 + c) * K + a]] = 1;
+        }
+        for (size_t r0 = 0; r0 < nb * N && rc == DECDS_OK;) {
+            if (!take[r0]) {
+                r0++;
+                continue;
+            }
+            size_t r1 = r0 + 1;
+            while (r1 < nb * N && take[r1]) r1++;
+            if ((e = copy_h2d(dcoded[k] + r0 * F, coded_host + (b0 * N + r0) * F, (r1 - r0) * F, uin.pinned(),
+                              ctx->in_ring, pp.h2d)))
+                rc = decds_hip_error(e, "H2D");
+            r0 = r1;
+        }
+        if (rc) break;
+        if ((e = hipMemcpyAsync(dcand[k], cand_h[k], nb * N, hipMemcpyHostToDevice, pp.h2d)) ||
+            (e = hipEventRecord(pp.in_done[k], pp.h2d)) || (e = hipStreamWaitEvent(pp.comp, pp.in_done[k], 0))) {
+            rc = decds_hip_error(e, "H2D");
+            break;
+        }
+        if ((rc = decds_repair_batch(ctx, dcoded[k], F, nb, dcand[k], dplan[k], reinterpret_cast<int8_t *>(dverd[k]),
+                                     ddst[k], reinterpret_cast<int32_t *>(dstat[k]), pp.comp)))
+            break;
+        if ((e = hipEventRecord(pp.k_done[k], pp.comp)) || (e = hipStreamWaitEvent(pp.d2h, pp.k_done[k], 0)) ||
+            (e = hipMemcpyAsync(stat_h[k], dstat[k], nb * sizeof(int32_t), hipMemcpyDeviceToHost, pp.d2h))) {
+            rc = decds_hip_error(e, "D2H");
+            break;
+        }
+        // repaired data of the ready chunksets, runs of consecutive ones as one copy each; the last
+        // chunkset of the blob truncated to its real size (blob.rs:464). Unready chunksets get no data.
+        for (size_t c0 = 0; c0 < nb && rc == DECDS_OK;) {
+            const size_t off0 = (b0 + c0) * CS;
+            if (status_host[b0 + c0] != DECDS_OK) {
+                std::memset(out + off0, 0, std::min(blob_len - off0, (size_t)CS));
+                c0++;
+                continue;
+            }
+            size_t c1 = c0 + 1;
+            while (c1 < nb && status_host[b0 + c1] == DECDS_OK) c1++;
+            const size_t len = std::min(blob_len - off0, (c1 - c0) * CS);
+            if ((e = copy_d2h(out + off0, ddst[k] + c0 * CS, len, uout.pinned(), ctx->out_ring, pp.d2h)))
+                rc = decds_hip_error(e, "D2H");
+            c0 = c1;
+        }
+        if (rc) break;
+        if ((e = hipEventRecord(pp.out_done[k], pp.d2h))) {
+            rc = decds_hip_error(e, "hipEventRecord");
+            break;
+        }
+        pending_b0[k] = b0;
+        pending_nb[k] = nb;
+    }
+    for (int j = 0; j < SLOTS && rc == DECDS_OK; j++) rc = finish(j);  // each finish() waits on its own event
+    return finish_call(ctx, pp, rc);
+}
+
+// Runs fn(ctx_g, lo, hi) for contiguous chunkset shards [lo, hi) of [0, n), one host thread per
+// context; the first failing shard's status and message are the call's.
+template <class Fn>
+int run_shards(decds_ctx *const *ctxs, size_t n_ctx, size_t n, Fn fn) {
+    if (!ctxs || n_ctx == 0) return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "no contexts");
+    for (size_t g = 0; g < n_ctx; g++)
+        if (!ctxs[g]) return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "null context %zu", g);
+    const size_t per = (n + n_ctx - 1) / n_ctx;
+    if (n_ctx == 1) return fn(ctxs[0], (size_t)0, n);
+    std::vector<int> st(n_ctx, DECDS_OK);
+    std::vector<std::string> msg(n_ctx);
+    std::vector<std::thread> th;
+    for (size_t g = 0; g < n_ctx; g++) {
+        const size_t lo = std::min(g * per, n), hi = std::min(lo + per, n);
+        if (lo == hi) continue;
+        th.emplace_back([&, g, lo, hi] {
+            st[g] = fn(ctxs[g], lo, hi);
+            if (st[g] != DECDS_OK) msg[g] = decds_last_error();
+        });
+    }
+    for (auto &t : th) t.join();
+    for (size_t g = 0; g < n_ctx; g++)
+        if (st[g] != DECDS_OK) return decds_set_error(st[g], "shard %zu: %s", g, msg[g].c_str());
+    return DECDS_OK;
+}
+
+std::mutex g_rng_mu;
+void random_coeffs(uint8_t *out, size_t len) {
+    // the reference draws coding vectors from rand::rng() (chunkset.rs:42): OS-seeded, not reproducible
+    static std::mt19937_64 g{std::random_device{}()};
+    std::lock_guard<std::mutex> lk(g_rng_mu);
+    for (size_t i = 0; i < len; i++) out[i] = (uint8_t)g();
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------ Blob ----
+struct decds_blob {
+    uint64_t byte_length = 0, n = 0;
+    uint8_t digest[32], root[32];
+    std::vector<uint8_t> roots;      // n x 32 chunkset root commitments
+    std::vector<uint8_t> cs_proofs;  // n x 16 x PROOF_SIZE x 32 chunkset-level proofs
+    std::vector<uint8_t> blob_proofs;  // n x depth x 32 blob-level proofs (blob.rs:266-273)
+    size_t depth = 0;
+    uint8_t *coded = nullptr;        // n x 16 x F coded rows (page-locked via decds_host_alloc)
+    std::vector<uint8_t> coded_vec;  // fallback storage when a page-locked allocation is refused
+    ~decds_blob() {
+        if (coded && coded_vec.empty()) (void)decds_host_free(coded);
+    }
+};
+
+// ---------------------------------------------------------------------------- RepairingBlob ----
+namespace {
+struct RbChunkset {
+    uint8_t basis[K * K], piv[K];
+    uint8_t cv[K][K];  // coding vectors of the accepted rows, acceptance order
+    uint32_t rank = 0;
+    bool repaired = false;  // get_repaired_chunkset took it (blob.rs:458-462: even if repair fails)
+    bool decoded = false;   // decoded on the device into its slot's result area
+    int32_t dec_status = DECDS_OK;
+    int32_t slot = -1;
+};
+constexpr size_t RB_SLAB_SLOTS = 8;
+constexpr size_t RB_MAX_DECODE = 64;   // chunksets decoded per device batch
+constexpr size_t RB_MAX_ROWS = 256;    // rows validated per device batch (decds_repairing_blob_add_chunks)
+constexpr size_t RB_ROWS_BYTES = (K * F + 255) & ~(size_t)255;
+constexpr size_t RB_SLOT_BYTES = RB_ROWS_BYTES + ((CS + 255) & ~(size_t)255);
+// small device / pinned areas: plans, bases, statuses, valid flags
+constexpr size_t RB_SM_PLAN = 0, RB_SM_INB = RB_SM_PLAN + RB_MAX_DECODE * 128, RB_SM_OUTB = RB_SM_INB + RB_MAX_DECODE * 8,
+                 RB_SM_STAT = RB_SM_OUTB + RB_MAX_DECODE * 8, RB_SM_VALID = RB_SM_STAT + RB_MAX_DECODE * 4,
+                 RB_SM_BYTES = RB_SM_VALID + RB_MAX_ROWS;
+}  // namespace
+
+struct decds_repairing_blob {
+    decds_ctx *ctx = nullptr;
+    uint64_t byte_length = 0, n = 0;
+    uint8_t root[32];
+    std::vector<uint8_t> cs_roots;
+    std::vector<RbChunkset> cs;
+    hipStream_t s = nullptr;
+    BounceRing in_ring, out_ring;
+    std::vector<uint8_t *> slabs;
+    std::vector<int32_t> free_slots;
+    uint8_t *d_small = nullptr, *h_small = nullptr;
+    uint8_t *d_hdr = nullptr;     // chunkset roots (n x 32) + blob root (32), for decds_validate_batch
+    uint8_t *d_batch = nullptr;   // RB_MAX_ROWS rows + ids + proofs + digests of one validation batch
+    size_t batch_plen = 0;
+    ~decds_repairing_blob() {
+        if (ctx) (void)hipSetDevice(ctx->device);
+        if (s) (void)hipStreamSynchronize(s);
+        in_ring.abandon();
+        out_ring.abandon();
+        for (uint8_t *p : slabs) (void)hipFree(p);
+        for (uint8_t *p : {d_small, d_hdr, d_batch})
+            if (p) (void)hipFree(p);
+        if (h_small) (void)hipHostFree(h_small);
+        if (s) (void)hipStreamDestroy(s);
+    }
+    uint8_t *slot_rows(int32_t slot) const {
+        return slabs[slot / RB_SLAB_SLOTS] + (slot % RB_SLAB_SLOTS) * RB_SLOT_BYTES;
+    }
+    uint8_t *slot_out(int32_t slot) const { return slot_rows(slot) + RB_ROWS_BYTES; }
+    size_t chunkset_size(size_t c) const {  // BlobHeader::get_chunkset_size (blob.rs:84-94)
+        const uint64_t from = c * CS;
+        return (size_t)(std::min<uint64_t>(from + CS, byte_length) - from);
+    }
+    int take_slot(RbChunkset &c) {
+        if (c.slot >= 0) return DECDS_OK;
+        if (free_slots.empty()) {
+            uint8_t *p = nullptr;
+            hipError_t e = hipMalloc(reinterpret_cast<void **>(&p), RB_SLAB_SLOTS * RB_SLOT_BYTES);
+            if (e) return decds_hip_error(e, "hipMalloc (repair slots)");
+            slabs.push_back(p);
+            for (size_t i = RB_SLAB_SLOTS; i-- > 0;) free_slots.push_back((int32_t)((slabs.size() - 1) * RB_SLAB_SLOTS + i));
+        }
+        c.slot = free_slots.back();
+        free_slots.pop_back();
+        return DECDS_OK;
+    }
+    void drop_slot(RbChunkset &c) {
+        if (c.slot >= 0) free_slots.push_back(c.slot);
+        c.slot = -1;
+    }
+    // the routing checks of RepairingBlob::add_chunk that precede validation (blob.rs:374-381)
+    int route_check(uint64_t cs_id) {
+        if (cs_id >= n)
+            return decds_set_error(DECDS_ERR_INVALID_CHUNKSET_ID, "invalid chunkset id: %llu (num_chunksets: %llu)",
+                                   (unsigned long long)cs_id, (unsigned long long)n);
+        if (cs[cs_id].repaired)
+            return decds_set_error(DECDS_ERR_CHUNKSET_ALREADY_REPAIRED, "chunkset %llu is already repaired",
+                                   (unsigned long long)cs_id);
+        return DECDS_OK;
+    }
+    // after validation (blob.rs:383-388): ready check, then add_chunk_unvalidated's rank step
+    // (chunkset.rs:177-183). On success the row's coding vector is recorded and its slot row index
+    // (rank - 1) returned through *row.
+    int accept(uint64_t cs_id, const uint8_t *cv, size_t len, uint32_t *row) {
+        RbChunkset &c = cs[cs_id];
+        if (c.rank == K)
+            return decds_set_error(DECDS_ERR_CHUNKSET_READY_TO_REPAIR, "chunkset %llu is ready to repair",
+                                   (unsigned long long)cs_id);
+        if (len != F)
+            return decds_set_error(DECDS_ERR_CHUNK_DECODING_FAILED,
+                                   "decoding chunk for chunkset %llu failed: invalid piece length %zu",
+                                   (unsigned long long)cs_id, len);
+        int s = take_slot(c);
+        if (s) return s;
+        if (!decds_rank_push(c.basis, c.piv, &c.rank, cv, ctx->poly))
+            return decds_set_error(DECDS_ERR_CHUNK_DECODING_FAILED,
+                                   "decoding chunk for chunkset %llu failed: received piece is not useful",
+                                   (unsigned long long)cs_id);
+        std::memcpy(c.cv[c.rank - 1], cv, K);
+        *row = c.rank - 1;
+        return DECDS_OK;
+    }
+    // decode `first` and up to RB_MAX_DECODE - 1 further ready, undecoded chunksets in one launch
+    int decode_ready(size_t first) {
+        std::vector<size_t> todo{first};
+        for (size_t c = 0; c < n && todo.size() < RB_MAX_DECODE; c++)
+            if (c != first && cs[c].rank == K && !cs[c].decoded && !cs[c].repaired) todo.push_back(c);
+        const size_t m = todo.size();
+        RepairPlan *plans = reinterpret_cast<RepairPlan *>(h_small + RB_SM_PLAN);
+        uint64_t *inb = reinterpret_cast<uint64_t *>(h_small + RB_SM_INB), *outb = reinterpret_cast<uint64_t *>(h_small + RB_SM_OUTB);
+        for (size_t i = 0; i < m; i++) {
+            RbChunkset &c = cs[todo[i]];
+            std::memset(&plans[i], 0, sizeof(RepairPlan));
+            for (uint32_t k = 0; k < K; k++) plans[i].sel[k] = (uint8_t)k;
+            plans[i].rank = K;
+            if (!host_gf_invert(&c.cv[0][0], plans[i].inv, ctx->poly))
+                return decds_set_error(DECDS_ERR_CHUNKSET_REPAIRING_FAILED, "accepted coding vectors are singular");
+            inb[i] = reinterpret_cast<uint64_t>(slot_rows(c.slot));
+            outb[i] = reinterpret_cast<uint64_t>(slot_out(c.slot));
+        }
+        hipError_t e;
+        if ((e = hipMemcpyAsync(d_small, h_small, RB_SM_STAT, hipMemcpyHostToDevice, s)) ||
+            (e = hipMemsetAsync(d_small + RB_SM_STAT, 0, m * 4, s)))
+            return decds_hip_error(e, "H2D (plans)");
+        e = launch_decode(ctx->geom, nullptr, F, m, d_small + RB_SM_PLAN, nullptr,
+                          reinterpret_cast<int32_t *>(d_small + RB_SM_STAT), reinterpret_cast<const uint64_t *>(d_small + RB_SM_INB),
+                          reinterpret_cast<const uint64_t *>(d_small + RB_SM_OUTB), ctx->poly, ctx->marker, s);
+        if (e) return decds_hip_error(e, "rlnc_decode_kernel launch");
+        if ((e = hipMemcpyAsync(h_small + RB_SM_STAT, d_small + RB_SM_STAT, m * 4, hipMemcpyDeviceToHost, s)) ||
+            (e = hipStreamSynchronize(s)))
+            return decds_hip_error(e, "D2H (statuses)");
+        const int32_t *st = reinterpret_cast<const int32_t *>(h_small + RB_SM_STAT);
+        for (size_t i = 0; i < m; i++) {
+            cs[todo[i]].decoded = true;
+            cs[todo[i]].dec_status = st[i];
+        }
+        return DECDS_OK;
+    }
+};
+
+extern "C" {
+
+int decds_blob_encode_host(decds_ctx *ctx, const uint8_t *blob, size_t blob_len, const uint8_t *coeffs_host,
+                           uint8_t *coded_host, size_t batch) {
+    if (blob_len == 0) return decds_set_error(DECDS_ERR_EMPTY_DATA_FOR_BLOB, "empty data for blob");  // blob.rs:245-247
+    if (!blob || !coeffs_host || !coded_host) return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "null buffer");
+    return encode_range(ctx, blob, blob_len, coeffs_host, coded_host, batch, nullptr);
+}
+
+int decds_blob_encode_host_multi(decds_ctx *const *ctxs, size_t n_ctx, const uint8_t *blob, size_t blob_len,
+                                 const uint8_t *coeffs_host, uint8_t *coded_host, size_t batch) {
+    if (blob_len == 0) return decds_set_error(DECDS_ERR_EMPTY_DATA_FOR_BLOB, "empty data for blob");
+    if (!blob || !coeffs_host || !coded_host) return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "null buffer");
+    const size_t n = (blob_len + CS - 1) / CS;
+    return run_shards(ctxs, n_ctx, n, [&](decds_ctx *ctx, size_t lo, size_t hi) {
+        const size_t len = std::min<uint64_t>(blob_len, hi * CS) - lo * CS;
+        return encode_range(ctx, blob + lo * CS, len, coeffs_host + lo * N * K, coded_host + lo * N * F, batch, nullptr);
+    });
+}
+
+static int check_repair_args(const uint8_t *coded_host, size_t n, const uint8_t *cand_host, size_t blob_len,
+                             const uint8_t *out, const int32_t *status_host) {
+    if (!coded_host || !cand_host || !out || !status_host || n == 0)
+        return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "null buffer or no chunksets");
+    if (blob_len > n * CS || blob_len <= (n - 1) * CS)
+        return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "blob length %zu inconsistent with %zu chunksets", blob_len, n);
+    return DECDS_OK;
+}
+
+int decds_blob_repair_host(decds_ctx *ctx, const uint8_t *coded_host, size_t n, const uint8_t *cand_host,
+                           size_t blob_len, uint8_t *out, int32_t *status_host, size_t batch) {
+    int s = check_repair_args(coded_host, n, cand_host, blob_len, out, status_host);
+    if (s) return s;
+    return repair_range(ctx, coded_host, n, cand_host, blob_len, out, status_host, batch);
+}
+
+int decds_blob_repair_host_multi(decds_ctx *const *ctxs, size_t n_ctx, const uint8_t *coded_host, size_t n,
+                                 const uint8_t *cand_host, size_t blob_len, uint8_t *out, int32_t *status_host,
+                                 size_t batch) {
+    int s = check_repair_args(coded_host, n, cand_host, blob_len, out, status_host);
+    if (s) return s;
+    return run_shards(ctxs, n_ctx, n, [&](decds_ctx *ctx, size_t lo, size_t hi) {
+        const size_t len = std::min<uint64_t>(blob_len, hi * CS) - lo * CS;
+        return repair_range(ctx, coded_host + lo * N * F, hi - lo, cand_host + lo * N, len, out + lo * CS,
+                            status_host + lo, batch);
+    });
+}
+
+// ---- Blob -------------------------------------------------------------------------------------
+int decds_blob_new(decds_ctx *const *ctxs, size_t n_ctx, const uint8_t *data, size_t len, const uint8_t *coeffs,
+                   decds_blob **out) {
+    if (!out) return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "null out pointer");
+    *out = nullptr;
+    if (len == 0) return decds_set_error(DECDS_ERR_EMPTY_DATA_FOR_BLOB, "empty data for blob");  // blob.rs:245-247
+    if (!data) return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "null data");
+    if (!ctxs || n_ctx == 0) return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "no contexts");
+    auto *b = new decds_blob;
+    b->byte_length = len;
+    b->n = (len + CS - 1) / CS;  // blob.rs:252
+    const size_t n = b->n;
+    std::vector<uint8_t> cv;
+    if (!coeffs) {
+        cv.resize(n * N * K);
+        random_coeffs(cv.data(), cv.size());
+        coeffs = cv.data();
+    }
+    void *p = nullptr;
+    if (decds_host_alloc(n * N * F, &p) == DECDS_OK) {
+        b->coded = static_cast<uint8_t *>(p);
+    } else {  // page-locked memory refused: plain memory, staged copies
+        b->coded_vec.resize(n * N * F);
+        b->coded = b->coded_vec.data();
+    }
+    b->roots.resize(n * 32);
+    b->cs_proofs.resize(n * N * PROOF_SIZE * 32);
+    // blob.rs:249 whole-blob BLAKE3 on host threads, beside the device work
+    std::thread dig([&] {
+        const unsigned hw = std::thread::hardware_concurrency();
+        decds_blake3_parallel(data, len, b->digest, (int)std::min(16u, hw ? hw : 4u));
+    });
+    int s = run_shards(ctxs, n_ctx, n, [&](decds_ctx *ctx, size_t lo, size_t hi) {
+        const size_t l = std::min<uint64_t>(len, hi * CS) - lo * CS;
+        const CommitOut cm{b->roots.data() + lo * 32, b->cs_proofs.data() + lo * N * PROOF_SIZE * 32, lo};
+        return encode_range(ctx, data + lo * CS, l, coeffs + lo * N * K, b->coded + lo * N * F, 0, &cm);
+    });
+    dig.join();
+    if (s) {
+        delete b;
+        return s;
+    }
+    // blob.rs:266-273: Merkle tree over the chunkset roots; every chunk carries its chunkset's path
+    int depth = 0;
+    while (((size_t)1 << depth) < n) depth++;
+    b->depth = (size_t)depth;
+    b->blob_proofs.resize(std::max<size_t>(1, n * b->depth * 32));
+    if ((s = decds_merkle_tree(b->roots.data(), n, b->root, b->blob_proofs.data())) < 0) {
+        delete b;
+        return s;
+    }
+    *out = b;
+    return DECDS_OK;
+}
+
+int decds_blob_get_header(const decds_blob *b, uint64_t *byte_length, uint64_t *num_chunksets, uint8_t *digest,
+                          uint8_t *root, const uint8_t **chunkset_roots) {
+    if (!b) return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "null blob");
+    if (byte_length) *byte_length = b->byte_length;
+    if (num_chunksets) *num_chunksets = b->n;
+    if (digest) std::memcpy(digest, b->digest, 32);
+    if (root) std::memcpy(root, b->root, 32);
+    if (chunkset_roots) *chunkset_roots = b->roots.data();
+    return DECDS_OK;
+}
+
+size_t decds_blob_proof_len(const decds_blob *b) { return b ? PROOF_SIZE + b->depth : 0; }
+
+int decds_blob_get_chunk(const decds_blob *b, size_t chunkset_id, size_t share_id, const uint8_t **data,
+                         uint8_t *proof, size_t proof_cap) {
+    if (!b) return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "null blob");
+    if (share_id >= N)
+        return decds_set_error(DECDS_ERR_INVALID_SHARE_ID, "invalid erasure coded share id: %zu (num_shares: %u)", share_id, N);
+    if (chunkset_id >= b->n)
+        return decds_set_error(DECDS_ERR_INVALID_CHUNKSET_ID, "invalid chunkset id: %zu (num_chunksets: %llu)", chunkset_id,
+                               (unsigned long long)b->n);
+    if (data) *data = b->coded + (chunkset_id * N + share_id) * F;
+    if (proof) {
+        const size_t plen = PROOF_SIZE + b->depth;
+        if (proof_cap < plen * 32) return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "proof buffer < %zu", plen * 32);
+        std::memcpy(proof, &b->cs_proofs[(chunkset_id * N + share_id) * PROOF_SIZE * 32], PROOF_SIZE * 32);
+        if (b->depth) std::memcpy(proof + PROOF_SIZE * 32, &b->blob_proofs[chunkset_id * b->depth * 32], b->depth * 32);
+    }
+    return DECDS_OK;
+}
+
+int decds_blob_get_share(const decds_blob *b, size_t share_id, uint8_t *data, size_t data_cap, uint8_t *proofs,
+                         size_t proofs_cap) {
+    if (!b) return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "null blob");
+    if (share_id >= N)  // blob.rs:307-309
+        return decds_set_error(DECDS_ERR_INVALID_SHARE_ID, "invalid erasure coded share id: %zu (num_shares: %u)", share_id, N);
+    const size_t plen = PROOF_SIZE + b->depth;
+    if ((data && data_cap < b->n * F) || (proofs && proofs_cap < b->n * plen * 32))
+        return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "output buffers too small");
+    for (size_t c = 0; c < b->n; c++) {
+        const uint8_t *d;
+        int s = decds_blob_get_chunk(b, c, share_id, &d, proofs ? proofs + c * plen * 32 : nullptr, plen * 32);
+        if (s) return s;
+        if (data) std::memcpy(data + c * F, d, F);
+    }
+    return DECDS_OK;
+}
+
+void decds_blob_free(decds_blob *b) { delete b; }
+
+// ---- RepairingBlob ----------------------------------------------------------------------------
+int decds_repairing_blob_new(decds_ctx *ctx, uint64_t byte_length, uint64_t num_chunksets, const uint8_t *root,
+                             const uint8_t *chunkset_roots, decds_repairing_blob **out) {
+    if (!out) return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "null out pointer");
+    *out = nullptr;
+    if (!root || (num_chunksets && !chunkset_roots) || num_chunksets == 0)
+        return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "null header field or no chunksets");
+    if (byte_length > num_chunksets * CS || byte_length <= (num_chunksets - 1) * CS)
+        return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "blob length %llu inconsistent with %llu chunksets",
+                               (unsigned long long)byte_length, (unsigned long long)num_chunksets);
+    int s = decds_ctx_bind(ctx);
+    if (s) return s;
+    auto *rb = new decds_repairing_blob;
+    rb->ctx = ctx;
+    rb->byte_length = byte_length;
+    rb->n = num_chunksets;
+    std::memcpy(rb->root, root, 32);
+    rb->cs_roots.assign(chunkset_roots, chunkset_roots + num_chunksets * 32);
+    rb->cs.resize(num_chunksets);
+    hipError_t e;
+    if ((e = hipStreamCreateWithFlags(&rb->s, hipStreamNonBlocking)) ||
+        (e = hipMalloc(reinterpret_cast<void **>(&rb->d_small), RB_SM_BYTES)) ||
+        (e = hipHostMalloc(reinterpret_cast<void **>(&rb->h_small), RB_SM_BYTES, hipHostMallocDefault)) ||
+        (e = hipMalloc(reinterpret_cast<void **>(&rb->d_hdr), (num_chunksets + 1) * 32)) ||
+        (e = hipMemcpyAsync(rb->d_hdr, chunkset_roots, num_chunksets * 32, hipMemcpyHostToDevice, rb->s)) ||
+        (e = hipMemcpyAsync(rb->d_hdr + num_chunksets * 32, root, 32, hipMemcpyHostToDevice, rb->s)) ||
+        (e = hipStreamSynchronize(rb->s))) {
+        delete rb;
+        return decds_hip_error(e, "RepairingBlob setup");
+    }
+    *out = rb;
+    return DECDS_OK;
+}
+
+int decds_repairing_blob_add_chunk(decds_repairing_blob *rb, uint64_t chunkset_id, uint64_t chunk_id,
+                                   const uint8_t *data, size_t len, const uint8_t *proof, size_t proof_len) {
+    if (!rb) return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "null repairing blob");
+    int s = rb->route_check(chunkset_id);
+    if (s) return s;
+    // BlobHeader::validate_chunk (blob.rs:211-215): blob-level proof at the global chunk id, the
+    // chunkset id in range, then the first 4 hashes against the chunkset root (chunk.rs:88-110)
+    bool ok = proof && proof_len >= PROOF_SIZE && (data || len == 0);
+    if (ok) {
+        uint8_t leaf[32];
+        decds_chunk_digest(chunkset_id, chunk_id, data, len, leaf);
+        ok = decds_merkle_verify(chunk_id, leaf, proof, proof_len, rb->root) == 1 &&
+             decds_merkle_verify(chunk_id % N, leaf, proof, PROOF_SIZE, &rb->cs_roots[chunkset_id * 32]) == 1;
+    }
+    if (!ok)
+        return decds_set_error(DECDS_ERR_INVALID_PROOF_IN_CHUNK, "invalid proof in chunk of chunkset %llu",
+                               (unsigned long long)chunkset_id);
+    if ((s = decds_ctx_bind(rb->ctx))) return s;
+    uint32_t row;
+    if ((s = rb->accept(chunkset_id, data, len, &row))) return s;
+    // the row goes to its device slot now (staged: the caller's buffer is free when this returns)
+    hipError_t e = rb->in_ring.h2d(rb->slot_rows(rb->cs[chunkset_id].slot) + row * F, data, F, rb->s);
+    return e ? decds_hip_error(e, "H2D (accepted row)") : DECDS_OK;
+}
+
+int decds_repairing_blob_add_chunks(decds_repairing_blob *rb, size_t n_rows, const uint64_t *ids, const uint8_t *rows,
+                                    const uint8_t *proofs, size_t proof_len, int32_t *status) {
+    if (!rb || (n_rows && (!ids || !rows || !status))) return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "null argument");
+    if (n_rows && proof_len && !proofs) return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "null proofs");
+    int s = decds_ctx_bind(rb->ctx);
+    if (s) return s;
+    decds_ctx *ctx = rb->ctx;
+    const size_t P = proof_len * 32;
+    // device batch area: RB_MAX_ROWS rows | ids | proofs (sized for the longest proof seen) | digests
+    hipError_t e;
+    if (!rb->d_batch || rb->batch_plen < proof_len) {
+        if (rb->d_batch) {
+            (void)hipStreamSynchronize(rb->s);
+            (void)hipFree(rb->d_batch);
+            rb->d_batch = nullptr;
+        }
+        const size_t total = RB_MAX_ROWS * (F + 16 + P + 32);
+        if ((e = hipMalloc(reinterpret_cast<void **>(&rb->d_batch), total))) return decds_hip_error(e, "hipMalloc");
+        rb->batch_plen = proof_len;
+    }
+    const size_t a_ids = RB_MAX_ROWS * F, a_prf = a_ids + RB_MAX_ROWS * 16,
+                 a_dig = a_prf + RB_MAX_ROWS * rb->batch_plen * 32;
+    HostUse urows(rows, n_rows * F), uids(ids, n_rows * 16), uprf(proofs, n_rows * P);
+    for (size_t r0 = 0; r0 < n_rows; r0 += RB_MAX_ROWS) {
+        const size_t m = std::min(RB_MAX_ROWS, n_rows - r0);
+        // BlobHeader::validate_chunk for the whole batch on the device (one digest per row, both proofs)
+        if ((e = copy_h2d(rb->d_batch, rows + r0 * F, m * F, urows.pinned(), rb->in_ring, rb->s)) ||
+            (e = copy_h2d(rb->d_batch + a_ids, reinterpret_cast<const uint8_t *>(ids + 2 * r0), m * 16, uids.pinned(),
+                          rb->in_ring, rb->s)) ||
+            (P && (e = copy_h2d(rb->d_batch + a_prf, proofs + r0 * P, m * P, uprf.pinned(), rb->in_ring, rb->s))))
+            return decds_hip_error(e, "H2D (rows)");
+        if ((s = decds_validate_batch(ctx, rb->d_batch, F, m, reinterpret_cast<const uint64_t *>(rb->d_batch + a_ids),
+                                      rb->d_batch + a_prf, proof_len, rb->d_hdr, rb->n, rb->d_hdr + rb->n * 32,
+                                      rb->d_batch + a_dig, rb->d_small + RB_SM_VALID, rb->s)))
+            return s;
+        if ((e = hipMemcpyAsync(rb->h_small + RB_SM_VALID, rb->d_small + RB_SM_VALID, m, hipMemcpyDeviceToHost, rb->s)) ||
+            (e = hipStreamSynchronize(rb->s)))
+            return decds_hip_error(e, "D2H (verdicts)");
+        // RepairingBlob::add_chunk's checks in arrival order (blob.rs:373-394)
+        for (size_t i = 0; i < m; i++) {
+            const uint64_t cid = ids[2 * (r0 + i)];
+            int st = rb->route_check(cid);
+            if (st == DECDS_OK && !rb->h_small[RB_SM_VALID + i])
+                st = decds_set_error(DECDS_ERR_INVALID_PROOF_IN_CHUNK, "invalid proof in chunk of chunkset %llu",
+                                     (unsigned long long)cid);
+            uint32_t row = 0;
+            if (st == DECDS_OK) st = rb->accept(cid, rows + (r0 + i) * F, F, &row);
+            if (st == DECDS_OK &&
+                (e = hipMemcpyAsync(rb->slot_rows(rb->cs[cid].slot) + row * F, rb->d_batch + i * F, F,
+                                    hipMemcpyDeviceToDevice, rb->s)))
+                return decds_hip_error(e, "D2D (accepted row)");
+            status[r0 + i] = st;
+        }
+    }
+    if ((e = hipStreamSynchronize(rb->s))) return decds_hip_error(e, "hipStreamSynchronize");
+    return DECDS_OK;
+}
+
+int decds_repairing_blob_is_chunkset_ready_to_repair(const decds_repairing_blob *rb, size_t chunkset_id, int *out) {
+    if (!rb || !out) return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "null argument");
+    if (chunkset_id >= rb->n)  // blob.rs:407-414
+        return decds_set_error(DECDS_ERR_INVALID_CHUNKSET_ID, "invalid chunkset id: %zu (num_chunksets: %llu)", chunkset_id,
+                               (unsigned long long)rb->n);
+    *out = !rb->cs[chunkset_id].repaired && rb->cs[chunkset_id].rank == K;
+    return DECDS_OK;
+}
+
+int decds_repairing_blob_is_chunkset_already_repaired(const decds_repairing_blob *rb, size_t chunkset_id, int *out) {
+    if (!rb || !out) return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "null argument");
+    if (chunkset_id >= rb->n)  // blob.rs:424-430
+        return decds_set_error(DECDS_ERR_INVALID_CHUNKSET_ID, "invalid chunkset id: %zu (num_chunksets: %llu)", chunkset_id,
+                               (unsigned long long)rb->n);
+    *out = rb->cs[chunkset_id].repaired;
+    return DECDS_OK;
+}
+
+int decds_repairing_blob_get_repaired_chunkset(decds_repairing_blob *rb, size_t chunkset_id, uint8_t *out,
+                                               size_t out_cap, size_t *out_len) {
+    if (!rb) return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "null repairing blob");
+    // blob.rs:451-473: id check, already repaired, not yet ready, then the chunkset is consumed
+    if (chunkset_id >= rb->n)
+        return decds_set_error(DECDS_ERR_INVALID_CHUNKSET_ID, "invalid chunkset id: %zu (num_chunksets: %llu)", chunkset_id,
+                               (unsigned long long)rb->n);
+    RbChunkset &c = rb->cs[chunkset_id];
+    if (c.repaired) return decds_set_error(DECDS_ERR_CHUNKSET_ALREADY_REPAIRED, "chunkset %zu is already repaired", chunkset_id);
+    if (c.rank != K) return decds_set_error(DECDS_ERR_CHUNKSET_NOT_YET_READY, "chunkset %zu is not ready to repair", chunkset_id);
+    const size_t size = rb->chunkset_size(chunkset_id);
+    if (!out || out_cap < size) return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "out buffer < %zu", size);
+    int s = decds_ctx_bind(rb->ctx);
+    if (s) return s;
+    if (!c.decoded && (s = rb->decode_ready(chunkset_id))) return s;
+    c.repaired = true;  // blob.rs:458-462 takes the decoder out before repairing
+    if (c.dec_status != DECDS_OK) {
+        rb->drop_slot(c);
+        return decds_set_error(DECDS_ERR_CHUNKSET_REPAIRING_FAILED, "chunkset %zu repairing failed: RLNC Decoding error: %s",
+                               chunkset_id, "invalid decoded data format");
+    }
+    HostUse uo(out, size);
+    hipError_t e;
+    if ((e = copy_d2h(out, rb->slot_out(c.slot), size, uo.pinned(), rb->out_ring, rb->s)) ||
+        (e = rb->out_ring.flush()) || (e = hipStreamSynchronize(rb->s))) {
+        rb->out_ring.abandon();
+        return decds_hip_error(e, "D2H (repaired chunkset)");
+    }
+    rb->drop_slot(c);
+    if (out_len) *out_len = size;  // blob.rs:464 truncate to the chunkset's real size
+    return DECDS_OK;
+}
+
+void decds_repairing_blob_free(decds_repairing_blob *rb) { delete rb; }
+
+}  // extern "C"

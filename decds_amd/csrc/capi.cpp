@@ -110,18 +110,27 @@ int decds_ctx_create(int device, decds_ctx **out) {
     c->marker = (uint8_t)MARKER_DEFAULT;
     c->gen = host_gf_generator(POLY_DEFAULT);
     c->geom.num_cus = prop.multiProcessorCount;
-    if (const char *w = std::getenv("DECDS_WGS_PER_CU")) c->geom.wgs_per_cu = std::atoi(w) == 1 ? 1 : 2;
     *out = c;
     return DECDS_OK;
 }
 
 int decds_ctx_destroy(decds_ctx *ctx) {
-    if (ctx && ctx->host_scratch) {
-        (void)hipSetDevice(ctx->device);
-        (void)hipFree(ctx->host_scratch);
-    }
+    if (!ctx) return DECDS_OK;
+    (void)hipSetDevice(ctx->device);
+    decds_lanes_destroy(ctx);
+    if (ctx->host_scratch) (void)hipFree(ctx->host_scratch);
     delete ctx;
     return DECDS_OK;
+}
+
+int decds_device_status(const decds_ctx *ctx) {
+    int s = decds_ctx_bind(ctx);
+    if (s) return s;
+    // a sticky device fault surfaces here; report it rather than whichever call runs next
+    hipError_t e = hipDeviceSynchronize();
+    if (e != hipSuccess) return decds_hip_error(e, "device status");
+    e = hipGetLastError();
+    return e == hipSuccess ? DECDS_OK : decds_hip_error(e, "device status (last error)");
 }
 
 int decds_ctx_set_field(decds_ctx *ctx, uint32_t poly, uint8_t marker) {
@@ -184,7 +193,7 @@ int decds_decode_batch(decds_ctx *ctx, const uint8_t *coded, size_t coded_pitch,
     int s;
     if ((s = decds_ctx_bind(ctx)) || (s = check_n(n)) || (s = check_pitch(coded_pitch))) return s;
     if (!coded || !plan || !dst || !status) return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "null buffer");
-    hipError_t e = launch_decode(ctx->geom, coded, coded_pitch, n, plan, dst, status, ctx->poly,
+    hipError_t e = launch_decode(ctx->geom, coded, coded_pitch, n, plan, dst, status, nullptr, nullptr, ctx->poly,
                                  ctx->marker, (hipStream_t)stream);
     return e == hipSuccess ? DECDS_OK : decds_hip_error(e, "rlnc_decode_kernel launch");
 }

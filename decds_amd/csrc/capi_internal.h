@@ -3,9 +3,16 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <condition_variable>
 #include <mutex>
+#include <vector>
 
+#include "host_mem.h"
 #include "rlnc_kernels.h"
+
+namespace decds {
+struct Lane;  // chunkset.cpp: the buffers and stream of one in-flight chunkset-mirror call
+}
 
 struct decds_ctx {
     int device;
@@ -13,15 +20,23 @@ struct decds_ctx {
     uint8_t marker;    // boundary marker appended by rlnc Encoder::new (0x81 [recalled])
     uint32_t gen;      // smallest generator of GF(2^8)* under poly (the plan kernel's log/exp tables)
     decds::LaunchGeom geom;
-    // device buffers of the host blob paths (decds_blob_*_host), kept across calls (grow-only) so a
-    // call does not pay hipMalloc / hipFree of its slot buffers; host_mu serialises those calls
+    // host blob paths (decds_blob_*_host, Blob, RepairingBlob): device slot buffers kept across
+    // calls (grow-only) and the pinned bounce rings for caller memory that is not page-locked;
+    // host_mu serialises those calls on one context
     std::mutex host_mu;
     uint8_t *host_scratch = nullptr;
     size_t host_scratch_cap = 0;
+    decds::BounceRing in_ring, out_ring;
+    // chunkset mirror (decds_chunkset_new, decds_repairing_chunkset_repair): a pool of lanes, one
+    // per concurrent caller (the reference calls ChunkSet::new from rayon workers, blob.rs:256-264)
+    std::mutex lane_mu;
+    std::condition_variable lane_cv;
+    std::vector<decds::Lane *> lanes_all, lanes_free;
 };
 
 // at least `bytes` of the context's host-path scratch (caller holds ctx->host_mu)
 hipError_t decds_ctx_scratch(decds_ctx *ctx, size_t bytes, uint8_t **out);
+void decds_lanes_destroy(decds_ctx *ctx);  // chunkset.cpp
 
 int decds_set_error(int code, const char *fmt, ...);
 int decds_hip_error(hipError_t e, const char *what);
@@ -33,4 +48,6 @@ uint8_t host_gf_mul(uint8_t a, uint8_t b, uint32_t poly);
 uint8_t host_gf_inv(uint8_t a, uint32_t poly);
 // smallest element of multiplicative order 255, or 0 when poly is reducible (no field)
 uint32_t host_gf_generator(uint32_t poly);
+// inverse of a 10x10 matrix over GF(2^8) (row-major); false if singular
+bool host_gf_invert(const uint8_t *m, uint8_t *inv, uint32_t poly);
 }  // namespace decds

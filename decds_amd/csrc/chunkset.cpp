@@ -1,16 +1,21 @@
-// chunkset.cpp — host-side mirror of decds-lib's chunkset API (chunkset.rs) and of the blob-level
-// chunkset iteration (blob.rs) over the gfx950 batch kernels. Same names, argument meaning and
-// error behaviour as the reference, including ChunkSet::new's commitment (digests, Merkle root,
-// proofs: computed on the device by decds_commit_batch) and RepairingChunkSet::add_chunk's proof check.
+// chunkset.cpp — host-side mirror of decds-lib's chunkset API (chunkset.rs) over the gfx950 batch
+// kernels. Same names, argument meaning and error behaviour as the reference, including
+// ChunkSet::new's commitment (digests, Merkle root, proofs: computed on the device by the commit
+// kernels) and RepairingChunkSet::add_chunk's proof check.
 //
 //   decds_chunkset_new                 ChunkSet::new                    chunkset.rs:37-69
 //   decds_chunkset_get_chunk           ChunkSet::get_chunk              chunkset.rs:87-89
 //   decds_repairing_chunkset_*         RepairingChunkSet                chunkset.rs:107-208
-//   decds_blob_encode_host             Blob::new chunkset loop          blob.rs:244-264
-//   decds_blob_repair_host             RepairingBlob add/get_repaired   blob.rs:373-394, 451-473
+//
+// The reference calls ChunkSet::new from rayon workers (blob.rs:256-264), so concurrent callers
+// are the normal case: each call takes a lane from the context's pool — its own stream, device
+// buffers and page-locked staging, all kept across calls — so callers neither allocate per call
+// nor serialise on the null stream. Caller memory is copied through the lane's staging buffer
+// (the library never page-locks it).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <random>
@@ -18,18 +23,101 @@
 
 #include "../../include/decds_rlnc.h"
 #include "capi_internal.h"
+#include "commit_kernels.h"
 #include "rlnc_layout.h"
 
 using namespace decds;
 
+namespace decds {
+
+// Device and pinned buffers of one in-flight chunkset-mirror call. Small-area offsets (device and
+// host mirror alike):
+constexpr size_t SM_CV = 0, SM_CAND = 256, SM_STATUS = 288, SM_VERD = 320, SM_PLAN = 384, SM_ROOT = 512,
+                 SM_DIG = 1024, SM_PRF = 2048, SM_BYTES = 4096;
+static_assert(SM_PRF + N * PROOF_SIZE * 32 <= SM_BYTES && SM_DIG + N * 32 <= SM_PRF, "lane small-area layout");
+
+struct Lane {
+    hipStream_t s = nullptr;
+    uint8_t *d_cs = nullptr;     // CS: the chunkset (encode input / repaired output)
+    uint8_t *d_coded = nullptr;  // N*F coded rows (encode output / repair input in rows 0..9)
+    uint8_t *d_small = nullptr;  // SM_BYTES
+    uint8_t *h_big = nullptr;    // N*F page-locked staging (>= CS, >= K*F)
+    uint8_t *h_small = nullptr;  // SM_BYTES page-locked
+    ~Lane() {
+        if (s) (void)hipStreamSynchronize(s);
+        for (uint8_t *p : {d_cs, d_coded, d_small})
+            if (p) (void)hipFree(p);
+        for (uint8_t *p : {h_big, h_small})
+            if (p) (void)hipHostFree(p);
+        if (s) (void)hipStreamDestroy(s);
+    }
+    hipError_t init() {
+        hipError_t e;
+        if ((e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking)) || (e = hipMalloc(reinterpret_cast<void **>(&d_cs), CS)) ||
+            (e = hipMalloc(reinterpret_cast<void **>(&d_coded), N * F)) ||
+            (e = hipMalloc(reinterpret_cast<void **>(&d_small), SM_BYTES)) ||
+            (e = hipHostMalloc(reinterpret_cast<void **>(&h_big), N * F, hipHostMallocDefault)) ||
+            (e = hipHostMalloc(reinterpret_cast<void **>(&h_small), SM_BYTES, hipHostMallocDefault)))
+            return e;
+        return hipSuccess;
+    }
+};
+static_assert(N * F >= CS && N * F >= K * F, "lane staging holds every transfer");
+
 namespace {
 
-// RAII device buffer
-struct DevBuf {
-    uint8_t *p = nullptr;
-    hipError_t alloc(size_t n) { return hipMalloc(reinterpret_cast<void **>(&p), n); }
-    ~DevBuf() {
-        if (p) (void)hipFree(p);
+size_t max_lanes() {
+    static const size_t m = [] {
+        const char *e = std::getenv("DECDS_MAX_LANES");
+        const int v = e ? std::atoi(e) : 16;
+        return (size_t)std::max(1, v);
+    }();
+    return m;
+}
+
+// a free lane of ctx (created on demand up to max_lanes, else wait for one); caller is bound
+int lane_acquire(decds_ctx *ctx, Lane **out) {
+    std::unique_lock<std::mutex> g(ctx->lane_mu);
+    for (;;) {
+        if (!ctx->lanes_free.empty()) {
+            *out = ctx->lanes_free.back();
+            ctx->lanes_free.pop_back();
+            return DECDS_OK;
+        }
+        if (ctx->lanes_all.size() < max_lanes()) break;
+        ctx->lane_cv.wait(g);
+    }
+    ctx->lanes_all.push_back(nullptr);  // reserve the slot while allocating outside the lock
+    g.unlock();
+    Lane *l = new Lane;
+    hipError_t e = l->init();
+    g.lock();
+    auto it = std::find(ctx->lanes_all.begin(), ctx->lanes_all.end(), nullptr);
+    if (e != hipSuccess) {
+        ctx->lanes_all.erase(it);
+        g.unlock();
+        delete l;
+        ctx->lane_cv.notify_one();
+        return decds_hip_error(e, "lane setup (stream, device buffers, pinned staging)");
+    }
+    *it = l;
+    *out = l;
+    return DECDS_OK;
+}
+
+void lane_release(decds_ctx *ctx, Lane *l) {
+    {
+        std::lock_guard<std::mutex> g(ctx->lane_mu);
+        ctx->lanes_free.push_back(l);
+    }
+    ctx->lane_cv.notify_one();
+}
+
+struct LaneGuard {
+    decds_ctx *ctx;
+    Lane *l = nullptr;
+    ~LaneGuard() {
+        if (l) lane_release(ctx, l);
     }
 };
 
@@ -41,8 +129,15 @@ std::mt19937_64 &rng() {
     return g;
 }
 
-
 }  // namespace
+}  // namespace decds
+
+void decds_lanes_destroy(decds_ctx *ctx) {
+    std::lock_guard<std::mutex> g(ctx->lane_mu);
+    for (Lane *l : ctx->lanes_all) delete l;
+    ctx->lanes_all.clear();
+    ctx->lanes_free.clear();
+}
 
 struct decds_chunkset {
     size_t id;
@@ -75,31 +170,34 @@ int decds_chunkset_new(decds_ctx *ctx, size_t chunkset_id, const uint8_t *data, 
     if (!data) return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "null data");
     int s = decds_ctx_bind(ctx);
     if (s) return s;
-    uint8_t cv[N * K];
+    LaneGuard lg{ctx};
+    if ((s = lane_acquire(ctx, &lg.l))) return s;
+    Lane &L = *lg.l;
+    uint8_t *cv = L.h_small + SM_CV;
     if (coeffs) {
-        std::memcpy(cv, coeffs, sizeof cv);
+        std::memcpy(cv, coeffs, N * K);
     } else {
         std::lock_guard<std::mutex> g(g_rng_mu);
-        for (auto &b : cv) b = (uint8_t)rng()();
+        for (size_t i = 0; i < N * K; i++) cv[i] = (uint8_t)rng()();
     }
-    DevBuf dsrc, dcv, ddst, dcommit;
-    constexpr size_t DIG = N * 32, ROOT = 32, PRF = N * PROOF_SIZE * 32;
+    par_memcpy(L.h_big, data, CS);
     hipError_t e;
-    if ((e = dsrc.alloc(CS)) || (e = dcv.alloc(sizeof cv)) || (e = ddst.alloc(N * F)) || (e = dcommit.alloc(DIG + ROOT + PRF)))
-        return decds_hip_error(e, "hipMalloc");
-    if ((e = hipMemcpy(dsrc.p, data, CS, hipMemcpyHostToDevice)) || (e = hipMemcpy(dcv.p, cv, sizeof cv, hipMemcpyHostToDevice)))
-        return decds_hip_error(e, "hipMemcpy H2D");
-    if ((s = decds_encode_batch(ctx, dsrc.p, 1, dcv.p, ddst.p, F, nullptr))) return s;
+    if ((e = hipMemcpyAsync(L.d_cs, L.h_big, CS, hipMemcpyHostToDevice, L.s)) ||
+        (e = hipMemcpyAsync(L.d_small + SM_CV, cv, N * K, hipMemcpyHostToDevice, L.s)))
+        return decds_hip_error(e, "H2D");
+    if ((s = decds_encode_batch(ctx, L.d_cs, 1, L.d_small + SM_CV, L.d_coded, F, L.s))) return s;
     // chunkset.rs:54-63: chunk digests -> 16-leaf Merkle tree -> root + one proof per chunk
-    if ((s = decds_commit_batch(ctx, ddst.p, F, 1, chunkset_id, dcommit.p, dcommit.p + DIG, dcommit.p + DIG + ROOT, nullptr)))
+    if ((s = decds_commit_batch(ctx, L.d_coded, F, 1, chunkset_id, L.d_small + SM_DIG, L.d_small + SM_ROOT,
+                                L.d_small + SM_PRF, L.s)))
         return s;
+    if ((e = hipMemcpyAsync(L.h_big, L.d_coded, N * F, hipMemcpyDeviceToHost, L.s)) ||
+        (e = hipMemcpyAsync(L.h_small + SM_ROOT, L.d_small + SM_ROOT, SM_BYTES - SM_ROOT, hipMemcpyDeviceToHost, L.s)) ||
+        (e = hipStreamSynchronize(L.s)))
+        return decds_hip_error(e, "D2H");
     auto *c = new decds_chunkset{chunkset_id, std::vector<uint8_t>(N * F), {}, {}, {}};
-    if ((e = hipMemcpy(c->coded.data(), ddst.p, N * F, hipMemcpyDeviceToHost)) ||
-        (e = hipMemcpy(c->root, dcommit.p + DIG, ROOT, hipMemcpyDeviceToHost)) ||
-        (e = hipMemcpy(c->proofs, dcommit.p + DIG + ROOT, PRF, hipMemcpyDeviceToHost))) {
-        delete c;
-        return decds_hip_error(e, "hipMemcpy D2H");
-    }
+    par_memcpy(c->coded.data(), L.h_big, N * F);
+    std::memcpy(c->root, L.h_small + SM_ROOT, 32);
+    std::memcpy(c->proofs, L.h_small + SM_PRF, sizeof c->proofs);
     *out = c;
     return DECDS_OK;
 }
@@ -210,27 +308,34 @@ int decds_repairing_chunkset_repair(decds_repairing_chunkset *r, uint8_t *out, s
     // chunkset.rs:201,206
     if (r->rank != K) return decds_set_error(DECDS_ERR_CHUNKSET_NOT_YET_READY, "chunkset %zu is not ready to repair", r->id);
     if (!out || out_len < CS) return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "out buffer < %llu", (unsigned long long)CS);
-    int s = decds_ctx_bind(r->ctx);
+    decds_ctx *ctx = r->ctx;
+    int s = decds_ctx_bind(ctx);
     if (s) return s;
-    DevBuf dcoded, dcand, dplan, dverd, dstat, ddst;
-    hipError_t e;
-    if ((e = dcoded.alloc(N * F)) || (e = dcand.alloc(N)) || (e = dplan.alloc(DECDS_REPAIR_PLAN_BYTES)) ||
-        (e = dverd.alloc(N)) || (e = dstat.alloc(sizeof(int32_t))) || (e = ddst.alloc(CS)))
-        return decds_hip_error(e, "hipMalloc");
-    uint8_t cand[N];
+    LaneGuard lg{ctx};
+    if ((s = lane_acquire(ctx, &lg.l))) return s;
+    Lane &L = *lg.l;
+    // the accepted rows as coded rows 0..9 of one chunkset, arrival order = acceptance order
+    uint8_t *cand = L.h_small + SM_CAND;
     for (uint32_t i = 0; i < N; i++) cand[i] = i < K ? (uint8_t)i : (uint8_t)DECDS_NO_CANDIDATE;
-    if ((e = hipMemcpy(dcoded.p, r->rows.data(), K * F, hipMemcpyHostToDevice)) ||
-        (e = hipMemcpy(dcand.p, cand, N, hipMemcpyHostToDevice)))
-        return decds_hip_error(e, "hipMemcpy H2D");
-    if ((s = decds_repair_batch(r->ctx, dcoded.p, F, 1, dcand.p, dplan.p, reinterpret_cast<int8_t *>(dverd.p), ddst.p,
-                                reinterpret_cast<int32_t *>(dstat.p), nullptr)))
+    par_memcpy(L.h_big, r->rows.data(), K * F);
+    hipError_t e;
+    if ((e = hipMemcpyAsync(L.d_coded, L.h_big, K * F, hipMemcpyHostToDevice, L.s)) ||
+        (e = hipMemcpyAsync(L.d_small + SM_CAND, cand, N, hipMemcpyHostToDevice, L.s)))
+        return decds_hip_error(e, "H2D");
+    if ((s = decds_repair_batch(ctx, L.d_coded, F, 1, L.d_small + SM_CAND, L.d_small + SM_PLAN,
+                                reinterpret_cast<int8_t *>(L.d_small + SM_VERD), L.d_cs,
+                                reinterpret_cast<int32_t *>(L.d_small + SM_STATUS), L.s)))
         return s;
-    int32_t st = 0;
-    if ((e = hipMemcpy(&st, dstat.p, sizeof st, hipMemcpyDeviceToHost)) || (e = hipMemcpy(out, ddst.p, CS, hipMemcpyDeviceToHost)))
-        return decds_hip_error(e, "hipMemcpy D2H");
+    if ((e = hipMemcpyAsync(L.h_big, L.d_cs, CS, hipMemcpyDeviceToHost, L.s)) ||
+        (e = hipMemcpyAsync(L.h_small + SM_STATUS, L.d_small + SM_STATUS, 4, hipMemcpyDeviceToHost, L.s)) ||
+        (e = hipStreamSynchronize(L.s)))
+        return decds_hip_error(e, "D2H");
+    int32_t st;
+    std::memcpy(&st, L.h_small + SM_STATUS, 4);
     if (st != DECDS_OK)
         return decds_set_error(DECDS_ERR_CHUNKSET_REPAIRING_FAILED, "chunkset %zu repairing failed: RLNC Decoding error: %s",
                                r->id, st == DECDS_ERR_CHUNKSET_REPAIRING_FAILED ? "invalid decoded data format" : decds_status_string(st));
+    par_memcpy(out, L.h_big, CS);
     r->repaired = true;  // repair(self) consumes the decoder (chunkset.rs:200)
     r->rows.clear();
     r->rows.shrink_to_fit();
@@ -238,255 +343,5 @@ int decds_repairing_chunkset_repair(decds_repairing_chunkset *r, uint8_t *out, s
 }
 
 void decds_repairing_chunkset_free(decds_repairing_chunkset *r) { delete r; }
-
-// ------------------------------------------------------------------ blob-level batching ------
-// Two streams alternate over batches: while batch b runs its kernel, batch b+1's H2D and batch
-// b-1's D2H proceed on the copy engines. Caller buffers are page-locked with hipHostRegister for
-// the duration of the call so the copies DMA directly from/to them.
-namespace {
-// Page-locks a caller buffer for the duration of one call unless the caller already did
-// (decds_host_register): then registration fails with "already registered" and is left alone.
-struct HostReg {
-    void *p = nullptr;
-    bool ok = false;
-    HostReg(const void *ptr, size_t n) : p(const_cast<void *>(ptr)) {
-        ok = n && hipHostRegister(p, n, hipHostRegisterDefault) == hipSuccess;
-        if (!ok) (void)hipGetLastError();
-    }
-    ~HostReg() {
-        if (ok) (void)hipHostUnregister(p);
-    }
-};
-}  // namespace
-
-// Copy / compute pipeline of the host blob paths: one stream per engine (H2D, kernels, D2H) and
-// SLOTS buffer sets, ordered by events, so the link carries H2D and D2H at the same time (PCIe is
-// full duplex: 53 + 57 GB/s alone, 98 GB/s together, tools/pciebench.py). Round 1's two streams,
-// each H2D -> kernel -> D2H in order, kept one direction busy at a time (60 GB/s in sum).
-constexpr int SLOTS = 3;
-inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
-struct Pipe {
-    hipStream_t h2d = nullptr, comp = nullptr, d2h = nullptr;
-    hipEvent_t in_done[SLOTS] = {}, k_done[SLOTS] = {}, out_done[SLOTS] = {};
-    hipError_t init() {
-        hipError_t e;
-        for (hipStream_t *st : {&h2d, &comp, &d2h})
-            if ((e = hipStreamCreateWithFlags(st, hipStreamNonBlocking))) return e;
-        for (int i = 0; i < SLOTS; i++)
-            for (hipEvent_t *ev : {&in_done[i], &k_done[i], &out_done[i]}) {
-                if ((e = hipEventCreateWithFlags(ev, hipEventDisableTiming))) return e;
-                if ((e = hipEventRecord(*ev, comp))) return e;  // every slot starts free
-            }
-        return hipSuccess;
-    }
-    hipError_t drain() {
-        hipError_t e = hipSuccess, f;
-        for (hipStream_t st : {h2d, comp, d2h})
-            if (st && (f = hipStreamSynchronize(st)) && !e) e = f;
-        return e;
-    }
-    ~Pipe() {
-        (void)drain();
-        for (int i = 0; i < SLOTS; i++)
-            for (hipEvent_t ev : {in_done[i], k_done[i], out_done[i]})
-                if (ev) (void)hipEventDestroy(ev);
-        for (hipStream_t st : {h2d, comp, d2h})
-            if (st) (void)hipStreamDestroy(st);
-    }
-};
-
-int decds_blob_encode_host(decds_ctx *ctx, const uint8_t *blob, size_t blob_len, const uint8_t *coeffs_host,
-                           uint8_t *coded_host, size_t batch) {
-    if (blob_len == 0) return decds_set_error(DECDS_ERR_EMPTY_DATA_FOR_BLOB, "empty data for blob");  // blob.rs:245-247
-    if (!blob || !coeffs_host || !coded_host) return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "null buffer");
-    int s = decds_ctx_bind(ctx);
-    if (s) return s;
-    const size_t n = (blob_len + CS - 1) / CS;  // blob.rs:252
-    if (batch == 0) batch = 16;  // 8-32 measured best
-    batch = std::min(batch, n);
-    HostReg rin(blob, blob_len), rout(coded_host, n * N * F), rcv(coeffs_host, n * N * K);
-    std::lock_guard<std::mutex> lock(ctx->host_mu);
-    uint8_t *din[SLOTS], *dout[SLOTS], *dcv[SLOTS];
-    const size_t sz_in = align256(batch * CS), sz_out = align256(batch * N * F), sz_cv = align256(batch * N * K);
-    uint8_t *base;
-    hipError_t e;
-    if ((e = decds_ctx_scratch(ctx, SLOTS * (sz_in + sz_out + sz_cv), &base))) return decds_hip_error(e, "hipMalloc");
-    for (int i = 0; i < SLOTS; i++, base += sz_in + sz_out + sz_cv) din[i] = base, dout[i] = base + sz_in, dcv[i] = base + sz_in + sz_out;
-    Pipe pp;
-    if ((e = pp.init())) return decds_hip_error(e, "stream/event setup");
-    int rc = DECDS_OK;
-    for (size_t b0 = 0, it = 0; b0 < n && rc == DECDS_OK; b0 += batch, it++) {
-        const int k = (int)(it % SLOTS);
-        const size_t nb = std::min(batch, n - b0);
-        const size_t off = b0 * CS, have = std::min(blob_len - off, nb * CS);
-        // inputs of slot k: free once the slot's previous kernel has read them
-        if ((e = hipStreamWaitEvent(pp.h2d, pp.k_done[k], 0)) ||
-            (e = hipMemcpyAsync(din[k], blob + off, have, hipMemcpyHostToDevice, pp.h2d)) ||
-            (have < nb * CS && (e = hipMemsetAsync(din[k] + have, 0, nb * CS - have, pp.h2d))) ||  // blob.rs:254 zero pad
-            (e = hipMemcpyAsync(dcv[k], coeffs_host + b0 * N * K, nb * N * K, hipMemcpyHostToDevice, pp.h2d)) ||
-            (e = hipEventRecord(pp.in_done[k], pp.h2d))) {
-            rc = decds_hip_error(e, "H2D");
-            break;
-        }
-        // coded rows of slot k: free once the slot's previous D2H has read them
-        if ((e = hipStreamWaitEvent(pp.comp, pp.in_done[k], 0)) || (e = hipStreamWaitEvent(pp.comp, pp.out_done[k], 0))) {
-            rc = decds_hip_error(e, "hipStreamWaitEvent");
-            break;
-        }
-        if ((rc = decds_encode_batch(ctx, din[k], nb, dcv[k], dout[k], F, pp.comp))) break;
-        if ((e = hipEventRecord(pp.k_done[k], pp.comp)) || (e = hipStreamWaitEvent(pp.d2h, pp.k_done[k], 0)) ||
-            (e = hipMemcpyAsync(coded_host + b0 * N * F, dout[k], nb * N * F, hipMemcpyDeviceToHost, pp.d2h)) ||
-            (e = hipEventRecord(pp.out_done[k], pp.d2h))) {
-            rc = decds_hip_error(e, "D2H");
-            break;
-        }
-    }
-    if ((e = pp.drain()) && rc == DECDS_OK) rc = decds_hip_error(e, "hipStreamSynchronize");
-    return rc;
-}
-
-int decds_blob_repair_host(decds_ctx *ctx, const uint8_t *coded_host, size_t n, const uint8_t *cand_host,
-                           size_t blob_len, uint8_t *out, int32_t *status_host, size_t batch) {
-    if (!coded_host || !cand_host || !out || !status_host || n == 0)
-        return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "null buffer or no chunksets");
-    if (blob_len > n * CS || blob_len <= (n - 1) * CS)
-        return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "blob length %zu inconsistent with %zu chunksets", blob_len, n);
-    int s = decds_ctx_bind(ctx);
-    if (s) return s;
-    if (batch == 0) batch = 16;  // 8-32 measured best
-    batch = std::min(batch, n);
-    // RepairingBlob::add_chunk over the arrival order (blob.rs:373-394): the rank test runs on the
-    // 10-byte coding vectors on the host, so only the 10 accepted rows of each chunkset cross PCIe
-    std::vector<uint8_t> sel(n * K, 0);
-    for (size_t c = 0; c < n; c++) {
-        uint8_t basis[K * K], piv[K];
-        uint32_t rank = 0;
-        for (uint32_t a = 0; a < N && rank < K; a++) {
-            const uint8_t row = cand_host[c * N + a];
-            if (row >= N) break;
-            if (decds_rank_push(basis, piv, &rank, coded_host + (c * N + row) * F, ctx->poly)) sel[c * K + rank - 1] = row;
-        }
-        status_host[c] = rank == K ? DECDS_OK : DECDS_ERR_CHUNKSET_NOT_YET_READY;
-    }
-    // per-slot candidate lists and device statuses in page-locked memory: a pageable source or
-    // target would make hipMemcpyAsync a staged copy that blocks this thread until its stream
-    // reaches it, stalling the issue of the next slot
-    struct Pinned {
-        void *p = nullptr;
-        ~Pinned() {
-            if (p) (void)hipHostFree(p);
-        }
-    } pin;
-    {
-        hipError_t pe = hipHostMalloc(&pin.p, SLOTS * batch * (N + sizeof(int32_t)), hipHostMallocDefault);
-        if (pe) return decds_hip_error(pe, "hipHostMalloc");
-    }
-    uint8_t *cand_h[SLOTS];
-    int32_t *stat_h[SLOTS];
-    for (int i = 0; i < SLOTS; i++) {
-        stat_h[i] = reinterpret_cast<int32_t *>(pin.p) + i * batch;
-        cand_h[i] = reinterpret_cast<uint8_t *>(pin.p) + SLOTS * batch * sizeof(int32_t) + i * batch * N;
-    }
-    HostReg rout(out, blob_len), rin(coded_host, n * N * F);
-    std::lock_guard<std::mutex> lock(ctx->host_mu);
-    uint8_t *dcoded[SLOTS], *dcand[SLOTS], *dplan[SLOTS], *dverd[SLOTS], *dstat[SLOTS], *ddst[SLOTS];
-    const size_t sz[6] = {align256(batch * N * F), align256(batch * N), align256(batch * DECDS_REPAIR_PLAN_BYTES),
-                          align256(batch * N), align256(batch * sizeof(int32_t)), align256(batch * CS)};
-    const size_t per = sz[0] + sz[1] + sz[2] + sz[3] + sz[4] + sz[5];
-    uint8_t *base;
-    hipError_t e;
-    if ((e = decds_ctx_scratch(ctx, SLOTS * per, &base))) return decds_hip_error(e, "hipMalloc");
-    for (int i = 0; i < SLOTS; i++) {
-        uint8_t **dst[6] = {&dcoded[i], &dcand[i], &dplan[i], &dverd[i], &dstat[i], &ddst[i]};
-        for (int j = 0; j < 6; j++) *dst[j] = base, base += sz[j];
-    }
-    Pipe pp;
-    if ((e = pp.init())) return decds_hip_error(e, "stream/event setup");
-    int rc = DECDS_OK;
-    size_t pending_b0[SLOTS], pending_nb[SLOTS] = {};
-    for (int i = 0; i < SLOTS; i++) pending_b0[i] = (size_t)-1;
-    // host side of slot k once its D2H is done: device statuses, zeroed output of unrepaired chunksets
-    auto finish = [&](int k) -> int {
-        if (pending_b0[k] == (size_t)-1) return DECDS_OK;
-        hipError_t ee = hipEventSynchronize(pp.out_done[k]);
-        if (ee) return decds_hip_error(ee, "hipEventSynchronize");
-        for (size_t c = 0; c < pending_nb[k]; c++) {
-            const size_t cs = pending_b0[k] + c;
-            int32_t &hs = status_host[cs];
-            if (hs == DECDS_OK && stat_h[k][c] != DECDS_OK) hs = DECDS_ERR_CHUNKSET_REPAIRING_FAILED;
-            if (hs != DECDS_OK) {  // no data for a chunkset that could not be repaired
-                const size_t off = cs * CS;
-                std::memset(out + off, 0, std::min(blob_len - off, (size_t)CS));
-            }
-        }
-        pending_b0[k] = (size_t)-1;
-        return DECDS_OK;
-    };
-    for (size_t b0 = 0, it = 0; b0 < n && rc == DECDS_OK; b0 += batch, it++) {
-        const int k = (int)(it % SLOTS);
-        if ((rc = finish(k))) break;  // slot k's previous batch fully done: all its buffers are free
-        const size_t nb = std::min(batch, n - b0);
-        // the accepted rows keep their own row slots on the device (slot layout = host layout less
-        // b0 chunksets), so runs of consecutive accepted rows — across chunkset boundaries too —
-        // cross the link as one copy each instead of one copy per row
-        std::vector<uint8_t> take(nb * N, 0);
-        for (size_t c = 0; c < nb; c++) {
-            const bool ready = status_host[b0 + c] == DECDS_OK;
-            for (uint32_t a = 0; a < N; a++)
-                cand_h[k][c * N + a] = ready && a < K ? sel[(b0 + c) * K + a] : (uint8_t)DECDS_NO_CANDIDATE;
-            if (ready)
-                for (uint32_t a = 0; a < K; a++) take[c * N + sel[(b0 + c) * K + a]] = 1;
-        }
-        for (size_t r0 = 0; r0 < nb * N && rc == DECDS_OK;) {
-            if (!take[r0]) {
-                r0++;
-                continue;
-            }
-            size_t r1 = r0 + 1;
-            while (r1 < nb * N && take[r1]) r1++;
-            if ((e = hipMemcpyAsync(dcoded[k] + r0 * F, coded_host + (b0 * N + r0) * F, (r1 - r0) * F,
-                                    hipMemcpyHostToDevice, pp.h2d)))
-                rc = decds_hip_error(e, "H2D");
-            r0 = r1;
-        }
-        if (rc) break;
-        if ((e = hipMemcpyAsync(dcand[k], cand_h[k], nb * N, hipMemcpyHostToDevice, pp.h2d)) ||
-            (e = hipEventRecord(pp.in_done[k], pp.h2d)) || (e = hipStreamWaitEvent(pp.comp, pp.in_done[k], 0))) {
-            rc = decds_hip_error(e, "H2D");
-            break;
-        }
-        if ((rc = decds_repair_batch(ctx, dcoded[k], F, nb, dcand[k], dplan[k], reinterpret_cast<int8_t *>(dverd[k]),
-                                     ddst[k], reinterpret_cast<int32_t *>(dstat[k]), pp.comp)))
-            break;
-        // blob.rs:464: truncate the last chunkset to its real size
-        const size_t off = b0 * CS, keep = std::min(blob_len - off, nb * CS);
-        if ((e = hipEventRecord(pp.k_done[k], pp.comp)) || (e = hipStreamWaitEvent(pp.d2h, pp.k_done[k], 0)) ||
-            (e = hipMemcpyAsync(stat_h[k], dstat[k], nb * sizeof(int32_t), hipMemcpyDeviceToHost, pp.d2h)) ||
-            (e = hipMemcpyAsync(out + off, ddst[k], keep, hipMemcpyDeviceToHost, pp.d2h)) ||
-            (e = hipEventRecord(pp.out_done[k], pp.d2h))) {
-            rc = decds_hip_error(e, "D2H");
-            break;
-        }
-        pending_b0[k] = b0;
-        pending_nb[k] = nb;
-    }
-    for (size_t j = 0; j < SLOTS; j++) {  // oldest pending slot first
-        int r2 = finish((int)(j % SLOTS));
-        if (r2 && rc == DECDS_OK) rc = r2;
-    }
-    if ((e = pp.drain()) && rc == DECDS_OK) rc = decds_hip_error(e, "hipStreamSynchronize");
-    return rc;
-}
-
-int decds_host_register(const void *ptr, size_t len) {
-    if (!ptr || !len) return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "null or empty buffer");
-    hipError_t e = hipHostRegister(const_cast<void *>(ptr), len, hipHostRegisterDefault);
-    return e == hipSuccess ? DECDS_OK : decds_hip_error(e, "hipHostRegister");
-}
-
-int decds_host_unregister(const void *ptr) {
-    hipError_t e = hipHostUnregister(const_cast<void *>(ptr));
-    return e == hipSuccess ? DECDS_OK : decds_hip_error(e, "hipHostUnregister");
-}
 
 }  // extern "C"

@@ -1,0 +1,340 @@
+// host_mem.cpp — registry of page-locked host ranges (decds_host_register / decds_host_alloc),
+// the host thread pool for staging copies, and the pinned bounce rings (host_mem.h).
+#include "host_mem.h"
+
+#include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <cstdlib>
+#include <cstring>
+#include <deque>
+#include <map>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "../../include/decds_rlnc.h"
+#include "capi_internal.h"
+
+namespace decds {
+
+namespace {
+
+// ---- registry ---------------------------------------------------------------------------------
+// A range stays page-locked while it has a registration (regs) or an in-flight use (uses); the last
+// of the two to drop it unlocks it. Ranges never overlap (a partial overlap is refused: locking the
+// same pages twice and unlocking one of them is exactly the hazard this replaces).
+struct Entry {
+    size_t len;
+    int regs;
+    int uses;
+    bool alloc;  // from decds_host_alloc (hipHostMalloc): freed, not unregistered
+};
+std::mutex g_reg_mu;
+std::map<uintptr_t, Entry> g_reg;
+
+// caller holds g_reg_mu
+void finalize_if_idle(std::map<uintptr_t, Entry>::iterator it) {
+    if (it->second.regs > 0 || it->second.uses > 0) return;
+    void *p = reinterpret_cast<void *>(it->first);
+    if (it->second.alloc)
+        (void)hipHostFree(p);
+    else
+        (void)hipHostUnregister(p);
+    g_reg.erase(it);
+}
+
+// entry whose range contains [p, p+n), or end()
+std::map<uintptr_t, Entry>::iterator find_containing(uintptr_t p, size_t n) {
+    auto it = g_reg.upper_bound(p);
+    if (it == g_reg.begin()) return g_reg.end();
+    --it;
+    if (p + n <= it->first + it->second.len) return it;
+    return g_reg.end();
+}
+
+bool overlaps(uintptr_t p, size_t n) {
+    auto it = g_reg.upper_bound(p);
+    if (it != g_reg.end() && it->first < p + n) return true;
+    if (it != g_reg.begin()) {
+        --it;
+        if (it->first + it->second.len > p) return true;
+    }
+    return false;
+}
+
+// ---- host pool --------------------------------------------------------------------------------
+class Pool {
+   public:
+    static Pool &get() {
+        static Pool p;
+        return p;
+    }
+    void run(size_t n, const std::function<void(size_t)> &fn) {
+        if (n == 0) return;
+        if (n == 1 || workers_.empty()) {
+            for (size_t i = 0; i < n; i++) fn(i);
+            return;
+        }
+        Job job{&fn, n};
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            jobs_.push_back(&job);
+        }
+        cv_.notify_all();
+        work(job);
+        std::unique_lock<std::mutex> g(mu_);
+        auto it = std::find(jobs_.begin(), jobs_.end(), &job);
+        if (it != jobs_.end()) jobs_.erase(it);
+        done_cv_.wait(g, [&] { return job.finished.load() == n && job.attached == 0; });
+    }
+    ~Pool() {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto &t : workers_) t.join();
+    }
+
+   private:
+    struct Job {
+        const std::function<void(size_t)> *fn;
+        size_t n;
+        std::atomic<size_t> next{0};
+        std::atomic<size_t> finished{0};
+        int attached = 0;  // workers holding a pointer to the job (under mu_)
+    };
+    Pool() {
+        unsigned t = std::thread::hardware_concurrency();
+        t = t ? std::min(8u, t) : 4u;
+        if (const char *e = std::getenv("DECDS_HOST_THREADS")) t = (unsigned)std::max(1, std::atoi(e));
+        for (unsigned i = 1; i < t; i++) workers_.emplace_back([this] { loop(); });
+    }
+    void work(Job &j) {
+        for (size_t i; (i = j.next.fetch_add(1)) < j.n;) {
+            (*j.fn)(i);
+            j.finished.fetch_add(1);
+        }
+    }
+    void loop() {
+        std::unique_lock<std::mutex> g(mu_);
+        for (;;) {
+            cv_.wait(g, [&] { return stop_ || !jobs_.empty(); });
+            if (stop_) return;
+            Job *j = jobs_.front();
+            if (j->next.load() >= j->n) {  // fully handed out: drop it from the queue
+                jobs_.pop_front();
+                continue;
+            }
+            j->attached++;
+            g.unlock();
+            work(*j);
+            g.lock();
+            j->attached--;
+            done_cv_.notify_all();
+        }
+    }
+    std::vector<std::thread> workers_;
+    std::mutex mu_;
+    std::condition_variable cv_, done_cv_;
+    std::deque<Job *> jobs_;
+    bool stop_ = false;
+};
+
+}  // namespace
+
+HostUse::HostUse(const void *p, size_t n) {
+    if (!p || !n) return;
+    std::lock_guard<std::mutex> g(g_reg_mu);
+    auto it = find_containing(reinterpret_cast<uintptr_t>(p), n);
+    if (it == g_reg.end() || it->second.regs == 0) return;
+    it->second.uses++;
+    key_ = it->first;
+}
+
+HostUse::~HostUse() {
+    if (!key_) return;
+    std::lock_guard<std::mutex> g(g_reg_mu);
+    auto it = g_reg.find(key_);
+    if (it == g_reg.end()) return;
+    it->second.uses--;
+    finalize_if_idle(it);
+}
+
+void host_parallel(size_t n, const std::function<void(size_t)> &fn) { Pool::get().run(n, fn); }
+
+void par_memcpy(void *dst, const void *src, size_t n) {
+    constexpr size_t PART = (size_t)2 << 20;
+    if (n < 2 * PART) {
+        std::memcpy(dst, src, n);
+        return;
+    }
+    const size_t parts = std::min<size_t>(16, n / PART);
+    const size_t step = (n / parts + 63) & ~(size_t)63;
+    host_parallel(parts, [&](size_t i) {
+        const size_t lo = i * step;
+        if (lo >= n) return;
+        std::memcpy(static_cast<uint8_t *>(dst) + lo, static_cast<const uint8_t *>(src) + lo, std::min(step, n - lo));
+    });
+}
+
+// ---- bounce rings -----------------------------------------------------------------------------
+hipError_t BounceRing::init() {
+    for (int i = 0; i < R; i++) {
+        hipError_t e;
+        if (!buf[i] && (e = hipHostMalloc(reinterpret_cast<void **>(&buf[i]), PIECE, hipHostMallocDefault))) return e;
+        if (!ev[i] && (e = hipEventCreateWithFlags(&ev[i], hipEventDisableTiming))) return e;
+    }
+    return hipSuccess;
+}
+
+hipError_t BounceRing::settle(int i) {
+    if (used[i]) {
+        hipError_t e = hipEventSynchronize(ev[i]);
+        if (e) return e;
+        used[i] = false;
+    }
+    if (pend_dst[i]) {
+        par_memcpy(pend_dst[i], buf[i], pend_len[i]);
+        pend_dst[i] = nullptr;
+    }
+    return hipSuccess;
+}
+
+hipError_t BounceRing::h2d(uint8_t *ddst, const uint8_t *hsrc, size_t n, hipStream_t s) {
+    hipError_t e;
+    if ((e = init())) return e;
+    for (size_t o = 0; o < n; o += PIECE) {
+        const int i = next;
+        next = (next + 1) % R;
+        if ((e = settle(i))) return e;
+        const size_t len = std::min(PIECE, n - o);
+        par_memcpy(buf[i], hsrc + o, len);
+        if ((e = hipMemcpyAsync(ddst + o, buf[i], len, hipMemcpyHostToDevice, s)) || (e = hipEventRecord(ev[i], s)))
+            return e;
+        used[i] = true;
+    }
+    return hipSuccess;
+}
+
+hipError_t BounceRing::d2h(uint8_t *hdst, const uint8_t *dsrc, size_t n, hipStream_t s) {
+    hipError_t e;
+    if ((e = init())) return e;
+    for (size_t o = 0; o < n; o += PIECE) {
+        const int i = next;
+        next = (next + 1) % R;
+        if ((e = settle(i))) return e;
+        const size_t len = std::min(PIECE, n - o);
+        if ((e = hipMemcpyAsync(buf[i], dsrc + o, len, hipMemcpyDeviceToHost, s)) || (e = hipEventRecord(ev[i], s)))
+            return e;
+        used[i] = true;
+        pend_dst[i] = hdst + o;
+        pend_len[i] = len;
+    }
+    return hipSuccess;
+}
+
+hipError_t BounceRing::flush() {
+    for (int k = 0; k < R; k++) {  // oldest piece first
+        hipError_t e = settle((next + k) % R);
+        if (e) return e;
+    }
+    return hipSuccess;
+}
+
+void BounceRing::abandon() {
+    for (int i = 0; i < R; i++) {
+        pend_dst[i] = nullptr;  // an abandoned call's copy-outs are dropped, never written late
+        if (used[i]) (void)hipEventSynchronize(ev[i]);
+        used[i] = false;
+    }
+}
+
+BounceRing::~BounceRing() {
+    abandon();
+    for (int i = 0; i < R; i++) {
+        if (ev[i]) (void)hipEventDestroy(ev[i]);
+        if (buf[i]) (void)hipHostFree(buf[i]);
+    }
+}
+
+hipError_t copy_h2d(uint8_t *d, const uint8_t *h, size_t n, bool pinned, BounceRing &ring, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    return pinned ? hipMemcpyAsync(d, h, n, hipMemcpyHostToDevice, s) : ring.h2d(d, h, n, s);
+}
+
+hipError_t copy_d2h(uint8_t *h, const uint8_t *d, size_t n, bool pinned, BounceRing &ring, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    return pinned ? hipMemcpyAsync(h, d, n, hipMemcpyDeviceToHost, s) : ring.d2h(h, d, n, s);
+}
+
+}  // namespace decds
+
+using namespace decds;
+
+extern "C" {
+
+int decds_host_register(const void *ptr, size_t len) {
+    if (!ptr || !len) return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "null or empty buffer");
+    const uintptr_t p = reinterpret_cast<uintptr_t>(ptr);
+    std::lock_guard<std::mutex> g(g_reg_mu);
+    auto it = g_reg.find(p);
+    if (it != g_reg.end() && it->second.len == len && !it->second.alloc) {
+        it->second.regs++;  // the same range again: one more registration to undo
+        return DECDS_OK;
+    }
+    if (overlaps(p, len))
+        return decds_set_error(DECDS_ERR_INVALID_ARGUMENT,
+                               "range [%p, +%zu) overlaps a range already registered with this library", ptr, len);
+    hipError_t e = hipHostRegister(const_cast<void *>(ptr), len, hipHostRegisterDefault);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();  // the failed call's own error, reported below
+        return decds_hip_error(e, "hipHostRegister");
+    }
+    g_reg.emplace(p, Entry{len, 1, 0, false});
+    return DECDS_OK;
+}
+
+int decds_host_unregister(const void *ptr) {
+    std::lock_guard<std::mutex> g(g_reg_mu);
+    auto it = g_reg.find(reinterpret_cast<uintptr_t>(ptr));
+    if (it == g_reg.end() || it->second.alloc || it->second.regs == 0)
+        return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "%p was not registered with decds_host_register", ptr);
+    it->second.regs--;
+    finalize_if_idle(it);  // deferred while a call still uses the range
+    return DECDS_OK;
+}
+
+int decds_host_alloc(size_t len, void **out) {
+    if (!out || !len) return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "null out pointer or empty size");
+    *out = nullptr;
+    void *p = nullptr;
+    hipError_t e = hipHostMalloc(&p, len, hipHostMallocDefault);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        return decds_hip_error(e, "hipHostMalloc");
+    }
+    std::lock_guard<std::mutex> g(g_reg_mu);
+    g_reg.emplace(reinterpret_cast<uintptr_t>(p), Entry{len, 1, 0, true});
+    *out = p;
+    return DECDS_OK;
+}
+
+int decds_host_free(void *ptr) {
+    std::lock_guard<std::mutex> g(g_reg_mu);
+    auto it = g_reg.find(reinterpret_cast<uintptr_t>(ptr));
+    if (it == g_reg.end() || !it->second.alloc || it->second.regs == 0)
+        return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "%p was not allocated with decds_host_alloc", ptr);
+    it->second.regs--;
+    finalize_if_idle(it);
+    return DECDS_OK;
+}
+
+int decds_host_is_registered(const void *ptr, size_t len) {
+    std::lock_guard<std::mutex> g(g_reg_mu);
+    auto it = find_containing(reinterpret_cast<uintptr_t>(ptr), len ? len : 1);
+    return it != g_reg.end() && it->second.regs > 0;
+}
+
+}  // extern "C"

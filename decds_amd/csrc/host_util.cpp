@@ -2,6 +2,7 @@
 // vectors (rlnc Decoder's "piece useful?" test, chunkset.rs:181-183) and the seeded byte stream.
 // These never touch chunk payloads; the payload arithmetic runs only in rlnc_kernels.hip.
 #include <cstring>
+#include <utility>
 
 #include "../../include/decds_rlnc.h"
 #include "capi_internal.h"
@@ -42,6 +43,29 @@ uint32_t host_gf_generator(uint32_t poly) {
         if (pw(255) == 1 && pw(85) != 1 && pw(51) != 1 && pw(15) != 1) return g;
     }
     return 0;
+}
+
+bool host_gf_invert(const uint8_t *m, uint8_t *inv, uint32_t poly) {
+    uint8_t a[K][2 * K];
+    for (uint32_t i = 0; i < K; i++)
+        for (uint32_t j = 0; j < K; j++) a[i][j] = m[i * K + j], a[i][K + j] = i == j;
+    for (uint32_t c = 0; c < K; c++) {
+        uint32_t p = c;
+        while (p < K && !a[p][c]) p++;
+        if (p == K) return false;
+        if (p != c)
+            for (uint32_t j = 0; j < 2 * K; j++) std::swap(a[p][j], a[c][j]);
+        const uint8_t f = host_gf_inv(a[c][c], poly);
+        for (uint32_t j = 0; j < 2 * K; j++) a[c][j] = host_gf_mul(a[c][j], f, poly);
+        for (uint32_t r = 0; r < K; r++)
+            if (r != c && a[r][c]) {
+                const uint8_t g = a[r][c];
+                for (uint32_t j = 0; j < 2 * K; j++) a[r][j] ^= host_gf_mul(g, a[c][j], poly);
+            }
+    }
+    for (uint32_t i = 0; i < K; i++)
+        for (uint32_t j = 0; j < K; j++) inv[i * K + j] = a[i][K + j];
+    return true;
 }
 
 }  // namespace decds

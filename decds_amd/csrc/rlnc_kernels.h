@@ -7,9 +7,7 @@
 namespace decds {
 
 struct LaunchGeom {
-    int num_cus;          // CUs on the device (256 on MI355X)
-    int wgs_per_cu = 2;   // resident streaming workgroups per CU (2 x 80 KiB LDS = all of it);
-                          // 1 leaves half the CU for a concurrent kernel (DECDS_WGS_PER_CU=1)
+    int num_cus;  // CUs on the device (256 on MI355X)
 };
 
 hipError_t launch_encode(const LaunchGeom &g, const uint8_t *src, size_t n, const uint8_t *coeffs,
@@ -18,9 +16,11 @@ hipError_t launch_encode(const LaunchGeom &g, const uint8_t *src, size_t n, cons
 hipError_t launch_repair_plan(const uint8_t *coded, size_t pitch, size_t n, const uint8_t *cand,
                               uint8_t *plan, int8_t *verdicts, int32_t *status, uint32_t poly,
                               uint32_t gen, hipStream_t stream);
+// in_bases / out_bases (device arrays of n addresses, or NULL): the gather form — chunkset c's
+// accepted rows at in_bases[c] + plan.sel[k]*pitch, its output at out_bases[c]
 hipError_t launch_decode(const LaunchGeom &g, const uint8_t *coded, size_t pitch, size_t n,
-                         const uint8_t *plan, uint8_t *dst, int32_t *status, uint32_t poly,
-                         uint32_t marker, hipStream_t stream);
+                         const uint8_t *plan, uint8_t *dst, int32_t *status, const uint64_t *in_bases,
+                         const uint64_t *out_bases, uint32_t poly, uint32_t marker, hipStream_t stream);
 hipError_t launch_fill_random(uint64_t seed, uint64_t byte_offset, uint8_t *dst, size_t nbytes,
                               hipStream_t stream);
 hipError_t configure_kernels();  // raise the dynamic-LDS limit once per process

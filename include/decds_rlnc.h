@@ -12,8 +12,11 @@
  * caller memory. A context owns only its device selection, field parameters and error text.
  *
  * Pointer kinds: *_batch functions take DEVICE pointers (hipMalloc'd or torch CUDA storage) and
- * are asynchronous on `stream`; decds_chunkset_* / decds_repairing_chunkset_* / decds_blob_*_host
- * take HOST pointers and are synchronous.
+ * are asynchronous on `stream`; decds_chunkset_* / decds_repairing_chunkset_* / decds_blob_* /
+ * decds_repairing_blob_* take HOST pointers and are synchronous. The library never page-locks
+ * caller memory behind the caller's back: host buffers inside a range registered with
+ * decds_host_register or allocated with decds_host_alloc are DMA'd directly, any other host memory
+ * is staged through the context's own page-locked buffers (correct, slower).
  *
  * Status codes map 1:1 onto decds-lib/src/errors.rs (DecdsError); negative codes are runtime
  * failures that the Rust side surfaces as ChunksetRepairingFailed — there is never a silent CPU
@@ -71,6 +74,9 @@ int decds_ctx_get_field(const decds_ctx *ctx, uint32_t *poly, uint8_t *marker);
 const char *decds_status_string(int status);
 const char *decds_last_error(void); /* thread-local text of the last failure */
 int decds_device_count(void);
+/* Waits for the context's device and reports a pending (sticky) device fault as DECDS_ERR_HIP, so a
+ * fault is attributed to the work that caused it, not to the next call that happens to sync. */
+int decds_device_status(const decds_ctx *ctx);
 
 /* ---- batch codec over device-resident chunksets (the hot path) ---------------------------- */
 /* Replaces ChunkSet::new's RLNC part for a batch of chunksets: Encoder::new(data, 10)
@@ -170,21 +176,82 @@ int decds_repairing_chunkset_is_ready_to_repair(const decds_repairing_chunkset *
 int decds_repairing_chunkset_repair(decds_repairing_chunkset *rcs, uint8_t *out, size_t out_len);
 void decds_repairing_chunkset_free(decds_repairing_chunkset *rcs);
 
-/* ---- blob-level batching (decds-lib/src/blob.rs), host buffers, pinned-staged -------------- */
+/* ---- blob-level batching (decds-lib/src/blob.rs), host buffers ----------------------------- */
 /* Blob::new's chunkset loop (blob.rs:252-264): zero-pads blob to n = ceil(len/CS) chunksets and
  * encodes them in device batches of `batch` chunksets (0 = 16; 8-32 measured best) with H2D,
  * kernels and D2H on one stream each over three slots, so PCIe carries both directions at once;
- * the slot buffers stay in ctx across calls (calls on one ctx are serialised). Page-lock the
- * caller buffers once (decds_host_register) for the full rate. coded_host: n*16 rows of
- * 1,048,587 bytes. coeffs_host: n x 16 x 10. */
+ * the slot buffers stay in ctx across calls (calls on one ctx are serialised). Register the
+ * caller buffers once (decds_host_register, or allocate them with decds_host_alloc) for the full
+ * rate. coded_host: n*16 rows of 1,048,587 bytes. coeffs_host: n x 16 x 10. */
 int decds_blob_encode_host(decds_ctx *ctx, const uint8_t *blob, size_t blob_len,
                            const uint8_t *coeffs_host, uint8_t *coded_host, size_t batch);
 /* RepairingBlob add_chunk/get_repaired_chunkset over all chunksets (blob.rs:373-394, 451-473):
  * coded_host: n*16 rows; cand_host: n x 16 arrival order; out: blob_len bytes (last chunkset
- * truncated as blob.rs:464); status_host: n per-chunkset status. */
+ * truncated as blob.rs:464; chunksets that cannot be repaired are zero-filled); status_host: n
+ * per-chunkset status. */
 int decds_blob_repair_host(decds_ctx *ctx, const uint8_t *coded_host, size_t n_chunksets,
                            const uint8_t *cand_host, size_t blob_len, uint8_t *out,
                            int32_t *status_host, size_t batch);
+/* The same over n_ctx contexts (devices): chunksets sharded by contiguous index range, one host
+ * thread and stream set per context, no collective (chunksets are independent, blob.rs:256-264).
+ * Identical output to the single-context calls. */
+int decds_blob_encode_host_multi(decds_ctx *const *ctxs, size_t n_ctx, const uint8_t *blob, size_t blob_len,
+                                 const uint8_t *coeffs_host, uint8_t *coded_host, size_t batch);
+int decds_blob_repair_host_multi(decds_ctx *const *ctxs, size_t n_ctx, const uint8_t *coded_host,
+                                 size_t n_chunksets, const uint8_t *cand_host, size_t blob_len, uint8_t *out,
+                                 int32_t *status_host, size_t batch);
+
+/* ---- Blob (blob.rs:227-318) ------------------------------------------------------------------ */
+typedef struct decds_blob decds_blob;
+/* Blob::new(data) (blob.rs:244-285): empty -> DECDS_ERR_EMPTY_DATA_FOR_BLOB; whole-blob BLAKE3
+ * digest (host threads); every chunkset RLNC-encoded with its commitment (digests, root, proofs) on
+ * the devices of ctxs (sharded as the _multi calls); blob-level Merkle tree over the chunkset roots
+ * with each chunk's blob-level path appended to its proof. coeffs: n x 16 x 10 or NULL (drawn from
+ * the library's RNG, as the reference draws from rand::rng()). */
+int decds_blob_new(decds_ctx *const *ctxs, size_t n_ctx, const uint8_t *data, size_t len, const uint8_t *coeffs,
+                   decds_blob **out);
+/* Blob::get_blob_header (blob.rs:288-290): BlobHeader fields; *chunkset_roots points into the blob */
+int decds_blob_get_header(const decds_blob *blob, uint64_t *byte_length, uint64_t *num_chunksets, uint8_t *digest,
+                          uint8_t *root, const uint8_t **chunkset_roots);
+/* hashes in every chunk's proof: 4 chunkset-level + ceil(log2(num_chunksets)) blob-level */
+size_t decds_blob_proof_len(const decds_blob *blob);
+/* chunk (chunkset_id, share_id) of the blob: *data -> its 1,048,587 coded bytes (inside the blob),
+ * proof <- decds_blob_proof_len hashes; share_id >= 16 -> DECDS_ERR_INVALID_SHARE_ID */
+int decds_blob_get_chunk(const decds_blob *blob, size_t chunkset_id, size_t share_id, const uint8_t **data,
+                         uint8_t *proof, size_t proof_cap);
+/* Blob::get_share (blob.rs:306-317): share share_id of every chunkset, data n x 1,048,587 bytes,
+ * proofs n x proof_len x 32; share_id >= 16 -> DECDS_ERR_INVALID_SHARE_ID */
+int decds_blob_get_share(const decds_blob *blob, size_t share_id, uint8_t *data, size_t data_cap, uint8_t *proofs,
+                         size_t proofs_cap);
+void decds_blob_free(decds_blob *blob);
+
+/* ---- RepairingBlob (blob.rs:321-473) ---------------------------------------------------------- */
+typedef struct decds_repairing_blob decds_repairing_blob;
+/* RepairingBlob::new(header) (blob.rs:341-353) from the BlobHeader fields it uses */
+int decds_repairing_blob_new(decds_ctx *ctx, uint64_t byte_length, uint64_t num_chunksets, const uint8_t *root,
+                             const uint8_t *chunkset_roots, decds_repairing_blob **out);
+/* RepairingBlob::add_chunk (blob.rs:373-394), in the reference's order: chunkset id out of range ->
+ * DECDS_ERR_INVALID_CHUNKSET_ID; chunkset already repaired -> DECDS_ERR_CHUNKSET_ALREADY_REPAIRED;
+ * BlobHeader::validate_chunk fails -> DECDS_ERR_INVALID_PROOF_IN_CHUNK; chunkset ready ->
+ * DECDS_ERR_CHUNKSET_READY_TO_REPAIR; then add_chunk_unvalidated (a piece that does not raise the
+ * rank -> DECDS_ERR_CHUNK_DECODING_FAILED). Accepted rows are kept on the device. */
+int decds_repairing_blob_add_chunk(decds_repairing_blob *rb, uint64_t chunkset_id, uint64_t chunk_id,
+                                   const uint8_t *data, size_t len, const uint8_t *proof, size_t proof_len);
+/* add_chunk for n_rows chunks in arrival order, validated as one device batch: ids n x (chunkset_id,
+ * chunk_id), rows n x 1,048,587, proofs n x proof_len x 32; status[i] = what the i-th add_chunk call
+ * would have returned. */
+int decds_repairing_blob_add_chunks(decds_repairing_blob *rb, size_t n_rows, const uint64_t *ids, const uint8_t *rows,
+                                    const uint8_t *proofs, size_t proof_len, int32_t *status);
+/* RepairingBlob::is_chunkset_ready_to_repair / is_chunkset_already_repaired (blob.rs:407-430) */
+int decds_repairing_blob_is_chunkset_ready_to_repair(const decds_repairing_blob *rb, size_t chunkset_id, int *out);
+int decds_repairing_blob_is_chunkset_already_repaired(const decds_repairing_blob *rb, size_t chunkset_id, int *out);
+/* RepairingBlob::get_repaired_chunkset (blob.rs:451-473): out receives get_chunkset_size(id) bytes
+ * (*out_len); the chunkset is consumed (also when its repair fails, as blob.rs:458-462). Ready
+ * chunksets are decoded in device batches: the first call decodes up to 64 ready chunksets at once
+ * and later calls for those only copy out. */
+int decds_repairing_blob_get_repaired_chunkset(decds_repairing_blob *rb, size_t chunkset_id, uint8_t *out,
+                                               size_t out_cap, size_t *out_len);
+void decds_repairing_blob_free(decds_repairing_blob *rb);
 
 /* ---- commitment layer (next row: chunk digests + Merkle trees) ------------ */
 /* ChunkSet::new's commitment for a batch (chunkset.rs:54-63): for coded row r = c*16+j,
@@ -244,10 +311,17 @@ int decds_blob_header_from_bytes(const uint8_t *bytes, size_t len, uint64_t *byt
  * split over up to nthreads host threads (same result as decds_blake3) */
 void decds_blake3_parallel(const uint8_t *data, size_t len, uint8_t out[32], int nthreads);
 
-/* Page-lock a caller buffer once for many host-path calls (otherwise each call pins and unpins
- * its buffers itself). Pair with decds_host_unregister before freeing the buffer. */
+/* Page-lock a caller buffer once for many host calls (unregistered memory is staged through the
+ * context's page-locked buffers instead). Registrations are refcounted per exact range; a range
+ * that partially overlaps a registered one is refused; an unregister while a call still uses the
+ * range takes effect when that call returns. Pair with decds_host_unregister before freeing. */
 int decds_host_register(const void *ptr, size_t len);
 int decds_host_unregister(const void *ptr);
+/* page-locked host memory the host paths DMA directly (hipHostMalloc + the same registry) */
+int decds_host_alloc(size_t len, void **out);
+int decds_host_free(void *ptr);
+/* 1 if [ptr, ptr+len) lies inside one registered or allocated range, else 0 */
+int decds_host_is_registered(const void *ptr, size_t len);
 
 #ifdef __cplusplus
 }

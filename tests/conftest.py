@@ -23,3 +23,16 @@ def kat():
 def ctx():
     import decds_amd
     return decds_amd.Context(0)
+
+
+@pytest.fixture(autouse=True)
+def _device_status_after_gpu_test(request):
+    """After every -m gpu test: wait for the device and fail THIS test if it left a device fault
+    (a sticky error would otherwise surface in whichever later test syncs first, GPUTEST_r01)."""
+    yield
+    if request.node.get_closest_marker("gpu") is None:
+        return
+    import torch
+    from decds_amd._capi import check, lib
+    torch.cuda.synchronize()
+    check(lib().decds_device_status(request.getfixturevalue("ctx").handle))

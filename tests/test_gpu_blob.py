@@ -1,0 +1,184 @@
+"""GPU parity of the Blob / RepairingBlob mirror (decds-lib/src/blob.rs:227-473) against oracle/:
+Blob::new's coded bytes, commitments, blob-level tree and get_share; RepairingBlob's incremental
+add_chunk / get_repaired_chunkset with every error branch, the reference's own tests
+(blob.rs:700-837) and the all-chunks shuffle round trip (tests.rs:4-57), and the batched add_chunks
+against sequential add_chunk calls."""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+import decds_amd  # noqa: E402
+from decds_amd import BlobHeader, DecdsError  # noqa: E402
+from decds_amd._capi import CHUNKSET_BYTES as CS, CODED_PIECE_BYTES as F, K, N  # noqa: E402
+import oracle as o  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+
+def _blob(ctx, blob_len, seed):
+    data = o.fill_random(seed, blob_len)
+    n = -(-blob_len // CS)
+    coeffs = o.fill_random(seed + 1, n * N * K)
+    return data, coeffs, decds_amd.Blob(ctx, data, coeffs)
+
+
+def _all_chunks(blob):
+    return [c for j in range(N) for c in blob.get_share(j)]  # the reference's order (blob.rs:710-712)
+
+
+def _raises(kind, fn, *a):
+    with pytest.raises(DecdsError) as e:
+        fn(*a)
+    assert e.value.kind == kind, e.value
+    return e.value
+
+
+def test_blob_new_matches_oracle(ctx):
+    blob_len = 2 * CS + CS // 2
+    data, coeffs, blob = _blob(ctx, blob_len, 0x1B10)
+    n = 3
+    coded = o.blob_encode(data, coeffs, nthreads=8)
+    h = blob.get_blob_header()
+    assert (h.get_blob_size(), h.get_num_chunksets()) == (blob_len, n)
+    assert h.get_blob_digest() == o.blake3(data)                                     # blob.rs:249
+    leaves = [[o.chunk_digest(c, c * N + j, coded[c * N + j]) for j in range(N)] for c in range(n)]
+    roots = [o.merkle(lv)[0] for lv in leaves]
+    assert h.chunkset_root_commitments == roots                                    # chunkset.rs:54-57
+    broot, bproofs = o.merkle(roots)                                                # blob.rs:266-273
+    assert h.get_root_commitment() == broot
+    assert blob.proof_len() == 4 + 2
+    for j in range(N):
+        share = blob.get_share(j)                                                   # blob.rs:306-317
+        assert len(share) == n
+        for c, ch in enumerate(share):
+            assert ch.get_chunkset_id() == c and ch.get_global_chunk_id() == c * N + j
+            assert ch.get_erasure_coded_data() == coded[c * N + j].tobytes()
+            cproof = o.merkle(leaves[c])[1][j]
+            assert ch.get_proof() == cproof + bproofs[c]                            # chunkset.rs:98-102
+            assert o.merkle_verify(c * N + j, leaves[c][j], ch.get_proof(), broot)  # chunk.rs:88-90
+    _raises("InvalidErasureCodedShareId", blob.get_share, N)
+    _raises("EmptyDataForBlob", decds_amd.Blob, ctx, b"")
+    # a multi-context Blob (shards over two contexts of the one device) is identical
+    ctx2 = decds_amd.Context(0)
+    b2 = decds_amd.Blob([ctx, ctx2], data, coeffs)
+    assert b2.get_blob_header() == h
+    assert [c.get_erasure_coded_data() for c in b2.get_share(7)] == [c.get_erasure_coded_data() for c in blob.get_share(7)]
+    del b2
+    ctx2.close()
+
+
+def test_repairing_blob_add_chunk_like_reference(ctx):
+    # blob.rs:700-762
+    _, _, blob = _blob(ctx, 2 * CS, 0x2B20)
+    header = blob.get_blob_header()
+    chunks = _all_chunks(blob)
+    rep = decds_amd.RepairingBlob(ctx, header)
+    rep.add_chunk(chunks[0])
+    bad_header = BlobHeader(header.byte_length, header.num_chunksets, header.digest, o.blake3(b"fake_root_commitment"),
+                            header.chunkset_root_commitments)
+    _raises("InvalidProofInChunk", decds_amd.RepairingBlob(ctx, bad_header).add_chunk, chunks[0])
+    ready = decds_amd.RepairingBlob(ctx, header)
+    cs0 = chunks[0].get_chunkset_id()
+    for c in chunks:
+        if c.get_chunkset_id() == cs0:
+            ready.add_chunk(c)
+            if ready.is_chunkset_ready_to_repair(cs0):
+                break
+    assert ready.is_chunkset_ready_to_repair(cs0)
+    extra = next(c for c in chunks if c.get_chunkset_id() == cs0 and c.get_global_chunk_id() != chunks[0].get_global_chunk_id())
+    _raises("ChunksetReadyToRepair", ready.add_chunk, extra)
+    ready.get_repaired_chunkset(cs0)
+    assert not ready.is_chunkset_ready_to_repair(cs0)
+    assert ready.is_chunkset_already_repaired(cs0)
+    _raises("ChunksetAlreadyRepaired", ready.add_chunk, chunks[0])
+
+
+def test_repairing_blob_get_repaired_chunkset_like_reference(ctx):
+    # blob.rs:765-837: 2.5 chunksets, the partial last one truncated
+    blob_len = 2 * CS + CS // 2
+    data, _, blob = _blob(ctx, blob_len, 0x3B30)
+    header = blob.get_blob_header()
+    chunks = _all_chunks(blob)
+    rep = decds_amd.RepairingBlob(ctx, header)
+    _raises("ChunksetNotYetReadyToRepair", rep.get_repaired_chunkset, 0)
+    for cid in (0, 2):
+        for c in chunks:
+            if c.get_chunkset_id() == cid:
+                rep.add_chunk(c)
+                if rep.is_chunkset_ready_to_repair(cid):
+                    break
+        assert rep.is_chunkset_ready_to_repair(cid)
+        got = rep.get_repaired_chunkset(cid)
+        assert got == data[cid * CS:min(blob_len, (cid + 1) * CS)].tobytes()
+        assert rep.is_chunkset_already_repaired(cid)
+        _raises("ChunksetAlreadyRepaired", rep.get_repaired_chunkset, cid)
+    _raises("InvalidChunksetId", rep.get_repaired_chunkset, 3)
+    _raises("InvalidChunksetId", rep.is_chunkset_ready_to_repair, 3)
+    _raises("InvalidChunksetId", rep.is_chunkset_already_repaired, 3)
+
+
+def test_repairing_blob_error_branches(ctx):
+    data, _, blob = _blob(ctx, CS + 99, 0x4B40)
+    header = blob.get_blob_header()
+    rep = decds_amd.RepairingBlob(ctx, header)
+    c0 = blob.get_chunk(0, 3)
+    moved = decds_amd.Chunk(5, c0.chunk_id, c0.erasure_coded_data, c0.proof)
+    _raises("InvalidChunksetId", rep.add_chunk, moved)                            # blob.rs:376-379
+    t = bytearray(c0.erasure_coded_data)
+    t[4321] ^= 1
+    _raises("InvalidProofInChunk", rep.add_chunk, decds_amd.Chunk(0, c0.chunk_id, bytes(t), c0.proof))
+    _raises("InvalidProofInChunk", rep.add_chunk, decds_amd.Chunk(0, c0.chunk_id, c0.erasure_coded_data, c0.proof[:3]))
+    wrong = blob.get_chunk(1, 3)                                                   # a valid chunk of chunkset 1
+    _raises("InvalidProofInChunk", rep.add_chunk, decds_amd.Chunk(0, c0.chunk_id, wrong.erasure_coded_data, wrong.proof))
+    rep.add_chunk(c0)
+    _raises("ChunkDecodingFailed", rep.add_chunk, c0)                              # not useful (chunkset.rs:181-183)
+    for j in range(N):
+        if rep.is_chunkset_ready_to_repair(0):
+            break
+        try:
+            rep.add_chunk(blob.get_chunk(0, j))
+        except DecdsError as e:
+            assert e.kind == "ChunkDecodingFailed"
+    _raises("ChunksetNotYetReadyToRepair", rep.get_repaired_chunkset, 1)
+    assert rep.get_repaired_chunkset(0) == data[:CS].tobytes()
+    _raises("ChunksetAlreadyRepaired", rep.add_chunk, c0)
+
+
+def test_repairing_blob_all_chunks_shuffled_batch_vs_sequential(ctx):
+    # tests.rs:4-57 through RepairingBlob: every chunk of every chunkset in one shuffled order, some
+    # tampered; the batched add_chunks must return exactly the sequential add_chunk results, and
+    # every chunkset repairs (several decoded in one device batch)
+    blob_len = 5 * CS + 4321
+    data, _, blob = _blob(ctx, blob_len, 0x5B50)
+    header = blob.get_blob_header()
+    n = header.get_num_chunksets()
+    chunks = _all_chunks(blob)
+    order = np.random.default_rng(3).permutation(len(chunks))
+    arrivals = []
+    for i, k in enumerate(order):
+        c = chunks[int(k)]
+        if i % 17 == 5:  # tamper with a few on the way
+            t = bytearray(c.erasure_coded_data)
+            t[i * 97 % F] ^= 0x10
+            c = decds_amd.Chunk(c.chunkset_id, c.chunk_id, bytes(t), c.proof)
+        arrivals.append(c)
+    seq = decds_amd.RepairingBlob(ctx, header)
+    want = []
+    for c in arrivals:
+        try:
+            seq.add_chunk(c)
+            want.append(0)
+        except DecdsError as e:
+            want.append(e.status)
+    bat = decds_amd.RepairingBlob(ctx, header)
+    got = bat.add_chunks(arrivals)
+    assert got.tolist() == want
+    assert 11 in want and 3 in want  # InvalidProofInChunk and ChunksetReadyToRepair both occurred
+    for rep in (bat, seq):
+        for c in range(n):
+            assert rep.is_chunkset_ready_to_repair(c)
+        for c in (3, 0, 5, 1, 2, 4):
+            assert rep.get_repaired_chunkset(c) == data[c * CS:min(blob_len, (c + 1) * CS)].tobytes(), c
+    # after everything is repaired, every further chunk is rejected as already repaired
+    assert set(bat.add_chunks(arrivals[:20]).tolist()) == {10}

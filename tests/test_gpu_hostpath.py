@@ -1,0 +1,154 @@
+"""GPU tests of the host-memory paths: the blob pipelines over many batches (every slot reused,
+an unready and a repair-failed chunkset in reused slots), registered vs staged caller memory, the
+multi-context (multi-device) shard forms, the host registry's rules, and concurrent chunkset-mirror
+callers (ChunkSet::new from rayon workers, blob.rs:256-264). Bit-exact against oracle/."""
+import threading
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+import decds_amd  # noqa: E402
+from decds_amd import codec  # noqa: E402
+from decds_amd._capi import CHUNKSET_BYTES as CS, CODED_PIECE_BYTES as F, K, N, DecdsError, check, lib  # noqa: E402
+import oracle as o  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+
+def _as(buf, src):
+    buf[:] = src
+    return buf
+
+
+def _cand_with_failures(coded, n, rng, not_ready, broken):
+    """random arrival orders; chunkset `not_ready` gets 9 candidates; chunkset `broken` gets one accepted
+    row corrupted in its last byte so piece 9's tail no longer decodes to marker || zeros"""
+    cand = np.full((n, N), 0xFF, np.uint8)
+    for c in range(n):
+        cand[c, :] = rng.permutation(N)
+    cand[not_ready, 9:] = 0xFF
+    sel = [int(x) for x in cand[broken, :K]]  # independent with overwhelming probability: checked below
+    inv = o.matrix_inverse(coded[[broken * N + r for r in sel], :K])
+    assert inv is not None
+    k = next(k for k in range(K) if inv[9, k])
+    coded = coded.copy()
+    coded[broken * N + sel[k], F - 1] ^= 0x5A
+    return cand, coded
+
+
+@pytest.mark.parametrize("batch,pinned", [(1, False), (2, True), (2, False), (3, True)])
+def test_blob_host_paths_reuse_every_slot(ctx, batch, pinned):
+    # 7 chunksets in batches of 1-3: 3-7 batches over the 3 slots, so every slot is reused; the
+    # unready chunkset (4) and the repair-failed one (5) sit in reused slots; last chunkset ragged
+    n = 7
+    blob_len = (n - 1) * CS + 12345
+    blob = o.fill_random(0xA5A5 + batch, blob_len)
+    coeffs = o.fill_random(0xC5C5 + batch, n * N * K)
+    hb = []
+    if pinned:  # registered caller memory: DMA'd directly
+        hb = [decds_amd.HostBuffer(blob_len), decds_amd.HostBuffer(n * N * F), decds_amd.HostBuffer(blob_len)]
+        blob_in, coded_out, rep_out = _as(hb[0].array, blob), hb[1].array.reshape(n * N, F), hb[2].array
+    else:  # plain memory: staged through the context's page-locked rings
+        blob_in, coded_out, rep_out = blob, None, None
+    coded = codec.blob_encode_host(ctx, blob_in, coeffs, batch=batch, out=coded_out)
+    assert np.array_equal(coded, o.blob_encode(blob, coeffs, nthreads=8))
+    cand, coded_bad = _cand_with_failures(coded, n, np.random.default_rng(batch), not_ready=4, broken=5)
+    if pinned:
+        coded_bad = _as(coded_out, coded_bad)
+    out, status = codec.blob_repair_host(ctx, coded_bad, cand, blob_len, batch=batch, out=rep_out)
+    assert status.tolist() == [0, 0, 0, 0, 5, 6, 0]
+    for c in range(n):
+        lo, hi = c * CS, min(blob_len, (c + 1) * CS)
+        if status[c] == 0:
+            assert np.array_equal(out[lo:hi], blob[lo:hi]), c
+        else:
+            assert not out[lo:hi].any(), c  # no data for a chunkset that could not be repaired
+    for b in hb:
+        b.free()
+
+
+def test_multi_context_shards_match_single(ctx):
+    # two contexts on the one device stand in for two GPUs: chunkset shards [0, 3) and [3, 5)
+    ctx2 = decds_amd.Context(0)
+    n = 5
+    blob_len = 4 * CS + 777
+    blob = o.fill_random(0xB0B0, blob_len)
+    coeffs = o.fill_random(0xB1B1, n * N * K)
+    single = codec.blob_encode_host(ctx, blob, coeffs, batch=2)
+    multi = codec.blob_encode_host_multi([ctx, ctx2], blob, coeffs, batch=2)
+    assert np.array_equal(single, multi)
+    cand = np.stack([np.random.default_rng(c).permutation(N) for c in range(n)]).astype(np.uint8)
+    cand[1, 9:] = 0xFF
+    o1, s1 = codec.blob_repair_host(ctx, single, cand, blob_len, batch=2)
+    o2, s2 = codec.blob_repair_host_multi([ctx, ctx2], single, cand, blob_len, batch=2)
+    assert s1.tolist() == s2.tolist() == [0, 5, 0, 0, 0]
+    assert np.array_equal(o1, o2)
+    ok = np.repeat(s1 == 0, CS)[:blob_len]
+    assert np.array_equal(o2[ok], blob[ok])
+    ctx2.close()
+
+
+def test_host_registry_rules(ctx):
+    L = lib()
+    a = np.zeros(3 << 20, np.uint8)
+    p = a.ctypes.data
+    assert L.decds_host_is_registered(p, a.nbytes) == 0
+    check(L.decds_host_register(p, a.nbytes))
+    check(L.decds_host_register(p, a.nbytes))                     # same range again: refcounted
+    assert L.decds_host_is_registered(p + 100, 1000) == 1
+    assert L.decds_host_register(p + 4096, 4096) == -2            # partial overlap refused
+    check(L.decds_host_unregister(p))
+    assert L.decds_host_is_registered(p, a.nbytes) == 1           # one registration left
+    check(L.decds_host_unregister(p))
+    assert L.decds_host_is_registered(p, a.nbytes) == 0
+    assert L.decds_host_unregister(p) == -2                       # not registered any more
+    hb = decds_amd.HostBuffer(5000)
+    assert L.decds_host_is_registered(hb.array.ctypes.data, 5000) == 1
+    assert L.decds_host_unregister(hb.array.ctypes.data) == -2    # allocations are freed, not unregistered
+    hb.free()
+    # a registered caller buffer used by a host path, unregistered in between calls
+    blob = o.fill_random(0xC0C0, CS + 5)
+    coeffs = o.fill_random(0xC1C1, 2 * N * K)
+    codec.host_register(blob)
+    got = codec.blob_encode_host(ctx, blob, coeffs)
+    codec.host_unregister(blob)
+    assert np.array_equal(got, o.blob_encode(blob, coeffs, nthreads=8))
+
+
+def test_chunkset_mirror_concurrent_callers(ctx):
+    # ChunkSet::new / RepairingChunkSet::repair from 8 threads at once, each on its own chunkset:
+    # every thread takes its own lane (stream, device buffers, staging)
+    T = 8
+    results, errors = [None] * T, []
+
+    def worker(t):
+        try:
+            data = o.fill_random(0xD000 + t, CS)
+            coeffs = o.fill_random(0xD100 + t, N * K)
+            cs = decds_amd.ChunkSet(ctx, t, data.tobytes(), coeffs.tobytes())
+            rcs = decds_amd.RepairingChunkSet(ctx, t, cs.get_root_commitment())
+            for j in np.random.default_rng(t).permutation(N)[:K + 2]:
+                if rcs.is_ready_to_repair():
+                    break
+                try:
+                    rcs.add_chunk(cs.get_chunk(int(j)))
+                except DecdsError as e:
+                    assert e.kind == "ChunkDecodingFailed"
+            results[t] = (cs, rcs.repair() == data.tobytes())
+        except Exception as e:  # surfaced below
+            errors.append(e)
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(T)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not errors, errors
+    assert all(r[1] for r in results)
+    for t in (0, T - 1):
+        data = o.fill_random(0xD000 + t, CS)
+        ref = o.chunkset_encode(data, o.fill_random(0xD100 + t, N * K), nthreads=8)
+        cs = results[t][0]
+        assert all(cs.get_chunk(j).erasure_coded_data == ref[j].tobytes() for j in range(N))

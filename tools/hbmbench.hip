@@ -1,0 +1,244 @@
+// hbmbench.hip — the HBM ceilings of this part, measured the way the codec kernels run: every
+// variant is first run back to back for --warm-ms (clocks and the memory subsystem ramp up over
+// hundreds of ms; round 1's copybench timed 12 launches of 0.2-0.4 ms from a cold chip), then
+// --reps launches are timed one by one with HIP events; median and best are printed as JSON lines.
+// GB/s counts bytes read + bytes written.
+//
+//   copy / read / write    grid-stride float4 streams, W workgroups per CU x 256 threads, U accesses
+//                          in flight per lane, plain or non-temporal stores
+//   blk_copy               each workgroup copies one contiguous span (no grid stride)
+//   codec_enc / codec_dec  the streaming kernels' exact access pattern without the GF arithmetic:
+//                          per 16-column lane block 10 row loads + 16 (10) row stores, rows at the
+//                          rlnc strides (L = 2^20+1 for pieces, F = L+10 for coded rows), units of
+//                          4 (8) tiles of 256 blocks per workgroup, 2 workgroups per CU
+//
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/hbmbench.hip -o tools/bin/hbmbench
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#define CK(x)                                                                   \
+    do {                                                                        \
+        hipError_t e_ = (x);                                                    \
+        if (e_ != hipSuccess) {                                                 \
+            std::fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e_));        \
+            std::exit(1);                                                       \
+        }                                                                       \
+    } while (0)
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+template <int U, int ST>  // ST: 0 plain, 1 nt, 2 sc1 (write-through, line dropped from L2)
+__device__ __forceinline__ void st16(u32x4 *p, u32x4 v) {
+    if constexpr (ST == 1)
+        __builtin_nontemporal_store(v, p);
+    else if constexpr (ST == 2) {
+        const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(p, 0, 16, 0x00020000);
+        __builtin_amdgcn_raw_buffer_store_b128(v, r, 0, 0, 16);
+    } else
+        *p = v;
+}
+
+template <int U, int ST>
+__global__ __launch_bounds__(256) void copy_k(const u32x4 *__restrict__ s, u32x4 *__restrict__ d, size_t n16) {
+    const size_t stride = (size_t)gridDim.x * 256;
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += stride * U) {
+        u32x4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; u++)
+            if (i + u * stride < n16) v[u] = s[i + u * stride];
+#pragma unroll
+        for (int u = 0; u < U; u++)
+            if (i + u * stride < n16) st16<U, ST>(d + i + u * stride, v[u]);
+    }
+}
+
+template <int U>
+__global__ __launch_bounds__(256) void read_k(const u32x4 *__restrict__ s, size_t n16, u32x4 *__restrict__ sink) {
+    const size_t stride = (size_t)gridDim.x * 256;
+    u32x4 acc = {0, 0, 0, 0};
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += stride * U) {
+#pragma unroll
+        for (int u = 0; u < U; u++)
+            if (i + u * stride < n16) acc ^= s[i + u * stride];
+    }
+    if (acc.x == 0x12345678u) sink[0] = acc;
+}
+
+template <int U, int ST>
+__global__ __launch_bounds__(256) void write_k(u32x4 *__restrict__ d, size_t n16) {
+    const size_t stride = (size_t)gridDim.x * 256;
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += stride * U) {
+#pragma unroll
+        for (int u = 0; u < U; u++)
+            if (i + u * stride < n16) st16<U, ST>(d + i + u * stride, u32x4{(uint32_t)i, 1u, 2u, 3u});
+    }
+}
+
+// each workgroup one contiguous span of `span` 16-byte words, 4 loads in flight per lane
+template <int ST>
+__global__ __launch_bounds__(256) void blk_copy_k(const u32x4 *__restrict__ s, u32x4 *__restrict__ d, size_t n16,
+                                                  size_t span) {
+    const size_t lo = (size_t)blockIdx.x * span, hi = std::min(n16, lo + span);
+    for (size_t i = lo + threadIdx.x; i < hi; i += 256 * 4) {
+        u32x4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+            if (i + u * 256 < hi) v[u] = s[i + u * 256];
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+            if (i + u * 256 < hi) st16<4, ST>(d + i + u * 256, v[u]);
+    }
+}
+
+// the codec kernels' memory pattern (no GF arithmetic): NIN row loads then NOUT row stores per lane
+// block, row bases at the rlnc strides, UNIT tiles of 256 blocks per workgroup, byte-misaligned
+// unaligned 16-B accesses exactly as the kernels issue them (buffer ops, OOB lanes dropped)
+constexpr uint64_t CSB = 10ull << 20, LB = (CSB + 10) / 10, FB = LB + 10;
+constexpr uint32_t BLOCKS = 65535;
+template <int NIN, int NOUT, int UNIT, int ST>
+__global__ __launch_bounds__(256, 2) void codec_k(const uint8_t *__restrict__ in, size_t in_stride, size_t in_row,
+                                                  uint32_t in_off, uint8_t *__restrict__ out, size_t out_stride,
+                                                  size_t out_row, uint32_t out_off, size_t n) {
+    const uint32_t t0 = blockIdx.x * UNIT, cs = t0 / 256, tile0 = t0 % 256;
+    if (cs >= n) return;
+    const uint8_t *ib = in + cs * in_stride;
+    uint8_t *ob = out + cs * out_stride;
+    const __amdgpu_buffer_rsrc_t ri = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(ib), 0, 0x80000000u, 0x00020000);
+    const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(ob, 0, 0x80000000u, 0x00020000);
+    u32x4 acc = {0, 0, 0, 0};
+    for (uint32_t t = tile0; t < tile0 + UNIT; t++) {
+        const uint32_t b = t * 256 + threadIdx.x;
+        const uint32_t col = b < BLOCKS ? b * 16 : 0x80000000u;
+        u32x4 x[NIN];
+#pragma unroll
+        for (int i = 0; i < NIN; i++) x[i] = __builtin_amdgcn_raw_buffer_load_b128(ri, (uint32_t)(i * in_row) + in_off + col, 0, 0);
+#pragma unroll
+        for (int i = 0; i < NIN; i++) acc ^= x[i];
+#pragma unroll
+        for (int j = 0; j < NOUT; j++)
+            __builtin_amdgcn_raw_buffer_store_b128(acc + (uint32_t)j, ro, (uint32_t)(j * out_row) + out_off + col, 0,
+                                                   ST == 1 ? 2 : ST == 2 ? 16 : 0);
+    }
+}
+
+struct Args {
+    int warm_ms = 300, reps = 20;
+    size_t gib = 1;
+};
+
+template <typename F>
+void run(const char *name, const char *cfg, double bytes, F f, const Args &a) {
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    auto t0 = std::chrono::steady_clock::now();
+    int warm = 0;
+    while (std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() < a.warm_ms) {
+        for (int i = 0; i < 10; i++) f();
+        CK(hipDeviceSynchronize());
+        warm += 10;
+    }
+    std::vector<float> ms;
+    for (int r = 0; r < a.reps; r++) {
+        CK(hipEventRecord(e0));
+        f();
+        CK(hipEventRecord(e1));
+        CK(hipEventSynchronize(e1));
+        float t;
+        CK(hipEventElapsedTime(&t, e0, e1));
+        ms.push_back(t);
+    }
+    std::sort(ms.begin(), ms.end());
+    const double med = ms[ms.size() / 2], best = ms[0];
+    std::printf("{\"variant\": \"%s\", \"cfg\": \"%s\", \"MB\": %.1f, \"warm_launches\": %d, \"ms_med\": %.4f, "
+                "\"GBps_med\": %.1f, \"GBps_best\": %.1f}\n",
+                name, cfg, bytes / 1e6, warm, med, bytes / med / 1e6, bytes / best / 1e6);
+    std::fflush(stdout);
+    CK(hipEventDestroy(e0));
+    CK(hipEventDestroy(e1));
+}
+
+int main(int argc, char **argv) {
+    Args a;
+    std::string only;
+    for (int i = 1; i < argc; i++) {
+        if (!std::strcmp(argv[i], "--warm-ms")) a.warm_ms = std::atoi(argv[++i]);
+        if (!std::strcmp(argv[i], "--reps")) a.reps = std::atoi(argv[++i]);
+        if (!std::strcmp(argv[i], "--gib")) a.gib = std::atoi(argv[++i]);
+        if (!std::strcmp(argv[i], "--only")) only = argv[++i];
+    }
+    auto want = [&](const char *g) { return only.empty() || only.find(g) != std::string::npos; };
+    hipDeviceProp_t prop;
+    CK(hipGetDeviceProperties(&prop, 0));
+    const int cus = prop.multiProcessorCount;
+    const size_t bytes = a.gib << 30, n16 = bytes / 16;
+    u32x4 *s, *d, *sink;
+    CK(hipMalloc(&s, bytes));
+    CK(hipMalloc(&d, bytes));
+    CK(hipMalloc(&sink, 64));
+    CK(hipMemset(s, 0x3c, bytes));
+    CK(hipMemset(d, 0, bytes));
+    char cfg[128];
+    if (want("stream")) {
+        for (int w : {2, 4, 8, 16}) {
+            const int grid = cus * w;
+            std::snprintf(cfg, sizeof cfg, "%d WG/CU, %zu GiB", w, a.gib);
+            run("read_u1", cfg, bytes, [&] { read_k<1><<<grid, 256>>>(s, n16, sink); }, a);
+            run("read_u4", cfg, bytes, [&] { read_k<4><<<grid, 256>>>(s, n16, sink); }, a);
+            run("write_u1", cfg, bytes, [&] { write_k<1, 0><<<grid, 256>>>(d, n16); }, a);
+            run("write_u4", cfg, bytes, [&] { write_k<4, 0><<<grid, 256>>>(d, n16); }, a);
+            run("write_u4_nt", cfg, bytes, [&] { write_k<4, 1><<<grid, 256>>>(d, n16); }, a);
+            run("write_u4_sc1", cfg, bytes, [&] { write_k<4, 2><<<grid, 256>>>(d, n16); }, a);
+            run("copy_u1", cfg, 2.0 * bytes, [&] { copy_k<1, 0><<<grid, 256>>>(s, d, n16); }, a);
+            run("copy_u2", cfg, 2.0 * bytes, [&] { copy_k<2, 0><<<grid, 256>>>(s, d, n16); }, a);
+            run("copy_u4", cfg, 2.0 * bytes, [&] { copy_k<4, 0><<<grid, 256>>>(s, d, n16); }, a);
+            run("copy_u4_nt", cfg, 2.0 * bytes, [&] { copy_k<4, 1><<<grid, 256>>>(s, d, n16); }, a);
+            run("copy_u4_sc1", cfg, 2.0 * bytes, [&] { copy_k<4, 2><<<grid, 256>>>(s, d, n16); }, a);
+        }
+        // one thread per float4, no grid stride (the "naive" copy many guides time)
+        std::snprintf(cfg, sizeof cfg, "1 float4/thread, %zu GiB", a.gib);
+        run("copy_flat", cfg, 2.0 * bytes, [&] { copy_k<1, 0><<<(unsigned)(n16 / 256), 256>>>(s, d, n16); }, a);
+        run("copy_flat_nt", cfg, 2.0 * bytes, [&] { copy_k<1, 1><<<(unsigned)(n16 / 256), 256>>>(s, d, n16); }, a);
+    }
+    if (want("blk")) {
+        for (size_t span_kib : {64, 256, 1024}) {
+            const size_t span = span_kib * 1024 / 16;
+            const unsigned grid = (unsigned)((n16 + span - 1) / span);
+            std::snprintf(cfg, sizeof cfg, "%zu KiB per WG, %zu GiB", span_kib, a.gib);
+            run("blk_copy", cfg, 2.0 * bytes, [&] { blk_copy_k<0><<<grid, 256>>>(s, d, n16, span); }, a);
+            run("blk_copy_nt", cfg, 2.0 * bytes, [&] { blk_copy_k<1><<<grid, 256>>>(s, d, n16, span); }, a);
+        }
+    }
+    if (want("codec")) {
+        // encode pattern: n chunksets of 10 MiB source -> 16 rows of F per chunkset
+        for (size_t n : {103, 256}) {
+            const size_t src_b = n * CSB, dst_b = n * 16 * FB;
+            if (src_b > bytes || dst_b > bytes) continue;
+            const double moved = (double)n * (CSB + 16 * FB);
+            std::snprintf(cfg, sizeof cfg, "%zu chunksets, pitch F", n);
+            const unsigned ge = (unsigned)(n * 64), gd = (unsigned)(n * 32);
+            auto *src = reinterpret_cast<const uint8_t *>(s);
+            auto *dst = reinterpret_cast<uint8_t *>(d);
+            run("codec_enc", cfg, moved, [&] { codec_k<10, 16, 4, 0><<<ge, 256>>>(src, CSB, LB, 0, dst, 16 * FB, FB, 10, n); }, a);
+            run("codec_enc_nt", cfg, moved, [&] { codec_k<10, 16, 4, 1><<<ge, 256>>>(src, CSB, LB, 0, dst, 16 * FB, FB, 10, n); }, a);
+            // aligned rows: pitch rounded to 256 B, payload offset 16 (what an aligned layout would give)
+            const size_t FA = (FB + 255) & ~(size_t)255;
+            if (n * 16 * FA <= bytes) {
+                std::snprintf(cfg, sizeof cfg, "%zu chunksets, pitch %zu, aligned rows", n, FA);
+                run("codec_enc_aligned", cfg, moved, [&] { codec_k<10, 16, 4, 0><<<ge, 256>>>(src, CSB, 1 << 20, 0, dst, 16 * FA, FA, 0, n); }, a);
+            }
+            std::snprintf(cfg, sizeof cfg, "%zu chunksets, pitch F", n);
+            const double dmoved = (double)n * (10 * FB + CSB);
+            run("codec_dec", cfg, dmoved, [&] { codec_k<10, 10, 8, 0><<<gd, 256>>>(dst, 16 * FB, FB, 10, reinterpret_cast<uint8_t *>(s), CSB, LB, 0, n); }, a);
+        }
+    }
+    CK(hipDeviceSynchronize());
+    return 0;
+}
