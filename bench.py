@@ -50,6 +50,8 @@ def parse():
     p.add_argument("--no-sweep", action="store_true", help="skip the encode batch sweep (256..1639 chunksets)")
     p.add_argument("--cpu-sample", type=int, default=0, help="chunksets in the CPU sample (0 = auto)")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
+    p.add_argument("--packed", action="store_true",
+                   help="coded rows packed at pitch 1,048,587 instead of the recommended 128-B-aligned layout")
     return p.parse_args()
 
 
@@ -149,7 +151,9 @@ def main():
             cand_h[c, :K] = rng.permutation(N)[:K]
         coeffs = torch.from_numpy(coeffs_h).to(dev)
         cand = torch.from_numpy(cand_h).to(dev)
-        coded = torch.empty(n * N * F, dtype=torch.uint8, device=dev)
+        # coded rows in the recommended device layout (include/decds_rlnc.h): pitch 1,048,704 with every
+        # payload 128-byte aligned — rlnc's byte-exact full coded pieces, line-aligned encoder stores
+        coded, pitch = codec.coded_buffer(n, aligned=not args.packed, device=dev)
         plan = torch.empty(n * 128, dtype=torch.uint8, device=dev)
         verd = torch.empty(n * N, dtype=torch.int8, device=dev)
         status = torch.empty(n, dtype=torch.int32, device=dev)
@@ -159,13 +163,13 @@ def main():
     def step(ev=None):
         if ev is not None:
             ev[0].record(stream)
-        codec.encode_batch(ctx, src, n, coeffs, coded, stream=stream)
+        codec.encode_batch(ctx, src, n, coeffs, coded, pitch, stream=stream)
         if ev is not None:
             ev[1].record(stream)
-        codec.repair_plan_batch(ctx, coded, n, cand, plan, verd, status, stream=stream)
+        codec.repair_plan_batch(ctx, coded, n, cand, plan, verd, status, pitch, stream=stream)
         if ev is not None:
             ev[2].record(stream)
-        codec.decode_batch(ctx, coded, n, plan, out, status, stream=stream)
+        codec.decode_batch(ctx, coded, n, plan, out, status, pitch, stream=stream)
         if ev is not None:
             ev[3].record(stream)
 
@@ -215,11 +219,11 @@ def main():
         dig = torch.empty(n * N * 32, dtype=torch.uint8, device=dev)
         roots = torch.empty(n * 32, dtype=torch.uint8, device=dev)
         proofs = torch.empty(n * N * 128, dtype=torch.uint8, device=dev)
-        codec.commit_batch(ctx, coded, n, dig, roots, proofs, first_chunkset_id=lo, stream=stream)
+        codec.commit_batch(ctx, coded, n, dig, roots, proofs, first_chunkset_id=lo, pitch=pitch, stream=stream)
         cev = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
         cev[0].record(stream)
         for s in range(args.steps):
-            codec.commit_batch(ctx, coded, n, dig, roots, proofs, first_chunkset_id=lo, stream=stream)
+            codec.commit_batch(ctx, coded, n, dig, roots, proofs, first_chunkset_id=lo, pitch=pitch, stream=stream)
             cev[s + 1].record(stream)
         stream.synchronize()
         c_ms = cev[0].elapsed_time(cev[-1]) / args.steps
@@ -238,15 +242,15 @@ def main():
             big = torch.empty(nmax * CS, dtype=torch.uint8, device=dev)
             codec.fill_random_device(ctx, 0xDEC05003, big, stream=stream)
             cbig = torch.from_numpy(codec.fill_random_host(0xC0EF0003, nmax * N * K)).to(dev)
-            obig = torch.empty(nmax * N * F, dtype=torch.uint8, device=dev)
+            obig, bpitch = codec.coded_buffer(nmax, aligned=not args.packed, device=dev)
         sweep = []
         for ns in SWEEP:
             reps = 3 if ns >= 1024 else 5 if ns >= 256 else 20
-            codec.encode_batch(ctx, big, ns, cbig, obig, stream=stream)
+            codec.encode_batch(ctx, big, ns, cbig, obig, bpitch, stream=stream)
             sev = [torch.cuda.Event(enable_timing=True) for _ in range(reps + 1)]
             sev[0].record(stream)
             for r in range(reps):
-                codec.encode_batch(ctx, big, ns, cbig, obig, stream=stream)
+                codec.encode_batch(ctx, big, ns, cbig, obig, bpitch, stream=stream)
                 sev[r + 1].record(stream)
             stream.synchronize()
             ms = sev[0].elapsed_time(sev[-1]) / reps
@@ -290,6 +294,7 @@ def main():
             "data": "synthetic (SplitMix64 random blob + coding vectors, seeded)",
             "value_def": "(blob bytes encoded + blob bytes of repaired chunksets) / 2 per second",
             "config": {"workload": args.config + ": " + desc, "chunksets_per_gpu": n,
+                       "coded_layout": "pitch %d, payloads %s" % (pitch, "packed" if args.packed else "128-B aligned"),
                        "blob_bytes_per_gpu": blob_per_gpu, "survivors_per_chunkset": K,
                        "parallelism": "chunkset-index shards x%d, no collective" % world},
             "roofline": {"bound": "hbm", "kernel": dominant, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,

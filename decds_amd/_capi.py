@@ -18,6 +18,8 @@ CHUNKSET_BYTES = 10 * (1 << 20)                     # ChunkSet::BYTE_LENGTH (chu
 PIECE_BYTES = (CHUNKSET_BYTES + 1 + K - 1) // K     # PADDED_CHUNK_BYTE_LEN (chunkset.rs:117)
 CODED_PIECE_BYTES = PIECE_BYTES + K                 # coding vector || payload
 REPAIR_PLAN_BYTES = 128
+CODED_PITCH_ALIGNED = 1048704       # recommended device layout (include/decds_rlnc.h): 128-B-aligned payloads
+CODED_ROW_OFFSET_ALIGNED = 118
 NO_CANDIDATE = 0xFF
 
 # status codes, 1:1 with decds-lib/src/errors.rs (see include/decds_rlnc.h)

