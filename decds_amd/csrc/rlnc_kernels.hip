@@ -32,14 +32,11 @@ namespace decds {
 // ---- geometry ---------------------------------------------------------------------------------
 constexpr uint32_t DECDS_NO_CANDIDATE_U8 = 0xFF;
 constexpr uint32_t WG = 256;                                  // 4 waves
-constexpr uint32_t WAVES_PER_SIMD = 2;                        // 2 workgroups x 80 KiB LDS = the CU's 160 KiB
 constexpr uint32_t TILE_BLOCKS = WG;                          // one 16-col block per lane per tile
-constexpr uint32_t TILES_PER_CS = (MAIN_BLOCKS + TILE_BLOCKS - 1) / TILE_BLOCKS;  // 256
 constexpr uint32_t ROW_BYTES = 16;                            // one nibble row: 16 outputs' products
 constexpr uint32_t TABLE_BYTES = 16 * ROW_BYTES;              // 16 nibble rows = 256 B = the 64 banks once
 constexpr uint32_t LDS_BYTES = K * 2 * TABLE_BYTES;           // 5 KiB
 constexpr uint32_t NXCD = 8;
-static_assert(TILES_PER_CS == 256, "tile geometry");
 
 // Work units (tiles per workgroup) of the non-persistent launches and the workgroup order
 // (DESIGN.md §5.1, §8). Tuning constants, overridable at build time for in-process A/B
@@ -144,31 +141,44 @@ __device__ __forceinline__ uint32_t tbl_mul(const uint8_t *lds, uint32_t i, uint
 // Rows are addressed as a wave-uniform base plus a 32-bit row offset through a buffer descriptor
 // covering 2 GiB from the base (the launchers keep every row offset below). Piece rows start at
 // i*L (L = 2^20 + 1) and coded payloads at r*pitch + 10, so most rows are byte-misaligned by the
-// rlnc layout itself; gfx9 vector memory accepts unaligned 16-B accesses. A lane with nothing to
-// do passes column OOB_COL: its buffer loads return zeros and its buffer stores are dropped by the
+// rlnc layout itself; gfx9 vector memory accepts unaligned accesses. A lane with nothing to do
+// passes column OOB_COL: its buffer loads return zeros and its buffer stores are dropped by the
 // range check, so the streaming loop needs no per-lane branch (stream_range).
+// DW = dwords per lane per row: 4 (16-column lane blocks) or 2 (8-column blocks: half the
+// accumulator and input registers, for more workgroups per CU).
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+template <int DW> struct VecT;
+template <> struct VecT<4> { using T = u32x4; };
+template <> struct VecT<2> { using T = u32x2; };
+template <int DW> using Vec = typename VecT<DW>::T;
 constexpr uint32_t BUF_RECORDS = 0x80000000u;
 constexpr uint32_t OOB_COL = 0x80000000u;
 
-__device__ __forceinline__ uint4 ldrow(const uint8_t *base, uint32_t off) {
+template <int DW>
+__device__ __forceinline__ Vec<DW> ldrow(const uint8_t *base, uint32_t off) {
     const __amdgpu_buffer_rsrc_t r =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(base), 0, BUF_RECORDS, 0x00020000);
-    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
-    return make_uint4(v.x, v.y, v.z, v.w);
+    if constexpr (DW == 4)
+        return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+    else
+        return __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0);
 }
 
-__device__ __forceinline__ void strow(uint8_t *base, uint32_t off, uint4 v) {
-    const u32x4 w = {v.x, v.y, v.z, v.w};
+template <int DW>
+__device__ __forceinline__ void strow(uint8_t *base, uint32_t off, Vec<DW> v) {
     const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, 0, BUF_RECORDS, 0x00020000);
-    __builtin_amdgcn_raw_buffer_store_b128(w, r, off, 0, 0);
+    if constexpr (DW == 4)
+        __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 0);
+    else
+        __builtin_amdgcn_raw_buffer_store_b64(v, r, off, 0, 0);
 }
 
-template <int NIN>
-__device__ __forceinline__ void load_block(uint4 (&x)[NIN], const uint8_t *ibase, const uint32_t (&ioff)[NIN],
+template <int NIN, int DW>
+__device__ __forceinline__ void load_block(Vec<DW> (&x)[NIN], const uint8_t *ibase, const uint32_t (&ioff)[NIN],
                                            uint32_t col0) {
 #pragma unroll
-    for (int i = 0; i < NIN; i++) x[i] = ldrow(ibase, ioff[i] + col0);
+    for (int i = 0; i < NIN; i++) x[i] = ldrow<DW>(ibase, ioff[i] + col0);
 }
 
 // 4x4 byte transpose: out[b].byte[p] = in[p].byte[b]
@@ -184,10 +194,6 @@ __device__ __forceinline__ void transpose4x4(uint32_t a0, uint32_t a1, uint32_t 
     b3 = __builtin_amdgcn_perm(u3, u1, 0x07060302u);
 }
 
-__device__ __forceinline__ uint32_t word_of(const uint4 &v, int w) {
-    return w == 0 ? v.x : w == 1 ? v.y : w == 2 ? v.z : v.w;
-}
-
 __device__ __forceinline__ void xor3_into(uint32_t (&acc)[4], const u32x4 &a, const u32x4 &b) {
     // v_bitop3_b32 (gfx950): acc ^ a ^ b in one VALU op (truth table 0x96)
     acc[0] = __builtin_amdgcn_bitop3_b32(acc[0], a.x, b.x, 0x96);
@@ -197,7 +203,7 @@ __device__ __forceinline__ void xor3_into(uint32_t (&acc)[4], const u32x4 &a, co
 }
 
 // ---- hand-pipelined lookups ---------------------------------------------------------------------
-// The lookups of one lane block are cut into 4*NIN groups (input i, dword w: 4 columns x {lo, hi}
+// The lookups of one lane block are cut into DW*NIN groups (input i, dword w: 4 columns x {lo, hi}
 // = 8 reads); group g+1 is issued before group g is consumed, so 8-16 reads are in flight per wave
 // (hipcc's own schedule waits after every column: ~4 in flight). Reads are inline asm with
 // immediate table offsets and explicit counted waits (cdna_hip_programming.md §5.7 form (ii)):
@@ -205,9 +211,9 @@ __device__ __forceinline__ void xor3_into(uint32_t (&acc)[4], const u32x4 &a, co
 // The row address of a lookup is nibble * 16 (the table base is the instruction's offset): byte p's
 // high nibble masked in place (xw >> 8p) & 0xF0, its low nibble masked and shifted up by 4 — hipcc
 // turns both into one SDWA op each (v_and_b32_sdwa / v_lshlrev_b32_sdwa with a byte select).
-template <int G>
+template <int G, int DW>
 __device__ __forceinline__ void lds_issue(u32x4 (&r)[8], uint32_t xw) {
-    constexpr int i = G >> 2;
+    constexpr int i = G / DW;
     constexpr uint32_t tlo = (2 * i) * TABLE_BYTES, thi = (2 * i + 1) * TABLE_BYTES;
     const uint32_t lo4 = xw & 0x0F0F0F0Fu;
 #pragma unroll
@@ -227,76 +233,95 @@ __device__ __forceinline__ void lds_wait(u32x4 (&r)[8]) {
                  : "memory");
 }
 
-// Group G of the lookups; input (G+1)>>2's register takes the next block's bytes (ncol0) as soon
+// Group G of the lookups; input (G+1)/DW's register takes the next block's bytes (ncol0) as soon
 // as that input's lookups are all issued — before this block's stores: gfx9's vmcnt counts stores
 // too, so a load issued behind the stores would also wait for them.
-template <int NIN, int G>
-__device__ __forceinline__ void lds_step(uint32_t (&acc)[16][4], u32x4 (&ra)[8], u32x4 (&rb)[8], uint4 (&x)[NIN],
-                                         const uint8_t *ibase, const uint32_t (&ioff)[NIN], uint32_t ncol0) {
-    constexpr int NG = 4 * NIN;
+template <int NIN, int DW, int G>
+__device__ __forceinline__ void lds_step(uint32_t (&acc)[4 * DW][4], u32x4 (&ra)[8], u32x4 (&rb)[8],
+                                         Vec<DW> (&x)[NIN], const uint8_t *ibase, const uint32_t (&ioff)[NIN],
+                                         uint32_t ncol0) {
+    constexpr int NG = DW * NIN;
     u32x4(&cur)[8] = (G & 1) ? rb : ra;  // group G's results
     u32x4(&nxt)[8] = (G & 1) ? ra : rb;
     if constexpr (G + 1 < NG) {
-        lds_issue<G + 1>(nxt, word_of(x[(G + 1) >> 2], (G + 1) & 3));
-        if constexpr (((G + 1) & 3) == 3) x[(G + 1) >> 2] = ldrow(ibase, ioff[(G + 1) >> 2] + ncol0);
+        lds_issue<G + 1, DW>(nxt, x[(G + 1) / DW][(G + 1) % DW]);
+        if constexpr (((G + 1) % DW) == DW - 1) x[(G + 1) / DW] = ldrow<DW>(ibase, ioff[(G + 1) / DW] + ncol0);
         lds_wait<8>(cur);
     } else {
         lds_wait<0>(cur);
     }
-    constexpr int w = G & 3;
+    constexpr int w = G % DW;
 #pragma unroll
     for (int p = 0; p < 4; p++) xor3_into(acc[4 * w + p], cur[2 * p], cur[2 * p + 1]);
 }
 
-template <int NIN, int... Gs>
-__device__ __forceinline__ void lookups(std::integer_sequence<int, Gs...>, uint32_t (&acc)[16][4], uint4 (&x)[NIN],
-                                        const uint8_t *ibase, const uint32_t (&ioff)[NIN], uint32_t ncol0) {
+template <int NIN, int DW, int... Gs>
+__device__ __forceinline__ void lookups(std::integer_sequence<int, Gs...>, uint32_t (&acc)[4 * DW][4],
+                                        Vec<DW> (&x)[NIN], const uint8_t *ibase, const uint32_t (&ioff)[NIN],
+                                        uint32_t ncol0) {
     u32x4 ra[8], rb[8];
-    lds_issue<0>(ra, x[0].x);
-    (lds_step<NIN, Gs>(acc, ra, rb, x, ibase, ioff, ncol0), ...);
+    lds_issue<0, DW>(ra, x[0][0]);
+    (lds_step<NIN, DW, Gs>(acc, ra, rb, x, ibase, ioff, ncol0), ...);
 }
 
-// One 16-column lane block: out_j[col0 .. col0+16) = sum_i M[j][i] * in_i[col0 .. col0+16).
+// One lane block of 4*DW columns: out_j[col0 ..) = sum_i M[j][i] * in_i[col0 ..).
 // x holds this block's inputs on entry and the inputs at column ncol0 on exit.
-template <int NIN, int NOUT>
-__device__ __forceinline__ void combine_block(uint4 (&x)[NIN], uint8_t *obase,
-                                              const uint32_t (&ooff)[NOUT], uint32_t col0, const uint8_t *ibase,
-                                              const uint32_t (&ioff)[NIN], uint32_t ncol0) {
-    uint32_t acc[16][4];  // acc[column][output group]: byte b = output 4*group + b
+template <int NIN, int NOUT, int DW>
+__device__ __forceinline__ void combine_block(Vec<DW> (&x)[NIN], uint8_t *obase, const uint32_t (&ooff)[NOUT],
+                                              uint32_t col0, const uint8_t *ibase, const uint32_t (&ioff)[NIN],
+                                              uint32_t ncol0) {
+    uint32_t acc[4 * DW][4];  // acc[column][output group]: byte b = output 4*group + b
 #pragma unroll
-    for (int c = 0; c < 16; c++)
+    for (int c = 0; c < 4 * DW; c++)
 #pragma unroll
         for (int q = 0; q < 4; q++) acc[c][q] = 0;
-    lookups<NIN>(std::make_integer_sequence<int, 4 * NIN>{}, acc, x, ibase, ioff, ncol0);
+    lookups<NIN, DW>(std::make_integer_sequence<int, DW * NIN>{}, acc, x, ibase, ioff, ncol0);
     // columns x outputs -> outputs x columns
 #pragma unroll
     for (int q = 0; q < 4; q++) {
         if (4 * q >= NOUT) break;
-        uint32_t o[4][4];  // o[b][w]: output 4q+b, columns 4w..4w+3
+        uint32_t o[4][DW];  // o[b][w]: output 4q+b, columns 4w..4w+3
 #pragma unroll
-        for (int w = 0; w < 4; w++)
+        for (int w = 0; w < DW; w++)
             transpose4x4(acc[4 * w + 0][q], acc[4 * w + 1][q], acc[4 * w + 2][q], acc[4 * w + 3][q], o[0][w], o[1][w],
                          o[2][w], o[3][w]);
 #pragma unroll
         for (int b = 0; b < 4; b++) {
             const int j = 4 * q + b;
-            if (j < NOUT) strow(obase, ooff[j] + col0, make_uint4(o[b][0], o[b][1], o[b][2], o[b][3]));
+            Vec<DW> v;
+#pragma unroll
+            for (int w = 0; w < DW; w++) v[w] = o[b][w];
+            if (j < NOUT) strow<DW>(obase, ooff[j] + col0, v);
         }
     }
 }
 
-// ---- column phase and edge columns --------------------------------------------------------------
-// Lane blocks cover payload columns from `phase` on (phase < 16, chosen by the launcher so that
-// coded rows at a 16-byte-aligned pitch are written on 16-byte boundaries); the workgroup owning
-// tile 0 does the edge columns byte by byte: e < phase is column e, the rest the columns after the
-// last block. Piece 9's main columns must stay below CS - 9L (its marker and padding are edge
-// columns), so a phase above 7 gives up one block: 33 edge columns instead of 17.
+// ---- geometry per lane-block width, column phase and edge columns -------------------------------
+// Lane blocks of COLS = 4*DW columns; a tile is 256 blocks. Blocks cover payload columns from
+// `phase` on (phase < COLS, chosen by the launcher so that coded rows at a COLS-aligned pitch are
+// written on COLS-byte boundaries); the workgroup owning tile 0 does the edge columns byte by byte:
+// e < phase is column e, the rest the columns after the last block. Piece 9's main columns must stay
+// below CS - 9L (its marker and padding are edge columns), so a phase above 7 gives up one block.
 constexpr uint32_t MAX_FULL_PHASE = (uint32_t)(CS - (K - 1) * L) - MAIN_COLS;
 static_assert(MAX_FULL_PHASE == 7, "layout");
-__device__ __forceinline__ uint32_t main_blocks(uint32_t phase) { return MAIN_BLOCKS - (phase > MAX_FULL_PHASE); }
-__device__ __forceinline__ uint32_t edge_cols(uint32_t phase) { return (uint32_t)L - main_blocks(phase) * COLS_PER_LANE; }
+template <int DW> constexpr uint32_t COLS = 4 * DW;
+template <int DW> constexpr uint32_t BLOCKS = MAIN_COLS / COLS<DW>;                 // 65535 / 131070
+template <int DW> constexpr uint32_t TILES = (BLOCKS<DW> + TILE_BLOCKS - 1) / TILE_BLOCKS;  // 256 / 512
+static_assert(BLOCKS<4> * COLS<4> == MAIN_COLS && BLOCKS<2> * COLS<2> == MAIN_COLS, "tiling covers the main columns");
+template <int DW>
+__device__ __forceinline__ uint32_t main_blocks(uint32_t phase) { return BLOCKS<DW> - (phase > MAX_FULL_PHASE); }
+template <int DW>
+__device__ __forceinline__ uint32_t edge_cols(uint32_t phase) { return (uint32_t)L - main_blocks<DW>(phase) * COLS<DW>; }
+template <int DW>
 __device__ __forceinline__ uint32_t edge_col(uint32_t e, uint32_t phase) {
-    return e < phase ? e : main_blocks(phase) * COLS_PER_LANE + e;
+    return e < phase ? e : main_blocks<DW>(phase) * COLS<DW> + e;
+}
+
+// this lane's first column of tile t of a range ending at tb, or out of range
+template <int DW>
+__device__ __forceinline__ uint32_t tile_col(uint32_t t, uint32_t tb, uint32_t phase) {
+    const uint32_t block = t * TILE_BLOCKS + threadIdx.x;
+    return t < tb && block < main_blocks<DW>(phase) ? block * COLS<DW> + phase : OOB_COL;
 }
 
 // Tiles [ta, tb) of one chunkset, branch-free: lanes past the last block use OOB_COL, so no lane
@@ -305,28 +330,22 @@ __device__ __forceinline__ uint32_t edge_col(uint32_t e, uint32_t phase) {
 // branch around the streaming code, or a reload path inside the loop, hipcc's wait-count pass
 // merges paths that issued no stores and waits with vmcnt(NIN-1) for the next tile's first input:
 // every tile then waited for the previous tile's stores as well; here it waits for the inputs only.
-// this lane's first column of tile t of a range ending at tb, or out of range
-__device__ __forceinline__ uint32_t tile_col(uint32_t t, uint32_t tb, uint32_t phase) {
-    const uint32_t block = t * TILE_BLOCKS + threadIdx.x;
-    return t < tb && block < main_blocks(phase) ? block * COLS_PER_LANE + phase : OOB_COL;
-}
-
-// HAVE: x already holds tile ta's inputs (loaded before the workgroup's table build)
-template <int NIN, int NOUT, bool HAVE>
-__device__ __forceinline__ void stream_range(uint32_t ta, uint32_t tb, uint32_t phase,
-                                             const uint8_t *ibase, const uint32_t (&ioff)[NIN], uint8_t *obase,
-                                             const uint32_t (&ooff)[NOUT], uint4 (&x)[NIN]) {
-    auto col = [&](uint32_t t) { return tile_col(t, tb, phase); };
-    if constexpr (!HAVE) load_block<NIN>(x, ibase, ioff, col(ta));
+// HAVE: x already holds tile ta's inputs (loaded before the workgroup's table build).
+template <int NIN, int NOUT, int DW, bool HAVE>
+__device__ __forceinline__ void stream_range(uint32_t ta, uint32_t tb, uint32_t phase, const uint8_t *ibase,
+                                             const uint32_t (&ioff)[NIN], uint8_t *obase,
+                                             const uint32_t (&ooff)[NOUT], Vec<DW> (&x)[NIN]) {
+    auto col = [&](uint32_t t) { return tile_col<DW>(t, tb, phase); };
+    if constexpr (!HAVE) load_block<NIN, DW>(x, ibase, ioff, col(ta));
     asm volatile("" ::: "memory");  // keep the dropped stores after the loads, as in the loop
 #pragma unroll
-    for (int j = 0; j < NOUT; j++) strow(obase, OOB_COL + ooff[j], make_uint4(0, 0, 0, 0));
+    for (int j = 0; j < NOUT; j++) strow<DW>(obase, OOB_COL + ooff[j], Vec<DW>{});
     // ta < tb (callers): a do-while, so no zero-trip guard lets hipcc sink the prologue loads
     // below the dropped stores (it did: vmcnt(9) again)
     uint32_t t = ta;
 #pragma unroll 1
     do {
-        combine_block<NIN, NOUT>(x, obase, ooff, col(t), ibase, ioff, col(t + 1));
+        combine_block<NIN, NOUT, DW>(x, obase, ooff, col(t), ibase, ioff, col(t + 1));
     } while (++t < tb);
 }
 
@@ -340,31 +359,32 @@ __device__ __forceinline__ uint32_t xcd_eighth_unit() {
     return x * per + (x < rem ? x : rem) + q;
 }
 
-// Encode: workgroup = UNIT consecutive tiles of one chunkset (256 tiles per chunkset).
+// Encode: workgroup = UNIT consecutive tiles of one chunkset (TILES<DW> tiles per chunkset).
 // The unit is walked as "segments up to the next chunkset boundary" although it never crosses one
-// (ENC_UNIT divides 256): with that loop hipcc allocates 228 VGPRs and no spills; the straight-line
-// form of the same work compiled to 256 VGPRs + 53 spilled (measured with
-// -Rpass-analysis=kernel-resource-usage).
-template <uint32_t UNIT, bool XCD_ORDER>
-__global__ __launch_bounds__(WG, WAVES_PER_SIMD) __attribute__((amdgpu_waves_per_eu(WAVES_PER_SIMD, WAVES_PER_SIMD)))
+// (UNIT divides TILES): with that loop hipcc allocated 228 VGPRs and no spills, the straight-line
+// form of the same work 256 VGPRs + 53 spilled (-Rpass-analysis=kernel-resource-usage).
+template <uint32_t UNIT, bool XCD_ORDER, int DW, int WAVES>
+__global__ __launch_bounds__(WG, WAVES) __attribute__((amdgpu_waves_per_eu(WAVES, WAVES)))
 void rlnc_encode_kernel(const uint8_t *__restrict__ src, size_t n, const uint8_t *__restrict__ coeffs,
                         uint8_t *__restrict__ dst, size_t pitch, uint32_t phase, uint32_t poly, uint32_t marker) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    static_assert(TILES_PER_CS % UNIT == 0, "a workgroup's tiles stay in one chunkset");
+    constexpr uint32_t T = TILES<DW>;
+    static_assert(T % UNIT == 0, "a workgroup's tiles stay in one chunkset");
     uint32_t ioff[K], ooff[N];
 #pragma unroll
     for (int i = 0; i < (int)K; i++) ioff[i] = (uint32_t)(i * L);              // piece i of the padded chunkset
 #pragma unroll
     for (int j = 0; j < (int)N; j++) ooff[j] = (uint32_t)(j * pitch + K);      // payload of coded row j
-    uint4 x[K];
+    Vec<DW> x[K];
     auto segment = [&](uint32_t t0, uint32_t te) {
-        const uint32_t cs = t0 / TILES_PER_CS, tile0 = t0 % TILES_PER_CS;
+        const uint32_t cs = t0 / T, tile0 = t0 % T;
         const uint8_t *M = coeffs + (size_t)cs * N * K;
         const uint8_t *ibase = src + (size_t)cs * CS;
         uint8_t *obase = dst + (size_t)cs * N * pitch;
         const uint32_t cw = table_coeffs<K, N>(M, K);
-        // the first tile's loads, in flight across the table build (issued after the coefficient loads)
-        if constexpr (DECDS_PREFETCH_FIRST) load_block<K>(x, ibase, ioff, tile_col(tile0, te - cs * TILES_PER_CS, phase));
+        // the first tile's loads, in flight across the table build (issued after the coefficient loads;
+        // issuing them first, so both latencies overlap, measured no faster: r02h)
+        if constexpr (DECDS_PREFETCH_FIRST) load_block<K, DW>(x, ibase, ioff, tile_col<DW>(tile0, te - cs * T, phase));
         lds_barrier();
         build_tables<K, N>(lds, cw, poly);
         lds_barrier();
@@ -372,8 +392,8 @@ void rlnc_encode_kernel(const uint8_t *__restrict__ src, size_t n, const uint8_t
             // coding-vector prefix of the 16 full coded pieces (rlnc layout: cv || payload)
             for (uint32_t idx = threadIdx.x; idx < N * K; idx += WG) obase[(idx / K) * pitch + idx % K] = M[idx];
             // piece 9 carries the boundary marker, then zero padding (Encoder::new, chunkset.rs:43)
-            for (uint32_t idx = threadIdx.x; idx < edge_cols(phase) * N; idx += WG) {
-                const uint32_t j = idx % N, col = edge_col(idx / N, phase);
+            for (uint32_t idx = threadIdx.x; idx < edge_cols<DW>(phase) * N; idx += WG) {
+                const uint32_t j = idx % N, col = edge_col<DW>(idx / N, phase);
                 uint32_t y = 0;
 #pragma unroll
                 for (uint32_t i = 0; i < K; i++) {
@@ -384,13 +404,13 @@ void rlnc_encode_kernel(const uint8_t *__restrict__ src, size_t n, const uint8_t
                 obase[j * pitch + K + col] = (uint8_t)y;
             }
         }
-        stream_range<K, N, DECDS_PREFETCH_FIRST>(tile0, te - cs * TILES_PER_CS, phase, ibase, ioff, obase, ooff, x);
+        stream_range<K, N, DW, DECDS_PREFETCH_FIRST>(tile0, te - cs * T, phase, ibase, ioff, obase, ooff, x);
     };
-    const uint64_t total = (uint64_t)n * TILES_PER_CS;
+    const uint64_t total = (uint64_t)n * T;
     uint32_t t0 = (XCD_ORDER ? xcd_eighth_unit() : blockIdx.x) * UNIT;
     const uint32_t t1 = (uint32_t)(t0 + UNIT < total ? t0 + UNIT : total);
     while (t0 < t1) {
-        const uint32_t cs_end = (t0 / TILES_PER_CS + 1) * TILES_PER_CS;
+        const uint32_t cs_end = (t0 / T + 1) * T;
         const uint32_t te = cs_end < t1 ? cs_end : t1;
         segment(t0, te);
         t0 = te;
@@ -402,7 +422,7 @@ void rlnc_encode_kernel(const uint8_t *__restrict__ src, size_t n, const uint8_t
 // rows plan.sel[k] at in_bases[cs] + sel*pitch, written to out_bases[cs] (the incremental
 // RepairingBlob keeps each chunkset's accepted rows in its own device slot).
 #ifndef DECDS_DEC_WAVES
-#define DECDS_DEC_WAVES 2  // waves per SIMD (the decode's 149 VGPRs would allow 3)
+#define DECDS_DEC_WAVES 2  // waves per SIMD (3 measured no faster, r02f)
 #endif
 template <uint32_t UNIT>
 __global__ __launch_bounds__(WG, DECDS_DEC_WAVES) __attribute__((amdgpu_waves_per_eu(DECDS_DEC_WAVES, DECDS_DEC_WAVES)))
@@ -410,9 +430,11 @@ void rlnc_decode_kernel(const uint8_t *__restrict__ coded, size_t pitch, size_t 
                         uint8_t *__restrict__ dst, int32_t *__restrict__ status, const uint64_t *__restrict__ in_bases,
                         const uint64_t *__restrict__ out_bases, uint32_t poly, uint32_t marker) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    static_assert(TILES_PER_CS % UNIT == 0, "a workgroup's tiles stay in one chunkset");
+    constexpr int DW = 4;
+    constexpr uint32_t T = TILES<DW>;
+    static_assert(T % UNIT == 0, "a workgroup's tiles stay in one chunkset");
     constexpr uint32_t phase = 0;  // aligned decode loads measured slower (+3…+5 %)
-    const uint32_t t0 = blockIdx.x * UNIT, cs = t0 / TILES_PER_CS, tile0 = t0 % TILES_PER_CS;
+    const uint32_t t0 = blockIdx.x * UNIT, cs = t0 / T, tile0 = t0 % T;
     if (cs >= n) return;
     const uint32_t *pw = reinterpret_cast<const uint32_t *>(plan + cs);
     const uint32_t w0 = __builtin_amdgcn_readfirstlane(pw[0]);
@@ -441,16 +463,16 @@ void rlnc_decode_kernel(const uint8_t *__restrict__ coded, size_t pitch, size_t 
         ibase = coded + (size_t)cs * N * pitch;
         obase = dst + (size_t)cs * CS;
     }
-    uint4 x[K];
-    if constexpr (DECDS_PREFETCH_FIRST) load_block<K>(x, ibase, ioff, tile_col(tile0, tile0 + UNIT, phase));
+    Vec<DW> x[K];
+    if constexpr (DECDS_PREFETCH_FIRST) load_block<K, DW>(x, ibase, ioff, tile_col<DW>(tile0, tile0 + UNIT, phase));
     build_tables<K, K>(lds, cw, poly);
     lds_barrier();
     if (tile0 == 0) {  // the whole workgroup: one pass over the edge columns
         // piece 9's must decode to marker || zeros (rlnc get_decoded_data strips them; a mismatch
         // is a repairing failure, chunkset.rs:202-204)
         bool ok = true;
-        for (uint32_t idx = threadIdx.x; idx < edge_cols(phase) * K; idx += WG) {
-            const uint32_t i = idx % K, col = edge_col(idx / K, phase);
+        for (uint32_t idx = threadIdx.x; idx < edge_cols<DW>(phase) * K; idx += WG) {
+            const uint32_t i = idx % K, col = edge_col<DW>(idx / K, phase);
             uint32_t z = 0;
 #pragma unroll
             for (uint32_t k = 0; k < K; k++) z ^= tbl_mul(lds, k, i, ibase[ioff[k] + col]);
@@ -462,7 +484,7 @@ void rlnc_decode_kernel(const uint8_t *__restrict__ coded, size_t pitch, size_t 
         }
         if (__any(!ok) && (threadIdx.x & 63u) == 0) status[cs] = 6;  // DECDS_ERR_CHUNKSET_REPAIRING_FAILED
     }
-    stream_range<K, K, DECDS_PREFETCH_FIRST>(tile0, tile0 + UNIT, phase, ibase, ioff, obase, ooff, x);
+    stream_range<K, K, DW, DECDS_PREFETCH_FIRST>(tile0, tile0 + UNIT, phase, ibase, ioff, obase, ooff, x);
 }
 
 // One wave per chunkset. Replays rlnc's incremental rank test over the candidates' 10-byte coding
@@ -618,17 +640,29 @@ __global__ void fill_random_bytes_kernel(uint64_t seed, uint64_t off, uint8_t *d
 }
 
 // ------------------------------------------------------------------------------ launchers ----
-// Column phase of the coded rows' payloads (edge_col): with a 16-byte-aligned pitch every row's
-// payload (row + 10) has the same alignment, and encode blocks starting `phase` columns in store
-// 16-byte aligned (-2…-3 %). Other pitches keep phase 0.
+// Column phase of the coded rows' payloads (edge_col): with a pitch that is a multiple of the
+// lane-block width every row's payload (row + 10) has the same alignment, and encode blocks starting
+// `phase` columns in store aligned. Other pitches keep phase 0.
+template <int DW>
 static uint32_t row_phase(const uint8_t *rows, size_t pitch) {
-    if (pitch % 16) return 0;
-    return (uint32_t)((16 - ((uintptr_t)rows + K) % 16) % 16);
+    constexpr uint32_t C = 4 * DW;
+    if (pitch % C) return 0;
+    return (uint32_t)((C - ((uintptr_t)rows + K) % C) % C);
 }
 
+// encode lane-block width and waves per SIMD: 16-column blocks, 2 waves (254 VGPRs). 8-column
+// blocks at 3 waves per SIMD (168 VGPRs) measured no faster at any unit size (r02g).
+#ifndef DECDS_ENC_DW
+#define DECDS_ENC_DW 4
+#endif
+#ifndef DECDS_ENC_WAVES
+#define DECDS_ENC_WAVES 2
+#endif
+#define ENC_BIG rlnc_encode_kernel<ENC_UNIT, DECDS_ENC_ORDER != 0, DECDS_ENC_DW, DECDS_ENC_WAVES>
+#define ENC_SMALL rlnc_encode_kernel<1, false, DECDS_ENC_DW, DECDS_ENC_WAVES>
+
 hipError_t configure_kernels() {
-    const void *fns[] = {reinterpret_cast<const void *>(rlnc_encode_kernel<ENC_UNIT, DECDS_ENC_ORDER != 0>),
-                         reinterpret_cast<const void *>(rlnc_encode_kernel<1, false>),
+    const void *fns[] = {reinterpret_cast<const void *>(ENC_BIG), reinterpret_cast<const void *>(ENC_SMALL),
                          reinterpret_cast<const void *>(rlnc_decode_kernel<DEC_UNIT>)};
     for (const void *f : fns) {
         hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
@@ -640,13 +674,14 @@ hipError_t configure_kernels() {
 hipError_t launch_encode(const LaunchGeom &, const uint8_t *src, size_t n, const uint8_t *coeffs, uint8_t *dst,
                          size_t pitch, uint32_t poly, uint32_t marker, hipStream_t stream) {
     if (n == 0) return hipSuccess;
-    const uint32_t phase = row_phase(dst, pitch);
+    const uint32_t phase = row_phase<DECDS_ENC_DW>(dst, pitch);
+    constexpr uint32_t T = TILES<DECDS_ENC_DW>;
     if (n <= ENC_SMALL_N)
-        hipLaunchKernelGGL((rlnc_encode_kernel<1, false>), dim3((uint32_t)(n * TILES_PER_CS)), dim3(WG), LDS_BYTES, stream,
-                           src, n, coeffs, dst, pitch, phase, poly, marker);
+        hipLaunchKernelGGL((ENC_SMALL), dim3((uint32_t)(n * T)), dim3(WG), LDS_BYTES, stream, src, n, coeffs, dst, pitch,
+                           phase, poly, marker);
     else
-        hipLaunchKernelGGL((rlnc_encode_kernel<ENC_UNIT, DECDS_ENC_ORDER != 0>), dim3((uint32_t)(n * (TILES_PER_CS / ENC_UNIT))),
-                           dim3(WG), LDS_BYTES, stream, src, n, coeffs, dst, pitch, phase, poly, marker);
+        hipLaunchKernelGGL((ENC_BIG), dim3((uint32_t)(n * (T / ENC_UNIT))), dim3(WG), LDS_BYTES, stream, src, n, coeffs,
+                           dst, pitch, phase, poly, marker);
     return hipGetLastError();
 }
 
@@ -665,7 +700,7 @@ hipError_t launch_decode(const LaunchGeom &, const uint8_t *coded, size_t pitch,
     const RepairPlan *pl = reinterpret_cast<const RepairPlan *>(plan);
     auto go = [&](auto unit) {
         constexpr uint32_t U = decltype(unit)::value;
-        hipLaunchKernelGGL(rlnc_decode_kernel<U>, dim3((uint32_t)(n * (TILES_PER_CS / U))), dim3(WG), LDS_BYTES,
+        hipLaunchKernelGGL(rlnc_decode_kernel<U>, dim3((uint32_t)(n * (TILES<4> / U))), dim3(WG), LDS_BYTES,
                            stream, coded, pitch, n, pl, dst, status, in_bases, out_bases, poly, marker);
         return hipGetLastError();
     };

@@ -248,6 +248,7 @@ int main(int argc, char **argv) {
         CODEC_ATTR(10, 16, 4, 0, 1); CODEC_ATTR(10, 16, 4, 0, 0); CODEC_ATTR(10, 16, 1, 0, 0); CODEC_ATTR(10, 16, 2, 0, 1);
         CODEC_ATTR(10, 16, 1, 0, 1); CODEC_ATTR(10, 16, 8, 0, 1); CODEC_ATTR(10, 16, 1, 0, 2); CODEC_ATTR(10, 16, 4, 0, 2);
         CODEC_ATTR(10, 16, 4, 1, 1); CODEC_ATTR(10, 10, 8, 0, 0); CODEC_ATTR(10, 10, 2, 0, 0);
+        CODEC_ATTR(10, 10, 1, 0, 0); CODEC_ATTR(10, 16, 2, 0, 0);
         for (size_t n : {103, 256}) {
             const size_t src_b = n * CSB, dst_b = n * 16 * FB;
             if (src_b > bytes || dst_b > bytes) continue;
@@ -278,6 +279,18 @@ int main(int argc, char **argv) {
             ENCA("enc_u4_xcd_outA256", LB, 0, 1048832, 0);
             ENCA("enc_u4_xcd_bothA16", 1 << 20, 0, 1048592, 16);
 #undef ENCA
+            // aligned output rows (payload 256-B aligned) at units 1 / 2 / 4 and 2 / 4 / many workgroups per CU
+#define ENCB(name, U, ORD, G, LB_) \
+    std::snprintf(cfg, sizeof cfg, "%zu cs, unit %d, order %d, out 1048832+0, LDS %u", n, U, ORD, (unsigned)(LB_)); \
+    run(name, cfg, moved, [&] { codec_k<10, 16, U, 0, ORD><<<G, 256, LB_>>>(src, CSB, LB, 0, dst, 16 * 1048832, 1048832, 0, n); }, a)
+            ENCB("encA_u1_disp_2wg", 1, 0, g1, LDS);
+            ENCB("encA_u1_disp_4wg", 1, 0, g1, LDS / 2);
+            ENCB("encA_u1_disp_max", 1, 0, g1, 0);
+            ENCB("encA_u2_disp_2wg", 2, 0, g2, LDS);
+            ENCB("encA_u4_disp_2wg", 4, 0, g4, LDS);
+            ENCB("encA_u4_xcd_2wg", 4, 1, g4, LDS);
+            ENCB("encA_u4_xcd_4wg", 4, 1, g4, LDS / 2);
+#undef ENCB
             std::snprintf(cfg, sizeof cfg, "%zu cs, unit 1, order 0, both aligned", n);
             run("enc_u1_disp_bothA16", cfg, moved, [&] { codec_k<10, 16, 1, 0, 0><<<g1, 256, LDS>>>(src, CSB, 1 << 20, 0, dst, 16 * 1048592, 1048592, 16, n); }, a);
             const size_t FA = (FB + 255) & ~(size_t)255;
@@ -292,6 +305,12 @@ int main(int argc, char **argv) {
             run("dec_u8_inA16", cfg, dmoved, [&] { codec_k<10, 10, 8, 0, 0><<<g8, 256, LDS>>>(dst, 16 * 1048592, 1048592, 16, reinterpret_cast<uint8_t *>(s), CSB, LB, 0, n); }, a);
             std::snprintf(cfg, sizeof cfg, "%zu cs, unit 8, output pieces 1 MiB apart (aligned stores)", n);
             run("dec_u8_outA", cfg, dmoved, [&] { codec_k<10, 10, 8, 0, 0><<<g8, 256, LDS>>>(dst, 16 * FB, FB, 10, reinterpret_cast<uint8_t *>(s), CSB, 1 << 20, 0, n); }, a);
+            std::snprintf(cfg, sizeof cfg, "%zu cs, unit 1, output pieces 1 MiB apart, 2 / 4 WG per CU", n);
+            run("dec_u1_outA_2wg", cfg, dmoved, [&] { codec_k<10, 10, 1, 0, 0><<<g1, 256, LDS>>>(dst, 16 * FB, FB, 10, reinterpret_cast<uint8_t *>(s), CSB, 1 << 20, 0, n); }, a);
+            run("dec_u1_outA_4wg", cfg, dmoved, [&] { codec_k<10, 10, 1, 0, 0><<<g1, 256, LDS / 2>>>(dst, 16 * FB, FB, 10, reinterpret_cast<uint8_t *>(s), CSB, 1 << 20, 0, n); }, a);
+            std::snprintf(cfg, sizeof cfg, "%zu cs, unit 1, 2 / 4 WG per CU", n);
+            run("dec_u1_2wg", cfg, dmoved, [&] { codec_k<10, 10, 1, 0, 0><<<g1, 256, LDS>>>(dst, 16 * FB, FB, 10, reinterpret_cast<uint8_t *>(s), CSB, LB, 0, n); }, a);
+            run("dec_u1_4wg", cfg, dmoved, [&] { codec_k<10, 10, 1, 0, 0><<<g1, 256, LDS / 2>>>(dst, 16 * FB, FB, 10, reinterpret_cast<uint8_t *>(s), CSB, LB, 0, n); }, a);
             std::snprintf(cfg, sizeof cfg, "%zu cs, unit 2, order 0, 2 WG/CU", n);
             run("dec_u2", cfg, dmoved, [&] { codec_k<10, 10, 2, 0, 0><<<g2, 256, LDS>>>(dst, 16 * FB, FB, 10, reinterpret_cast<uint8_t *>(s), CSB, LB, 0, n); }, a);
         }

@@ -20,4 +20,7 @@ for n in 103 1639; do grep -h tag $out/ab$n.jsonl; done | python -c "
 import sys,json
 for l in sys.stdin:
     d=json.loads(l); print('%-24s n=%5d enc %.4f (%.0f GB/s) dec %.4f (%.0f GB/s) step %.4f' % (d['tag'], d['n'], d['encode_ms'], d['encode_GBps'], d['decode_ms'], d['decode_GBps'], d['encode_ms']+d['plan_ms']+d['decode_ms']))"
+timeout -k 10 300 python -u tools/mirror_bench.py > $out/mirror.jsonl 2> $out/mirror.err || { echo mirror_bench failed; tail $out/mirror.err; exit 6; }
+cat $out/mirror.jsonl
+timeout -k 10 300 tools/bin/hbmbench --gib 4 --only codec > $out/hbm.jsonl 2> $out/hbm.err || { echo hbmbench failed; exit 5; }
 echo session-ok
