@@ -72,6 +72,15 @@ __device__ __forceinline__ uint32_t gf_mul(uint32_t a, uint32_t b, uint32_t poly
     return acc & 0xFFu;
 }
 
+// A wave-uniform 64-bit value in SGPRs. __builtin_amdgcn_readfirstlane returns int: each half goes
+// back through uint32_t, or a low half with bit 31 set would sign-extend into the high half (an
+// address above 2 GiB within its 4 GiB window became 0xFFFFFFFF'xxxxxxxx: GPUTEST r02i).
+__device__ __forceinline__ uint64_t uniform_u64(uint64_t v) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return ((uint64_t)hi << 32) | lo;
+}
+
 // Workgroup barrier for the LDS tables only: every wave's LDS accesses have completed, nothing
 // else. __syncthreads() also drains each wave's outstanding global stores (a release fence).
 __device__ __forceinline__ void lds_barrier() {
@@ -453,12 +462,8 @@ void rlnc_decode_kernel(const uint8_t *__restrict__ coded, size_t pitch, size_t 
     const uint8_t *ibase;
     uint8_t *obase;
     if (in_bases) {
-        const uint64_t ib = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(in_bases[cs] >> 32)) << 32) |
-                            __builtin_amdgcn_readfirstlane((uint32_t)in_bases[cs]);
-        const uint64_t ob = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(out_bases[cs] >> 32)) << 32) |
-                            __builtin_amdgcn_readfirstlane((uint32_t)out_bases[cs]);
-        ibase = reinterpret_cast<const uint8_t *>(ib);
-        obase = reinterpret_cast<uint8_t *>(ob);
+        ibase = reinterpret_cast<const uint8_t *>(uniform_u64(in_bases[cs]));
+        obase = reinterpret_cast<uint8_t *>(uniform_u64(out_bases[cs]));
     } else {
         ibase = coded + (size_t)cs * N * pitch;
         obase = dst + (size_t)cs * CS;

@@ -182,3 +182,37 @@ def test_repairing_blob_all_chunks_shuffled_batch_vs_sequential(ctx):
             assert rep.get_repaired_chunkset(c) == data[c * CS:min(blob_len, (c + 1) * CS)].tobytes(), c
     # after everything is repaired, every further chunk is rejected as already repaired
     assert set(bat.add_chunks(arrivals[:20]).tolist()) == {10}
+
+
+def test_repairing_blob_cfg2_slots_span_4gib_windows(ctx):
+    # cfg2 through RepairingBlob: 103 chunksets, 10 random survivors each, validated in device batches
+    # and decoded from per-chunkset device slots (gather form). The 103 slots span > 2 GiB of slabs, so
+    # some slot addresses have bit 31 of their low word set: r02i's fault (a sign-extended
+    # readfirstlane in the gather addressing) is hit deterministically here.
+    blob_len = 1 << 30
+    data, _, blob = _blob(ctx, blob_len, 0x6B60)
+    header = blob.get_blob_header()
+    n = header.get_num_chunksets()
+    assert n == 103
+    rng = np.random.default_rng(0x6B61)
+    plen = blob.proof_len()
+    rows = np.empty((n * K, F), np.uint8)
+    ids = np.empty((n * K, 2), np.uint64)
+    proofs = np.empty((n * K, plen * 32), np.uint8)
+    for c in range(n):
+        for a, j in enumerate(rng.permutation(N)[:K].tolist()):
+            ch = blob.get_chunk(c, j)
+            r = c * K + a
+            rows[r] = np.frombuffer(ch.erasure_coded_data, np.uint8)
+            ids[r] = (c, ch.chunk_id)
+            proofs[r] = np.frombuffer(b"".join(ch.proof), np.uint8)
+    rep = decds_amd.RepairingBlob(ctx, header)
+    st = rep.add_rows(rows, ids, proofs, plen)
+    del rows
+    assert set(st.tolist()) <= {0, 4}  # accepted, or not useful (a dependent survivor)
+    out = decds_amd.HostBuffer(CS)
+    for c in range(n):
+        if not rep.is_chunkset_ready_to_repair(c):
+            continue
+        got = rep.get_repaired_chunkset(c, out=out.array)
+        assert np.array_equal(got, data[c * CS:min(blob_len, (c + 1) * CS)]), c
