@@ -13,7 +13,10 @@ handling, but Blob::new / RepairingBlob run as device batches:
 The reference reads shares 0..15 per chunkset and stops once the chunkset is ready; invalid,
 unparsable and undecodable chunks are skipped (handle_repair.rs:57-76). Here every present share
 is read and validated, and the plan replays the same arrival order, so the accepted chunks are
-the ones the reference would accept.
+the ones the reference would accept. A share whose chunk claims ANOTHER chunkset's id is routed by
+the reference to that chunkset (blob.rs:374-379) — or ends the repair, when that chunkset is already
+repaired or out of range — so when the batched pass meets one, the repair is redone by the
+reference's own sequential loop over the incremental RepairingBlob (repair_blob_sequential).
 """
 import ctypes
 import os
@@ -154,7 +157,68 @@ def read_blob_metadata(chunk_dir):
     return h
 
 
+class _ForeignChunk(Exception):
+    """a parsed share claims another chunkset's id: only the sequential loop reproduces the reference"""
+
+
+def repair_blob_sequential(ctx, chunk_dir, target_dir):
+    """handle_repair.rs:41-92 exactly: chunkset directories in order, shares 0..15 of each until the
+    chunkset is ready, every parsed chunk through RepairingBlob::add_chunk (the C-ABI incremental
+    object: routing by the chunk's own chunkset id, validation, rank test), InvalidProofInChunk /
+    InvalidChunkMetadata / ChunkDecodingFailed ignored and any other error fatal (the reference
+    exits 1), then get_repaired_chunkset; finally repaired.data and its digest check."""
+    from .blob import RepairingBlob
+    header = read_blob_metadata(chunk_dir)
+    n = header.get_num_chunksets()
+    rep = RepairingBlob(ctx, header)
+    os.makedirs(target_dir, exist_ok=True)
+    parts = []
+    for c in range(n):
+        for j in range(N):
+            if rep.is_chunkset_ready_to_repair(c):
+                break
+            path = os.path.join(chunk_dir, "chunkset.%d" % c, "share%02d.data" % j)
+            if not os.path.isfile(path):
+                continue
+            try:
+                raw = open(path, "rb").read()
+                chunk, used = wire.pcc_from_bytes(raw)
+            except (OSError, DecdsError):
+                continue                                               # unreadable: skipped (utils.rs:47-65)
+            if used != len(raw):
+                continue
+            try:
+                rep.add_chunk(chunk)
+            except DecdsError as e:
+                if e.kind not in ("InvalidProofInChunk", "InvalidChunkMetadata", "ChunkDecodingFailed"):
+                    raise                                              # handle_repair.rs:64-67: exit(1)
+        if not rep.is_chunkset_ready_to_repair(c):
+            raise DecdsError(5, "failed to repair chunkset %d" % c)    # handle_repair.rs:77-80
+        data = rep.get_repaired_chunkset(c)
+        with open(os.path.join(target_dir, "chunkset.%d.data" % c), "wb") as f:
+            f.write(data)
+        parts.append(data)
+    out_path = os.path.join(target_dir, "repaired.data")
+    blob = b"".join(parts)
+    with open(out_path, "wb") as f:
+        f.write(blob)
+    if _blake3(np.frombuffer(blob, np.uint8)) != header.get_blob_digest():   # handle_repair.rs:129-151
+        raise DecdsError(6, "repaired blob digest does not match the header")
+    return out_path
+
+
 def repair_blob(ctx, chunk_dir, target_dir, batch=64, timings=None, threads=16):
+    """handle_repair over device batches (see _repair_batched); falls back to the reference's
+    sequential loop (repair_blob_sequential) when a share claims another chunkset's id."""
+    try:
+        return _repair_batched(ctx, chunk_dir, target_dir, batch, timings, threads)
+    except _ForeignChunk:
+        if timings is not None:
+            timings["sequential"] = True
+        return repair_blob_sequential(ctx, chunk_dir, target_dir)
+
+
+def _repair_batched(ctx, chunk_dir, target_dir, batch, timings, threads):
     """handle_repair over device batches. Returns the repaired bytes' path; raises DecdsError if a
     chunkset cannot be repaired or the repaired digest differs (handle_repair.rs:79-84, 129-151).
     Share files are read and parsed by `threads` workers straight into a page-locked staging
@@ -189,6 +253,7 @@ def repair_blob(ctx, chunk_dir, target_dir, batch=64, timings=None, threads=16):
         verd = torch.empty(bmax * N, dtype=torch.int8, device=dev)
         status = torch.empty(bmax, dtype=torch.int32, device=dev)
     t_read = t_dev = 0.0
+    foreign = [False]
 
     def read_chunkset(c0, s):                                          # handle_repair.rs:53-76
         cs, ch = ctypes.c_uint64(), ctypes.c_uint64()
@@ -206,6 +271,8 @@ def repair_blob(ctx, chunk_dir, target_dir, batch=64, timings=None, threads=16):
             src = (ctypes.c_char * len(raw)).from_buffer(raw)
             st = lib().decds_pcc_from_bytes(src, len(raw), ctypes.byref(cs), ctypes.byref(ch), ctypes.byref(dp),
                                             ctypes.byref(dl), ctypes.byref(pp), ctypes.byref(pl), ctypes.byref(used))
+            if st == 0 and used.value == len(raw) and cs.value != c0 + s:
+                foreign[0] = True                                      # routed elsewhere by the reference
             if st != 0 or used.value != len(raw) or dl.value != F or pl.value != plen:
                 continue                                               # unreadable / malformed: skipped
             base = ctypes.addressof(src)
@@ -221,6 +288,9 @@ def repair_blob(ctx, chunk_dir, target_dir, batch=64, timings=None, threads=16):
             t0 = time.perf_counter()
             list(pool.map(lambda s: read_chunkset(c0, s), range(b)))
             t_read += time.perf_counter() - t0
+            if foreign[0]:
+                stream.synchronize()
+                raise _ForeignChunk()
             t0 = time.perf_counter()
             m = b * N
             with torch.cuda.stream(stream):
@@ -230,8 +300,6 @@ def repair_blob(ctx, chunk_dir, target_dir, batch=64, timings=None, threads=16):
                 codec.validate_batch(ctx, rows_d, m, ids_d, prf_d, plen, roots_d, n, dig, valid, blob_root=broot_d,
                                      stream=stream)
                 v = valid[:m].cpu().numpy().astype(bool)
-                # RepairingBlob::add_chunk routes by the chunk's own chunkset id (blob.rs:374-379): a
-                # valid chunk in another chunkset's directory is kept only in its own directory
                 cand = np.full((b, N), NO_CANDIDATE, np.uint8)
                 for s in range(b):
                     ok = np.nonzero(filled[s * N:(s + 1) * N] & v[s * N:(s + 1) * N]

@@ -91,3 +91,25 @@ def test_metadata_with_trailing_bytes_is_rejected(ctx, tmp_path):
     with pytest.raises(DecdsError) as e:
         files.read_blob_metadata(str(d))
     assert e.value.kind == "BlobHeaderDeserializationFailed"
+
+
+def test_repair_foreign_shares_follow_the_reference(ctx, tmp_path):
+    # handle_repair.rs:41-92 + blob.rs:373-394: a chunk is routed by its OWN chunkset id. A share of
+    # chunkset 2 found in chunkset 0's directory goes to chunkset 2 (its own copy later is then not
+    # useful: ignored) and the repair succeeds; the same result as the batched pass, by the
+    # sequential loop the batched pass falls back to.
+    size = 2 * CS + 4321
+    blob, header, d = _broken(ctx, tmp_path, size, 0xF55E)
+    share = lambda c, j: os.path.join(d, "chunkset.%d" % c, "share%02d.data" % j)
+    open(share(0, 0), "wb").write(open(share(2, 5), "rb").read())
+    for j in range(1, 4):
+        os.remove(share(2, j))                                         # chunkset 2 needs the foreign copy less
+    t = {}
+    path = files.repair_blob(ctx, str(d), str(tmp_path / "r1"), batch=2, timings=t)
+    assert t.get("sequential") and open(path, "rb").read() == blob.tobytes()
+    # a share of chunkset 0 in chunkset 1's directory: chunkset 0 is repaired by then, so the
+    # reference stops with ChunksetAlreadyRepaired (not one of the errors it ignores)
+    open(share(1, 3), "wb").write(open(share(0, 7), "rb").read())
+    with pytest.raises(DecdsError) as e:
+        files.repair_blob(ctx, str(d), str(tmp_path / "r2"), batch=2)
+    assert e.value.kind == "ChunksetAlreadyRepaired"

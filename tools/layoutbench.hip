@@ -1,0 +1,164 @@
+// layoutbench.hip — does the coded-row layout in HBM bound the encode? The codec kernels' memory
+// pattern without the GF arithmetic (as tools/hbmbench.hip's codec_k: per 16-column lane block 10
+// input-row loads, then 16 output-row stores), with the coded rows in one of two layouts:
+//   rows       row j of chunkset c at (c*16 + j) * pitch (pitch 1,048,704, payload 128-B aligned):
+//              a tile's 16 row segments are 1 MiB apart — the shipped device layout
+//   tilemajor  [chunkset][tile][row][4096 B]: a tile's 16 row segments are one contiguous 64 KiB
+//              (rows are no longer contiguous; a host copy-out would gather them)
+// and the flat copy (one float4 per thread, no grid stride) as the reference ceiling. Every variant
+// is warmed for --warm-ms, then --reps launches are timed one by one; GB/s = bytes read + written.
+//
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/layoutbench.hip -o tools/bin/layoutbench
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#define CK(x)                                                            \
+    do {                                                                 \
+        hipError_t e_ = (x);                                             \
+        if (e_ != hipSuccess) {                                          \
+            std::fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e_)); \
+            std::exit(1);                                                \
+        }                                                                \
+    } while (0)
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+constexpr uint64_t CSB = 10ull << 20, LB = (CSB + 10) / 10, FB = LB + 10, PITCH = 1048704;
+constexpr uint32_t BLOCKS = 65535, TILES = 256, TILE_COLS = 4096;
+constexpr uint64_t TM_TILE = 16ull * TILE_COLS;          // one tile of the 16 rows, tile-major
+constexpr uint64_t TM_CS = TILES * TM_TILE;               // one chunkset, tile-major (16 MiB)
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void *p) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), 0, 0x80000000u, 0x00020000);
+}
+
+// workgroup -> unit: ORDER 0 dispatcher order, 1 each XCD sweeps one contiguous eighth
+template <int ORDER>
+__device__ __forceinline__ uint32_t unit_of() {
+    uint32_t u = blockIdx.x;
+    if constexpr (ORDER == 1) {
+        const uint32_t g = gridDim.x, x = u % 8, q = u / 8, per = g / 8, rem = g % 8;
+        u = x * per + (x < rem ? x : rem) + q;
+    }
+    return u;
+}
+
+// encode pattern: inputs = pieces of the contiguous chunkset (i * L), outputs in layout TM
+template <int UNIT, int ORDER, bool TM>
+__global__ __launch_bounds__(256) void enc_k(const uint8_t *__restrict__ in, uint8_t *__restrict__ out, size_t n) {
+    const uint32_t t0 = unit_of<ORDER>() * UNIT, cs = t0 / TILES, tile0 = t0 % TILES;
+    if (cs >= n) return;
+    const auto ri = rsrc(in + cs * CSB);
+    const auto ro = rsrc(out + cs * (TM ? TM_CS : 16 * PITCH));
+    u32x4 acc = {0, 0, 0, 0};
+    for (uint32_t t = tile0; t < tile0 + UNIT; t++) {
+        const uint32_t b = t * 256 + threadIdx.x;
+        const uint32_t col = b < BLOCKS ? b * 16 : 0x80000000u;
+        u32x4 x[10];
+#pragma unroll
+        for (int i = 0; i < 10; i++) x[i] = __builtin_amdgcn_raw_buffer_load_b128(ri, (uint32_t)(i * LB) + col, 0, 0);
+#pragma unroll
+        for (int i = 0; i < 10; i++) acc ^= x[i];
+        // tilemajor: row j of tile t at t*64 KiB + j*4 KiB (+ the lane's column within the tile)
+        const uint32_t obase = TM ? (b < BLOCKS ? t * (uint32_t)TM_TILE + threadIdx.x * 16 : 0x80000000u) : 128 + col;
+#pragma unroll
+        for (int j = 0; j < 16; j++)
+            __builtin_amdgcn_raw_buffer_store_b128(acc + (uint32_t)j, ro, obase + (uint32_t)(j * (TM ? TILE_COLS : PITCH)), 0, 0);
+    }
+}
+
+// decode pattern: inputs = 10 of the 16 coded rows (rows 0, 2, 3, 5, 6, 8, 9, 11, 13, 15) in layout
+// TM, outputs = pieces of the contiguous chunkset
+template <int UNIT, bool TM>
+__global__ __launch_bounds__(256) void dec_k(const uint8_t *__restrict__ in, uint8_t *__restrict__ out, size_t n) {
+    const uint32_t t0 = blockIdx.x * UNIT, cs = t0 / TILES, tile0 = t0 % TILES;
+    if (cs >= n) return;
+    constexpr uint32_t sel[10] = {0, 2, 3, 5, 6, 8, 9, 11, 13, 15};
+    const auto ri = rsrc(in + cs * (TM ? TM_CS : 16 * PITCH));
+    const auto ro = rsrc(out + cs * CSB);
+    u32x4 acc = {0, 0, 0, 0};
+    for (uint32_t t = tile0; t < tile0 + UNIT; t++) {
+        const uint32_t b = t * 256 + threadIdx.x;
+        const uint32_t col = b < BLOCKS ? b * 16 : 0x80000000u;
+        const uint32_t ibase = TM ? (b < BLOCKS ? t * (uint32_t)TM_TILE + threadIdx.x * 16 : 0x80000000u) : 128 + col;
+        u32x4 x[10];
+#pragma unroll
+        for (int k = 0; k < 10; k++)
+            x[k] = __builtin_amdgcn_raw_buffer_load_b128(ri, ibase + sel[k] * (uint32_t)(TM ? TILE_COLS : PITCH), 0, 0);
+#pragma unroll
+        for (int k = 0; k < 10; k++) acc ^= x[k];
+#pragma unroll
+        for (int i = 0; i < 10; i++) __builtin_amdgcn_raw_buffer_store_b128(acc + (uint32_t)i, ro, (uint32_t)(i * LB) + col, 0, 0);
+    }
+}
+
+__global__ __launch_bounds__(256) void copy_flat(const u32x4 *__restrict__ s, u32x4 *__restrict__ d, size_t n16) {
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n16) d[i] = s[i];
+}
+
+struct Args {
+    int warm_ms = 400, reps = 20;
+};
+
+template <typename F>
+void run(const char *name, size_t n, double bytes, F f, const Args &a) {
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    auto t0 = std::chrono::steady_clock::now();
+    while (std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() < a.warm_ms) {
+        for (int i = 0; i < 5; i++) f();
+        CK(hipDeviceSynchronize());
+    }
+    std::vector<float> ms;
+    for (int r = 0; r < a.reps; r++) {
+        CK(hipEventRecord(e0));
+        f();
+        CK(hipEventRecord(e1));
+        CK(hipEventSynchronize(e1));
+        float t;
+        CK(hipEventElapsedTime(&t, e0, e1));
+        ms.push_back(t);
+    }
+    std::sort(ms.begin(), ms.end());
+    std::printf("{\"variant\": \"%s\", \"chunksets\": %zu, \"ms_med\": %.4f, \"GBps_med\": %.1f, \"GBps_best\": %.1f}\n", name, n,
+                ms[ms.size() / 2], bytes / ms[ms.size() / 2] / 1e6, bytes / ms[0] / 1e6);
+    std::fflush(stdout);
+    CK(hipEventDestroy(e0));
+    CK(hipEventDestroy(e1));
+}
+
+int main(int argc, char **argv) {
+    Args a;
+    for (int i = 1; i < argc; i++) {
+        if (!std::strcmp(argv[i], "--warm-ms")) a.warm_ms = std::atoi(argv[++i]);
+        if (!std::strcmp(argv[i], "--reps")) a.reps = std::atoi(argv[++i]);
+    }
+    const size_t nmax = 1024;
+    uint8_t *src, *coded, *rep;
+    CK(hipMalloc(&src, nmax * CSB + 4096));
+    CK(hipMalloc(&coded, nmax * 16 * PITCH + 4096));
+    CK(hipMalloc(&rep, nmax * CSB + 4096));
+    CK(hipMemset(src, 0x3c, nmax * CSB));
+    CK(hipMemset(coded, 0x5a, nmax * 16 * PITCH));
+    for (size_t n : {103, 256, 1024}) {
+        const double eb = (double)n * (CSB + 16 * FB), db = (double)n * (10 * FB + CSB);
+        const unsigned g4 = (unsigned)(n * TILES / 4), g1 = (unsigned)(n * TILES);
+        run("enc_rows_u4_xcd", n, eb, [&] { enc_k<4, 1, false><<<g4, 256>>>(src, coded, n); }, a);
+        run("enc_rows_u1_disp", n, eb, [&] { enc_k<1, 0, false><<<g1, 256>>>(src, coded, n); }, a);
+        run("enc_tilemajor_u4_xcd", n, eb, [&] { enc_k<4, 1, true><<<g4, 256>>>(src, coded, n); }, a);
+        run("enc_tilemajor_u1_disp", n, eb, [&] { enc_k<1, 0, true><<<g1, 256>>>(src, coded, n); }, a);
+        run("dec_rows_u1", n, db, [&] { dec_k<1, false><<<g1, 256>>>(coded, rep, n); }, a);
+        run("dec_tilemajor_u1", n, db, [&] { dec_k<1, true><<<g1, 256>>>(coded, rep, n); }, a);
+        const size_t n16 = (size_t)n * CSB / 16;
+        run("copy_flat", n, 2.0 * n * CSB, [&] { copy_flat<<<(unsigned)((n16 + 255) / 256), 256>>>((const u32x4 *)src, (u32x4 *)rep, n16); }, a);
+    }
+    CK(hipDeviceSynchronize());
+    return 0;
+}
