@@ -227,9 +227,32 @@ def main():
             cev[s + 1].record(stream)
         stream.synchronize()
         c_ms = cev[0].elapsed_time(cev[-1]) / args.steps
+        # ChunkSet::new as one call (encode + commitment, chunkset.rs:37-63): on rows 16 bytes past a
+        # 128-byte boundary the chunk hashing is fused into the encode kernel (+ commit_fold_kernel)
+        with torch.cuda.stream(stream):
+            mbuf = torch.empty(n * N * codec.CODED_PITCH_ALIGNED + 256, dtype=torch.uint8, device=dev)
+            moff = (16 - mbuf.data_ptr()) % 128
+            mcoded = mbuf[moff:moff + (n * N - 1) * codec.CODED_PITCH_ALIGNED + F]
+            ws = codec.encode_commit_workspace(n, device=dev)
+        fused = lambda: codec.encode_commit_batch(ctx, src, n, coeffs, mcoded, dig, roots, proofs, first_chunkset_id=lo,
+                                                  pitch=codec.CODED_PITCH_ALIGNED, workspace=ws, stream=stream)
+        fused()
+        fev = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
+        fev[0].record(stream)
+        for s in range(args.steps):
+            fused()
+            fev[s + 1].record(stream)
+        stream.synchronize()
+        f_ms = fev[0].elapsed_time(fev[-1]) / args.steps
+        del mbuf, mcoded, ws
         commit = {"kernels": "chunk_digest_kernel + chunkset_merkle_kernel", "ms": round(c_ms, 4),
                   "coded_GBps": round(n * N * F / (c_ms * 1e-3) / 1e9, 1),
-                  "blob_GiBps": round(n * CS / GIB / (c_ms * 1e-3), 1), "bound": "valu (BLAKE3 rotates)"}
+                  "blob_GiBps": round(n * CS / GIB / (c_ms * 1e-3), 1), "bound": "valu (BLAKE3 rotates)",
+                  "chunkset_new": {"what": "ChunkSet::new = encode + commitment (decds_encode_commit_batch)",
+                                   "separate_ms": round(enc_ms + c_ms, 4),
+                                   "fused_ms": round(f_ms, 4),
+                                   "fused_kernels": "rlnc_encode_kernel<COMMIT> + commit_fold_kernel + chunkset_merkle_kernel",
+                                   "fused_blob_GiBps": round(n * CS / GIB / (f_ms * 1e-3), 1)}}
 
     # encode batch sweep beside the headline step (north_star: "at batch >= 256"):
     # one HBM-resident 16 GiB blob, encode-only launches of its first n chunksets, HIP events on the

@@ -88,6 +88,29 @@ def commit_batch(ctx, coded, n, digests, roots, proofs, first_chunkset_id=0, pit
                                    _ptr(proofs), _stream(stream)))
 
 
+def encode_commit_workspace(n, device="cuda"):
+    import torch
+    return torch.empty(max(1, lib().decds_encode_commit_workspace_bytes(n)), dtype=torch.uint8, device=device)
+
+
+def encode_commit_batch(ctx, src, n, coeffs, dst, digests, roots, proofs, first_chunkset_id=0,
+                        pitch=CODED_PIECE_BYTES, workspace=None, stream=None):
+    """ChunkSet::new for n device-resident chunksets (chunkset.rs:37-63): encode_batch + commit_batch
+    in one call; on 16-byte-aligned rows (coded_buffer(aligned=True)) the chunk hashing is fused into
+    the encode kernel. workspace: encode_commit_workspace(n) (allocated here when None)."""
+    _need(src, n * CHUNKSET_BYTES, "src")
+    _need(coeffs, n * N * K, "coeffs")
+    _need(dst, (n * N - 1) * pitch + CODED_PIECE_BYTES, "dst")
+    _need(digests, n * N * 32, "digests")
+    _need(roots, n * 32, "roots")
+    _need(proofs, n * N * 4 * 32, "proofs")
+    if workspace is None:
+        workspace = encode_commit_workspace(n, device=dst.device)
+    _need(workspace, lib().decds_encode_commit_workspace_bytes(n), "workspace")
+    check(lib().decds_encode_commit_batch(ctx.handle, _ptr(src), n, _ptr(coeffs), _ptr(dst), pitch, first_chunkset_id,
+                                          _ptr(digests), _ptr(roots), _ptr(proofs), _ptr(workspace), _stream(stream)))
+
+
 def validate_batch(ctx, coded, n_rows, ids, proofs, proof_len, chunkset_roots, num_chunksets, digests, valid,
                    blob_root=None, pitch=CODED_PIECE_BYTES, stream=None):
     """BlobHeader::validate_chunk (blob.rs:211-215) for n_rows received device-resident rows.

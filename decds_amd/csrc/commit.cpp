@@ -9,6 +9,7 @@
 #include "blake3_impl.h"
 #include "capi_internal.h"
 #include "commit_kernels.h"
+#include "rlnc_kernels.h"
 #include "rlnc_layout.h"
 
 using namespace decds;
@@ -163,6 +164,31 @@ int decds_commit_batch(decds_ctx *ctx, const uint8_t *coded, size_t pitch, size_
     if (pitch < F) return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "coded pitch %zu < %llu", pitch, (unsigned long long)F);
     hipError_t e = launch_commit(coded, pitch, n, first_chunkset_id, digests, roots, proofs, (hipStream_t)stream);
     return e == hipSuccess ? DECDS_OK : decds_hip_error(e, "commit kernels launch");
+}
+
+size_t decds_encode_commit_workspace_bytes(size_t n) { return n * N * 64 * 32; }
+
+int decds_encode_commit_batch(decds_ctx *ctx, const uint8_t *src, size_t n, const uint8_t *coeffs, uint8_t *dst,
+                              size_t pitch, uint64_t first_chunkset_id, uint8_t *digests, uint8_t *roots,
+                              uint8_t *proofs, void *workspace, void *stream) {
+    if (!encode_commit_fusable(dst, pitch) || !n) {  // unaligned rows: encode, then the commitment kernels
+        int s = decds_encode_batch(ctx, src, n, coeffs, dst, pitch, stream);
+        return s ? s : decds_commit_batch(ctx, dst, pitch, n, first_chunkset_id, digests, roots, proofs, stream);
+    }
+    int s = decds_ctx_bind(ctx);
+    if (s) return s;
+    if (!src || !coeffs || !dst || !digests || !roots || !proofs || !workspace)
+        return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "null buffer");
+    if (n > (1u << 24)) return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "chunkset count %zu too large", n);
+    if (pitch < F || (N - 1) * (uint64_t)pitch + F >= (1ull << 31))
+        return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "coded pitch %zu outside [%llu, 2 GiB / 16)", pitch,
+                               (unsigned long long)F);
+    auto *sub = static_cast<uint32_t *>(workspace);
+    hipError_t e = launch_encode_commit(src, n, coeffs, dst, pitch, ctx->poly, ctx->marker, first_chunkset_id, sub,
+                                        (hipStream_t)stream);
+    if (e) return decds_hip_error(e, "rlnc_encode_kernel<COMMIT> launch");
+    e = launch_commit_fold(dst, pitch, n, sub, digests, roots, proofs, (hipStream_t)stream);
+    return e == hipSuccess ? DECDS_OK : decds_hip_error(e, "commit_fold_kernel launch");
 }
 
 int decds_validate_batch(decds_ctx *ctx, const uint8_t *coded, size_t pitch, size_t n_rows, const uint64_t *ids,

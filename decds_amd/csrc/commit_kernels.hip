@@ -174,6 +174,50 @@ __global__ __launch_bounds__(DG_WG) void chunk_digest_kernel(const uint8_t *__re
     }
 }
 
+// Digest of each coded row from the fused encode's 64 subtree values (rlnc_encode_kernel<COMMIT>):
+// one wave per row, lane i holds subtree i (chunks 16i .. 16i+15); six PARENT levels fold them into
+// the 1024-chunk left tree, then the 27-byte 1025th chunk joins under ROOT, as chunk_digest_kernel.
+constexpr uint32_t SUBTREES = FULL_CHUNKS / 16;  // 64
+__global__ __launch_bounds__(SUBTREES) void commit_fold_kernel(const uint8_t *__restrict__ coded, size_t pitch,
+                                                               const uint32_t *__restrict__ sub,
+                                                               uint8_t *__restrict__ digests) {
+    const size_t row = blockIdx.x;
+    const uint32_t i = threadIdx.x;
+    uint32_t cv[8];
+    const uint32_t *p = sub + (row * SUBTREES + i) * 8;
+#pragma unroll
+    for (int w = 0; w < 8; w++) cv[w] = p[w];
+#pragma unroll
+    for (uint32_t k = 0; k < 6; k++) {
+        uint32_t sib[8], lo[8], hi[8];
+        const bool right = (i >> k) & 1u;
+#pragma unroll
+        for (int w = 0; w < 8; w++) {
+            sib[w] = __shfl_xor(cv[w], 1 << k, SUBTREES);
+            lo[w] = right ? sib[w] : cv[w];
+            hi[w] = right ? cv[w] : sib[w];
+        }
+        b3::parent(lo, hi, 0, cv);
+    }
+    if (i == 0) {
+        const uint8_t *piece = coded + row * pitch;
+        uint32_t m[16], last[8], root[8];
+#pragma unroll
+        for (int w = 0; w < 16; w++) {
+            uint32_t x = 0;
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+                if (4 * w + k < (int)LAST_BYTES) x |= (uint32_t)piece[FULL_CHUNKS * b3::CHUNK - 16 + 4 * w + k] << (8 * k);
+            m[w] = x;
+        }
+        b3::compress(b3::K3.iv, m, FULL_CHUNKS, LAST_BYTES, b3::CHUNK_START | b3::CHUNK_END, last);
+        b3::parent(cv, last, b3::ROOT, root);
+        uint32_t *d = reinterpret_cast<uint32_t *>(digests + row * 32);
+#pragma unroll
+        for (int w = 0; w < 8; w++) d[w] = root[w];
+    }
+}
+
 // Merkle tree of one chunkset's 16 digests (merkle_tree.rs:23-50) and the 4-hash inclusion proof of
 // every leaf (merkle_tree.rs:75-116); 16 leaves make a complete tree, no zero-hash padding. Lane
 // j of a 16-lane group holds the node above leaf j; at level l its sibling node sits in lane
@@ -265,6 +309,17 @@ hipError_t launch_commit(const uint8_t *coded, size_t pitch, size_t n, uint64_t 
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(chunk_digest_kernel, dim3((uint32_t)(n * N)), dim3(DG_WG), 0, stream, coded, pitch,
                        first_chunkset_id, (const uint64_t *)nullptr, digests);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(chunkset_merkle_kernel, dim3((uint32_t)((n * N + MK_WG - 1) / MK_WG)), dim3(MK_WG), 0, stream,
+                       digests, n, roots, proofs);
+    return hipGetLastError();
+}
+
+hipError_t launch_commit_fold(const uint8_t *coded, size_t pitch, size_t n, const uint32_t *sub, uint8_t *digests,
+                              uint8_t *roots, uint8_t *proofs, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(commit_fold_kernel, dim3((uint32_t)(n * N)), dim3(SUBTREES), 0, stream, coded, pitch, sub, digests);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(chunkset_merkle_kernel, dim3((uint32_t)((n * N + MK_WG - 1) / MK_WG)), dim3(MK_WG), 0, stream,

@@ -24,6 +24,7 @@
 
 #include <utility>
 
+#include "blake3_impl.h"
 #include "rlnc_kernels.h"
 #include "rlnc_layout.h"
 
@@ -311,26 +312,47 @@ __device__ __forceinline__ void combine_block(Vec<DW> (&x)[NIN], uint8_t *obase,
 // written on COLS-byte boundaries); the workgroup owning tile 0 does the edge columns byte by byte:
 // e < phase is column e, the rest the columns after the last block. Piece 9's main columns must stay
 // below CS - 9L (its marker and padding are edge columns), so a phase above 7 gives up one block.
+//
+// Message tiling (phase MSG_PHASE = 6, i.e. 16-byte-aligned rows): the chunk digest's message is
+// le64 ids (16 B) || row, so payload column p is message byte p + 26 and a block starting at column
+// 16m - 26 is message block m. Tiles then start MSG_SHIFT = 2 blocks early (tile t = message blocks
+// [256t, 256t + 256), its first two lanes idle in tile 0) and the last block joins the edge columns
+// (6 head + 27 tail): a tile is exactly 4 BLAKE3 chunks of every row, which the fused commitment
+// (rlnc_encode_kernel<COMMIT>) hashes right behind the stores. On rows at 16 mod 128 every wave's
+// 1 KiB store run is then 128-byte aligned.
 constexpr uint32_t MAX_FULL_PHASE = (uint32_t)(CS - (K - 1) * L) - MAIN_COLS;
 static_assert(MAX_FULL_PHASE == 7, "layout");
 template <int DW> constexpr uint32_t COLS = 4 * DW;
 template <int DW> constexpr uint32_t BLOCKS = MAIN_COLS / COLS<DW>;                 // 65535 / 131070
 template <int DW> constexpr uint32_t TILES = (BLOCKS<DW> + TILE_BLOCKS - 1) / TILE_BLOCKS;  // 256 / 512
 static_assert(BLOCKS<4> * COLS<4> == MAIN_COLS && BLOCKS<2> * COLS<2> == MAIN_COLS, "tiling covers the main columns");
-template <int DW>
-__device__ __forceinline__ uint32_t main_blocks(uint32_t phase) { return BLOCKS<DW> - (phase > MAX_FULL_PHASE); }
-template <int DW>
-__device__ __forceinline__ uint32_t edge_cols(uint32_t phase) { return (uint32_t)L - main_blocks<DW>(phase) * COLS<DW>; }
-template <int DW>
+constexpr uint32_t MSG_PHASE = (16 - (16 + K) % 16) % 16;
+template <int DW> constexpr uint32_t MSG_SHIFT = (16 + K + MSG_PHASE) / COLS<DW>;   // 2 / 4 blocks
+template <int DW> constexpr uint32_t MSG_MAIN = (MAIN_COLS - 16) / COLS<DW>;        // 65534 / 131068
+static_assert(MSG_PHASE == 6 && MSG_PHASE < COLS<2> && MSG_SHIFT<4> * COLS<4> == 32 && MSG_SHIFT<2> * COLS<2> == 32,
+              "message block m = payload block m - MSG_SHIFT");
+static_assert((MSG_SHIFT<4> + MSG_MAIN<4>) == TILES<4> * TILE_BLOCKS && (MSG_SHIFT<2> + MSG_MAIN<2>) == TILES<2> * TILE_BLOCKS,
+              "message tiles end where the 1024 full BLAKE3 chunks end");
+// MSG (compile time): message tiling, phase fixed at MSG_PHASE; else `phase` as passed
+template <int DW, bool MSG>
+__device__ __forceinline__ uint32_t main_blocks(uint32_t phase) {
+    if constexpr (MSG) return MSG_MAIN<DW>;
+    return BLOCKS<DW> - (phase > MAX_FULL_PHASE);
+}
+template <int DW, bool MSG>
+__device__ __forceinline__ uint32_t edge_cols(uint32_t phase) { return (uint32_t)L - main_blocks<DW, MSG>(phase) * COLS<DW>; }
+template <int DW, bool MSG>
 __device__ __forceinline__ uint32_t edge_col(uint32_t e, uint32_t phase) {
-    return e < phase ? e : main_blocks<DW>(phase) * COLS<DW> + e;
+    const uint32_t ph = MSG ? MSG_PHASE : phase;
+    return e < ph ? e : main_blocks<DW, MSG>(phase) * COLS<DW> + e;
 }
 
-// this lane's first column of tile t of a range ending at tb, or out of range
-template <int DW>
+// this lane's first column of tile t of a range ending at tb, or out of range (with message tiling
+// the lanes of the two blocks before column MSG_PHASE wrap to a huge block index: out of range too)
+template <int DW, bool MSG>
 __device__ __forceinline__ uint32_t tile_col(uint32_t t, uint32_t tb, uint32_t phase) {
-    const uint32_t block = t * TILE_BLOCKS + threadIdx.x;
-    return t < tb && block < main_blocks<DW>(phase) ? block * COLS<DW> + phase : OOB_COL;
+    const uint32_t block = t * TILE_BLOCKS + threadIdx.x - (MSG ? MSG_SHIFT<DW> : 0u);
+    return t < tb && block < main_blocks<DW, MSG>(phase) ? block * COLS<DW> + (MSG ? MSG_PHASE : phase) : OOB_COL;
 }
 
 // Tiles [ta, tb) of one chunkset, branch-free: lanes past the last block use OOB_COL, so no lane
@@ -340,11 +362,11 @@ __device__ __forceinline__ uint32_t tile_col(uint32_t t, uint32_t tb, uint32_t p
 // merges paths that issued no stores and waits with vmcnt(NIN-1) for the next tile's first input:
 // every tile then waited for the previous tile's stores as well; here it waits for the inputs only.
 // HAVE: x already holds tile ta's inputs (loaded before the workgroup's table build).
-template <int NIN, int NOUT, int DW, bool HAVE>
+template <int NIN, int NOUT, int DW, bool HAVE, bool MSG = false>
 __device__ __forceinline__ void stream_range(uint32_t ta, uint32_t tb, uint32_t phase, const uint8_t *ibase,
                                              const uint32_t (&ioff)[NIN], uint8_t *obase,
                                              const uint32_t (&ooff)[NOUT], Vec<DW> (&x)[NIN]) {
-    auto col = [&](uint32_t t) { return tile_col<DW>(t, tb, phase); };
+    auto col = [&](uint32_t t) { return tile_col<DW, MSG>(t, tb, phase); };
     if constexpr (!HAVE) load_block<NIN, DW>(x, ibase, ioff, col(ta));
     asm volatile("" ::: "memory");  // keep the dropped stores after the loads, as in the loop
 #pragma unroll
@@ -368,14 +390,85 @@ __device__ __forceinline__ uint32_t xcd_eighth_unit() {
     return x * per + (x < rem ? x : rem) + q;
 }
 
+// ---- fused commitment (ChunkSet::new, chunkset.rs:43-63) ---------------------------------------
+// With message tiling a unit of 4 tiles is BLAKE3 chunks [16u, 16u + 16) of every one of the
+// chunkset's 16 rows: 256 chunks, one per lane. Right behind its own row stores (still in L2) the
+// workgroup hashes them — lane l: row l / 16, chunk 16u + l % 16, 16 compressions over 64-byte
+// blocks read back with sc0 loads (line-aligned on 16-mod-128 rows) — and folds each row's 16 chunk
+// values into their subtree (an aligned subtree of the row's 1024-chunk left tree), written to
+// sub[(row * 64 + u) * 8]. commit_fold_kernel (commit_kernels.hip) then completes every row's digest
+// (64 subtrees + the 27-byte 1025th chunk) and the Merkle trees. The hashing is VALU work that runs
+// while the CU's other workgroup streams: it overlaps the encode's HBM time instead of following it.
+constexpr uint32_t FUSED_UNITS = 64;  // units of 16 BLAKE3 chunks per row (1024 full chunks)
+struct Msg64 {
+    uint32_t w[16];
+};
+
+__device__ __forceinline__ Msg64 ld_msg(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    Msg64 m;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, off + 16 * k, 0, 1);  // sc0: bypass the L1
+        m.w[4 * k] = v.x, m.w[4 * k + 1] = v.y, m.w[4 * k + 2] = v.z, m.w[4 * k + 3] = v.w;
+    }
+    return m;
+}
+
+__device__ __forceinline__ void hash_unit(uint8_t *obase, size_t pitch, uint32_t u, uint64_t cs_id,
+                                          uint32_t *__restrict__ sub_cs) {
+    __syncthreads();  // s_waitcnt vmcnt(0) + barrier: every row store of this workgroup is in L2
+    const uint32_t l = threadIdx.x, j = l >> 4, q = l & 15u, c = u * 16 + q;
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(obase, 0, BUF_RECORDS, 0x00020000);
+    // message byte 1024c of row j sits at row + 1024c - 16; for c == 0 the first 16 bytes are the ids
+    // (that offset wraps past the descriptor's range for row 0: the load returns zeros, replaced below)
+    const uint32_t off = (uint32_t)(j * pitch) + c * b3::CHUNK - 16u;
+    uint32_t cv[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) cv[i] = b3::K3.iv[i];
+    Msg64 m = ld_msg(r, off);
+    if (c == 0) {
+        const uint64_t chunk_id = cs_id * N + j;  // chunkset.rs:47
+        m.w[0] = (uint32_t)cs_id, m.w[1] = (uint32_t)(cs_id >> 32);
+        m.w[2] = (uint32_t)chunk_id, m.w[3] = (uint32_t)(chunk_id >> 32);
+    }
+#pragma unroll 1
+    for (uint32_t b = 0; b < 16; b++) {
+        const Msg64 nxt = ld_msg(r, off + b3::BLOCK * (b < 15 ? b + 1 : b));  // in flight across the compression
+        const uint32_t flags = (b == 0 ? b3::CHUNK_START : 0u) | (b == 15 ? b3::CHUNK_END : 0u);
+        b3::compress(cv, m.w, c, b3::BLOCK, flags, cv);
+        m = nxt;
+    }
+    // 16 chunks of row j (lanes 16j .. 16j+15) -> their subtree: level k pairs lanes q, q ^ 2^k
+#pragma unroll
+    for (uint32_t k = 0; k < 4; k++) {
+        uint32_t sib[8], lo[8], hi[8];
+        const bool right = (q >> k) & 1u;
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            sib[i] = __shfl_xor(cv[i], 1 << k, 16);
+            lo[i] = right ? sib[i] : cv[i];
+            hi[i] = right ? cv[i] : sib[i];
+        }
+        b3::parent(lo, hi, 0, cv);
+    }
+    if (q == 0) {
+        uint32_t *o = sub_cs + (j * FUSED_UNITS + u) * 8;
+#pragma unroll
+        for (int i = 0; i < 8; i++) o[i] = cv[i];
+    }
+}
+
 // Encode: workgroup = UNIT consecutive tiles of one chunkset (TILES<DW> tiles per chunkset).
 // The unit is walked as "segments up to the next chunkset boundary" although it never crosses one
 // (UNIT divides TILES): with that loop hipcc allocated 228 VGPRs and no spills, the straight-line
 // form of the same work 256 VGPRs + 53 spilled (-Rpass-analysis=kernel-resource-usage).
-template <uint32_t UNIT, bool XCD_ORDER, int DW, int WAVES>
+// COMMIT (UNIT 4, DW 4, message tiling): hash_unit after the unit's tiles; first_id = the batch's
+// first chunkset id, sub = n x 16 x 64 subtree chaining values.
+template <uint32_t UNIT, bool XCD_ORDER, int DW, int WAVES, bool MSG, bool COMMIT = false>
 __global__ __launch_bounds__(WG, WAVES) __attribute__((amdgpu_waves_per_eu(WAVES, WAVES)))
 void rlnc_encode_kernel(const uint8_t *__restrict__ src, size_t n, const uint8_t *__restrict__ coeffs,
-                        uint8_t *__restrict__ dst, size_t pitch, uint32_t phase, uint32_t poly, uint32_t marker) {
+                        uint8_t *__restrict__ dst, size_t pitch, uint32_t phase, uint32_t poly, uint32_t marker,
+                        uint64_t first_id, uint32_t *__restrict__ sub) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     constexpr uint32_t T = TILES<DW>;
     static_assert(T % UNIT == 0, "a workgroup's tiles stay in one chunkset");
@@ -393,7 +486,7 @@ void rlnc_encode_kernel(const uint8_t *__restrict__ src, size_t n, const uint8_t
         const uint32_t cw = table_coeffs<K, N>(M, K);
         // the first tile's loads, in flight across the table build (issued after the coefficient loads;
         // issuing them first, so both latencies overlap, measured no faster: r02h)
-        if constexpr (DECDS_PREFETCH_FIRST) load_block<K, DW>(x, ibase, ioff, tile_col<DW>(tile0, te - cs * T, phase));
+        if constexpr (DECDS_PREFETCH_FIRST) load_block<K, DW>(x, ibase, ioff, tile_col<DW, MSG>(tile0, te - cs * T, phase));
         lds_barrier();
         build_tables<K, N>(lds, cw, poly);
         lds_barrier();
@@ -401,8 +494,8 @@ void rlnc_encode_kernel(const uint8_t *__restrict__ src, size_t n, const uint8_t
             // coding-vector prefix of the 16 full coded pieces (rlnc layout: cv || payload)
             for (uint32_t idx = threadIdx.x; idx < N * K; idx += WG) obase[(idx / K) * pitch + idx % K] = M[idx];
             // piece 9 carries the boundary marker, then zero padding (Encoder::new, chunkset.rs:43)
-            for (uint32_t idx = threadIdx.x; idx < edge_cols<DW>(phase) * N; idx += WG) {
-                const uint32_t j = idx % N, col = edge_col<DW>(idx / N, phase);
+            for (uint32_t idx = threadIdx.x; idx < edge_cols<DW, MSG>(phase) * N; idx += WG) {
+                const uint32_t j = idx % N, col = edge_col<DW, MSG>(idx / N, phase);
                 uint32_t y = 0;
 #pragma unroll
                 for (uint32_t i = 0; i < K; i++) {
@@ -413,16 +506,26 @@ void rlnc_encode_kernel(const uint8_t *__restrict__ src, size_t n, const uint8_t
                 obase[j * pitch + K + col] = (uint8_t)y;
             }
         }
-        stream_range<K, N, DW, DECDS_PREFETCH_FIRST>(tile0, te - cs * T, phase, ibase, ioff, obase, ooff, x);
+        stream_range<K, N, DW, DECDS_PREFETCH_FIRST, MSG>(tile0, te - cs * T, phase, ibase, ioff, obase, ooff, x);
     };
     const uint64_t total = (uint64_t)n * T;
     uint32_t t0 = (XCD_ORDER ? xcd_eighth_unit() : blockIdx.x) * UNIT;
     const uint32_t t1 = (uint32_t)(t0 + UNIT < total ? t0 + UNIT : total);
+    [[maybe_unused]] const uint32_t unit0 = t0;
     while (t0 < t1) {
         const uint32_t cs_end = (t0 / T + 1) * T;
         const uint32_t te = cs_end < t1 ? cs_end : t1;
         segment(t0, te);
         t0 = te;
+    }
+    if constexpr (COMMIT) {
+        static_assert(MSG && UNIT * TILE_BLOCKS * COLS<DW> == 16 * b3::CHUNK && T / UNIT == FUSED_UNITS,
+                      "a commit unit is 16 BLAKE3 chunks of every row");
+        if (unit0 < t1) {
+            const uint32_t cs = unit0 / T;
+            hash_unit(dst + (size_t)cs * N * pitch, pitch, (unit0 % T) / UNIT, first_id + cs,
+                      sub + (size_t)cs * N * FUSED_UNITS * 8);
+        }
     }
 }
 
@@ -469,15 +572,15 @@ void rlnc_decode_kernel(const uint8_t *__restrict__ coded, size_t pitch, size_t 
         obase = dst + (size_t)cs * CS;
     }
     Vec<DW> x[K];
-    if constexpr (DECDS_PREFETCH_FIRST) load_block<K, DW>(x, ibase, ioff, tile_col<DW>(tile0, tile0 + UNIT, phase));
+    if constexpr (DECDS_PREFETCH_FIRST) load_block<K, DW>(x, ibase, ioff, tile_col<DW, false>(tile0, tile0 + UNIT, phase));
     build_tables<K, K>(lds, cw, poly);
     lds_barrier();
     if (tile0 == 0) {  // the whole workgroup: one pass over the edge columns
         // piece 9's must decode to marker || zeros (rlnc get_decoded_data strips them; a mismatch
         // is a repairing failure, chunkset.rs:202-204)
         bool ok = true;
-        for (uint32_t idx = threadIdx.x; idx < edge_cols<DW>(phase) * K; idx += WG) {
-            const uint32_t i = idx % K, col = edge_col<DW>(idx / K, phase);
+        for (uint32_t idx = threadIdx.x; idx < edge_cols<DW, false>(phase) * K; idx += WG) {
+            const uint32_t i = idx % K, col = edge_col<DW, false>(idx / K, phase);
             uint32_t z = 0;
 #pragma unroll
             for (uint32_t k = 0; k < K; k++) z ^= tbl_mul(lds, k, i, ibase[ioff[k] + col]);
@@ -663,11 +766,22 @@ static uint32_t row_phase(const uint8_t *rows, size_t pitch) {
 #ifndef DECDS_ENC_WAVES
 #define DECDS_ENC_WAVES 2
 #endif
-#define ENC_BIG rlnc_encode_kernel<ENC_UNIT, DECDS_ENC_ORDER != 0, DECDS_ENC_DW, DECDS_ENC_WAVES>
-#define ENC_SMALL rlnc_encode_kernel<1, false, DECDS_ENC_DW, DECDS_ENC_WAVES>
+#define ENC_KERNEL(UNIT, ORDER, MSG) rlnc_encode_kernel<UNIT, ORDER, DECDS_ENC_DW, DECDS_ENC_WAVES, MSG>
+// fused ChunkSet::new: 16-column blocks at 2 waves per SIMD (units of 4 tiles), or 8-column blocks
+// at 3 waves per SIMD (units of 8 tiles: one more workgroup per CU streams while another hashes)
+#ifndef DECDS_FUSE_DW
+#define DECDS_FUSE_DW 4
+#endif
+#define ENC_COMMIT rlnc_encode_kernel<16384 / (TILE_BLOCKS * 4 * DECDS_FUSE_DW), true, DECDS_FUSE_DW, (DECDS_FUSE_DW == 4 ? 2 : 3), true, true>
+// 16-byte-aligned rows (phase MSG_PHASE with 16-column blocks) take the message-tiled kernels
+constexpr bool MSG_OK = DECDS_ENC_DW == 4;
 
 hipError_t configure_kernels() {
-    const void *fns[] = {reinterpret_cast<const void *>(ENC_BIG), reinterpret_cast<const void *>(ENC_SMALL),
+    const void *fns[] = {reinterpret_cast<const void *>(ENC_KERNEL(ENC_UNIT, DECDS_ENC_ORDER != 0, false)),
+                         reinterpret_cast<const void *>(ENC_KERNEL(ENC_UNIT, DECDS_ENC_ORDER != 0, MSG_OK)),
+                         reinterpret_cast<const void *>(ENC_KERNEL(1, false, false)),
+                         reinterpret_cast<const void *>(ENC_KERNEL(1, false, MSG_OK)),
+                         reinterpret_cast<const void *>(ENC_COMMIT),
                          reinterpret_cast<const void *>(rlnc_decode_kernel<DEC_UNIT>)};
     for (const void *f : fns) {
         hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
@@ -680,13 +794,32 @@ hipError_t launch_encode(const LaunchGeom &, const uint8_t *src, size_t n, const
                          size_t pitch, uint32_t poly, uint32_t marker, hipStream_t stream) {
     if (n == 0) return hipSuccess;
     const uint32_t phase = row_phase<DECDS_ENC_DW>(dst, pitch);
+    const bool msg = MSG_OK && phase == MSG_PHASE;
     constexpr uint32_t T = TILES<DECDS_ENC_DW>;
-    if (n <= ENC_SMALL_N)
-        hipLaunchKernelGGL((ENC_SMALL), dim3((uint32_t)(n * T)), dim3(WG), LDS_BYTES, stream, src, n, coeffs, dst, pitch,
-                           phase, poly, marker);
+    const bool small = n <= ENC_SMALL_N;
+    const dim3 grid((uint32_t)(small ? n * T : n * (T / ENC_UNIT)));
+    const void *args_fn;
+    if (small)
+        args_fn = msg ? reinterpret_cast<const void *>(ENC_KERNEL(1, false, MSG_OK))
+                      : reinterpret_cast<const void *>(ENC_KERNEL(1, false, false));
     else
-        hipLaunchKernelGGL((ENC_BIG), dim3((uint32_t)(n * (T / ENC_UNIT))), dim3(WG), LDS_BYTES, stream, src, n, coeffs,
-                           dst, pitch, phase, poly, marker);
+        args_fn = msg ? reinterpret_cast<const void *>(ENC_KERNEL(ENC_UNIT, DECDS_ENC_ORDER != 0, MSG_OK))
+                      : reinterpret_cast<const void *>(ENC_KERNEL(ENC_UNIT, DECDS_ENC_ORDER != 0, false));
+    uint64_t first = 0;
+    uint32_t *sub = nullptr;
+    void *args[] = {&src, &n, &coeffs, &dst, &pitch, const_cast<uint32_t *>(&phase), &poly, &marker, &first, &sub};
+    return hipLaunchKernel(args_fn, grid, dim3(WG), args, LDS_BYTES, stream);
+}
+
+bool encode_commit_fusable(const uint8_t *dst, size_t pitch) { return row_phase<4>(dst, pitch) == MSG_PHASE; }
+static_assert(MSG_PHASE < COLS<2>, "16-byte-aligned rows have the message phase for both block widths");
+
+hipError_t launch_encode_commit(const uint8_t *src, size_t n, const uint8_t *coeffs, uint8_t *dst, size_t pitch,
+                                uint32_t poly, uint32_t marker, uint64_t first_id, uint32_t *sub, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    if (!encode_commit_fusable(dst, pitch)) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((ENC_COMMIT), dim3((uint32_t)(n * FUSED_UNITS)), dim3(WG), LDS_BYTES, stream, src, n, coeffs,
+                       dst, pitch, MSG_PHASE, poly, marker, first_id, sub);
     return hipGetLastError();
 }
 

@@ -268,6 +268,17 @@ void decds_repairing_blob_free(decds_repairing_blob *rb);
 int decds_commit_batch(decds_ctx *ctx, const uint8_t *coded, size_t pitch, size_t n_chunksets,
                        uint64_t first_chunkset_id, uint8_t *digests, uint8_t *roots, uint8_t *proofs,
                        void *stream);
+/* ChunkSet::new for a batch (chunkset.rs:37-63): decds_encode_batch + decds_commit_batch with the
+ * same arguments and results, but when the coded rows are 16-byte aligned (dst and dst_pitch
+ * multiples of 16, e.g. DECDS_CODED_PITCH_ALIGNED rows at DECDS_CODED_ROW_OFFSET_ALIGNED) the
+ * commitment's chunk hashing runs inside the encode kernel, right behind each workgroup's row stores,
+ * so the VALU-bound hashing overlaps the HBM-bound encode instead of re-reading every row afterwards
+ * (DESIGN.md §5.4). workspace: device memory of decds_encode_commit_workspace_bytes(n) bytes (unused
+ * on the unfused path, may then be NULL). */
+size_t decds_encode_commit_workspace_bytes(size_t n_chunksets);
+int decds_encode_commit_batch(decds_ctx *ctx, const uint8_t *src, size_t n_chunksets, const uint8_t *coeffs,
+                              uint8_t *dst, size_t dst_pitch, uint64_t first_chunkset_id, uint8_t *digests,
+                              uint8_t *roots, uint8_t *proofs, void *workspace, void *stream);
 /* host helpers: BLAKE3 (crate blake3 as used by decds), the Merkle tree over arbitrary n leaves
  * with decds' zero-hash padding (blob-level tree, blob.rs:266-273) and proof verification
  * (merkle_tree.rs:131-146). decds_merkle_tree returns the proof depth (proofs: n x depth x 32). */
