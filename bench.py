@@ -114,6 +114,7 @@ def main():
     import decds_amd
     from decds_amd import codec
     from decds_amd._capi import CHUNKSET_BYTES as CS, CODED_PIECE_BYTES as F, K, N
+    from decds_amd._capi import lib as _lib
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -278,7 +279,8 @@ def main():
             stream.synchronize()
             ms = sev[0].elapsed_time(sev[-1]) / reps
             gbs = ns * (CS + N * F) / (ms * 1e-3) / 1e9
-            sweep.append({"chunksets": ns, "encode_ms": round(ms, 3), "encode_GBps": round(gbs, 1),
+            sweep.append({"chunksets": ns, "kernel": _lib().decds_encode_kernel_name(ns).decode(),
+                          "encode_ms": round(ms, 3), "encode_GBps": round(gbs, 1),
                           "frac": round(gbs / HBM_PEAK_GBS, 4), "blob_GiBps": round(ns * CS / GIB / (ms * 1e-3), 1)})
         del big, cbig, obig
 
@@ -286,7 +288,8 @@ def main():
     dec_bytes = n_ready * (K * F + CS)      # ... of one decode launch (ready chunksets only)
     enc_gbs = enc_bytes / (enc_ms * 1e-3) / 1e9
     dec_gbs = dec_bytes / (dec_ms * 1e-3) / 1e9
-    dominant = "rlnc_encode_kernel" if enc_ms >= dec_ms else "rlnc_decode_kernel"
+    enc_kernel = _lib().decds_encode_kernel_name(n).decode()
+    dominant = enc_kernel if enc_ms >= dec_ms else "rlnc_decode_kernel"
     achieved = enc_gbs if dominant == "rlnc_encode_kernel" else dec_gbs
     traffic = None
     try:
@@ -326,7 +329,7 @@ def main():
                          "decode": {"kernel": "rlnc_decode_kernel", "achieved": round(dec_gbs, 1),
                                     "frac": round(dec_gbs / HBM_PEAK_GBS, 4),
                                     "bytes_per_launch": dec_bytes, "ms": round(dec_ms, 4)},
-                         "encode": {"kernel": "rlnc_encode_kernel", "achieved": round(enc_gbs, 1),
+                         "encode": {"kernel": enc_kernel, "achieved": round(enc_gbs, 1),
                                     "frac": round(enc_gbs / HBM_PEAK_GBS, 4),
                                     "bytes_per_launch": enc_bytes, "ms": round(enc_ms, 4)}},
             "breakdown": {"encode_ms": round(enc_ms, 4), "plan_ms": round(plan_ms, 4), "decode_ms": round(dec_ms, 4),

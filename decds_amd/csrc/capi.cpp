@@ -176,6 +176,8 @@ int decds_encode_batch(decds_ctx *ctx, const uint8_t *src, size_t n, const uint8
     return e == hipSuccess ? DECDS_OK : decds_hip_error(e, "rlnc_encode_kernel launch");
 }
 
+const char *decds_encode_kernel_name(size_t n_chunksets) { return encode_kernel_name(n_chunksets); }
+
 int decds_repair_plan_batch(decds_ctx *ctx, const uint8_t *coded, size_t coded_pitch, size_t n,
                             const uint8_t *cand, uint8_t *plan, int8_t *verdicts, int32_t *status,
                             void *stream) {

@@ -22,6 +22,7 @@
 // tools/study/rlnc_kernels_r01_study.hip with their measurements in DESIGN.md §8.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <utility>
 
 #include "blake3_impl.h"
@@ -41,10 +42,11 @@ constexpr uint32_t NXCD = 8;
 
 // Work units (tiles per workgroup) of the non-persistent launches and the workgroup order
 // (DESIGN.md §5.1, §8). Tuning constants, overridable at build time for in-process A/B
-// (tools/abbench.py); the shipped values are the defaults here. Encode: units of 4 tiles with each
-// XCD sweeping one contiguous eighth of the batch; batches of <= ENC_SMALL_N chunksets in units of
-// 1 in dispatcher order (a chunkset alone is 64 units of 4: a quarter of the CUs). Decode: units of 1
-// tile (+3…+11 % against 8 once the tables stopped being replicated, r02e).
+// (tools/abbench.py); the shipped values are the defaults here. Encode: batches of up to
+// ENC_SWEEP_MAX_N chunksets as a persistent sweep (rlnc_encode_sweep_kernel: +5 % at 103 chunksets,
+// ±0 at 256, r02o/p); larger ones in units of 4 tiles with each XCD sweeping one contiguous eighth
+// of the batch (the sweep's workgroups drift apart over many tiles: −5…−8 % at 1024-1639). Decode:
+// units of 1 tile (+3…+11 % against 8 once the tables stopped being replicated, r02e).
 #ifndef DECDS_ENC_UNIT
 #define DECDS_ENC_UNIT 4
 #endif
@@ -59,7 +61,10 @@ constexpr uint32_t NXCD = 8;
 #endif
 constexpr uint32_t ENC_UNIT = DECDS_ENC_UNIT;
 constexpr uint32_t DEC_UNIT = DECDS_DEC_UNIT;
-constexpr size_t ENC_SMALL_N = 16;
+#ifndef DECDS_ENC_SWEEP_MAX_N
+#define DECDS_ENC_SWEEP_MAX_N 256
+#endif
+constexpr size_t ENC_SWEEP_MAX_N = DECDS_ENC_SWEEP_MAX_N;
 
 // ---- GF(2^8) ----------------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t gf_mul(uint32_t a, uint32_t b, uint32_t poly) {
@@ -103,6 +108,19 @@ __device__ __forceinline__ uint32_t table_coeffs(const uint8_t *M, uint32_t ldm)
             if (4 * q + jj < (uint32_t)NOUT) w |= (uint32_t)M[(4 * q + jj) * ldm + i] << (8 * jj);
     }
     return w;
+}
+
+// table_coeffs with every lane loading (lanes past NIN*8 read lane 0's bytes and drop them): no
+// branch around the loads, so a loop that issues them keeps one memory-counter picture (stream_range)
+template <int NIN, int NOUT>
+__device__ __forceinline__ uint32_t table_coeffs_all(const uint8_t *M, uint32_t ldm) {
+    static_assert(NOUT == 16, "every coefficient word has 4 live outputs");
+    const bool live = threadIdx.x < NIN * 8;
+    const uint32_t p = live ? threadIdx.x : 0u, q = p & 3u, i = p >> 3;
+    uint32_t w = 0;
+#pragma unroll
+    for (uint32_t jj = 0; jj < 4; jj++) w |= (uint32_t)M[(4 * q + jj) * ldm + i] << (8 * jj);
+    return live ? w : 0u;
 }
 
 // Build the 2*NIN nibble tables of a NOUT x NIN coefficient matrix from the words of table_coeffs.
@@ -221,10 +239,10 @@ __device__ __forceinline__ void xor3_into(uint32_t (&acc)[4], const u32x4 &a, co
 // The row address of a lookup is nibble * 16 (the table base is the instruction's offset): byte p's
 // high nibble masked in place (xw >> 8p) & 0xF0, its low nibble masked and shifted up by 4 — hipcc
 // turns both into one SDWA op each (v_and_b32_sdwa / v_lshlrev_b32_sdwa with a byte select).
-template <int G, int DW>
+template <int G, int DW, uint32_t TB>
 __device__ __forceinline__ void lds_issue(u32x4 (&r)[8], uint32_t xw) {
     constexpr int i = G / DW;
-    constexpr uint32_t tlo = (2 * i) * TABLE_BYTES, thi = (2 * i + 1) * TABLE_BYTES;
+    constexpr uint32_t tlo = TB + (2 * i) * TABLE_BYTES, thi = TB + (2 * i + 1) * TABLE_BYTES;
     const uint32_t lo4 = xw & 0x0F0F0F0Fu;
 #pragma unroll
     for (int p = 0; p < 4; p++) {
@@ -246,7 +264,7 @@ __device__ __forceinline__ void lds_wait(u32x4 (&r)[8]) {
 // Group G of the lookups; input (G+1)/DW's register takes the next block's bytes (ncol0) as soon
 // as that input's lookups are all issued — before this block's stores: gfx9's vmcnt counts stores
 // too, so a load issued behind the stores would also wait for them.
-template <int NIN, int DW, int G>
+template <int NIN, int DW, uint32_t TB, int G>
 __device__ __forceinline__ void lds_step(uint32_t (&acc)[4 * DW][4], u32x4 (&ra)[8], u32x4 (&rb)[8],
                                          Vec<DW> (&x)[NIN], const uint8_t *ibase, const uint32_t (&ioff)[NIN],
                                          uint32_t ncol0) {
@@ -254,7 +272,7 @@ __device__ __forceinline__ void lds_step(uint32_t (&acc)[4 * DW][4], u32x4 (&ra)
     u32x4(&cur)[8] = (G & 1) ? rb : ra;  // group G's results
     u32x4(&nxt)[8] = (G & 1) ? ra : rb;
     if constexpr (G + 1 < NG) {
-        lds_issue<G + 1, DW>(nxt, x[(G + 1) / DW][(G + 1) % DW]);
+        lds_issue<G + 1, DW, TB>(nxt, x[(G + 1) / DW][(G + 1) % DW]);
         if constexpr (((G + 1) % DW) == DW - 1) x[(G + 1) / DW] = ldrow<DW>(ibase, ioff[(G + 1) / DW] + ncol0);
         lds_wait<8>(cur);
     } else {
@@ -265,18 +283,19 @@ __device__ __forceinline__ void lds_step(uint32_t (&acc)[4 * DW][4], u32x4 (&ra)
     for (int p = 0; p < 4; p++) xor3_into(acc[4 * w + p], cur[2 * p], cur[2 * p + 1]);
 }
 
-template <int NIN, int DW, int... Gs>
+template <int NIN, int DW, uint32_t TB, int... Gs>
 __device__ __forceinline__ void lookups(std::integer_sequence<int, Gs...>, uint32_t (&acc)[4 * DW][4],
                                         Vec<DW> (&x)[NIN], const uint8_t *ibase, const uint32_t (&ioff)[NIN],
                                         uint32_t ncol0) {
     u32x4 ra[8], rb[8];
-    lds_issue<0, DW>(ra, x[0][0]);
-    (lds_step<NIN, DW, Gs>(acc, ra, rb, x, ibase, ioff, ncol0), ...);
+    lds_issue<0, DW, TB>(ra, x[0][0]);
+    (lds_step<NIN, DW, TB, Gs>(acc, ra, rb, x, ibase, ioff, ncol0), ...);
 }
 
-// One lane block of 4*DW columns: out_j[col0 ..) = sum_i M[j][i] * in_i[col0 ..).
-// x holds this block's inputs on entry and the inputs at column ncol0 on exit.
-template <int NIN, int NOUT, int DW>
+// One lane block of 4*DW columns: out_j[col0 ..) = sum_i M[j][i] * in_i[col0 ..), tables at LDS
+// byte TB. x holds this block's inputs on entry and on exit the inputs at column ncol0 of the rows
+// at ibase + ioff (the next block's: the same chunkset's rows, or the next tile's chunkset's).
+template <int NIN, int NOUT, int DW, uint32_t TB = 0>
 __device__ __forceinline__ void combine_block(Vec<DW> (&x)[NIN], uint8_t *obase, const uint32_t (&ooff)[NOUT],
                                               uint32_t col0, const uint8_t *ibase, const uint32_t (&ioff)[NIN],
                                               uint32_t ncol0) {
@@ -285,7 +304,7 @@ __device__ __forceinline__ void combine_block(Vec<DW> (&x)[NIN], uint8_t *obase,
     for (int c = 0; c < 4 * DW; c++)
 #pragma unroll
         for (int q = 0; q < 4; q++) acc[c][q] = 0;
-    lookups<NIN, DW>(std::make_integer_sequence<int, DW * NIN>{}, acc, x, ibase, ioff, ncol0);
+    lookups<NIN, DW, TB>(std::make_integer_sequence<int, DW * NIN>{}, acc, x, ibase, ioff, ncol0);
     // columns x outputs -> outputs x columns
 #pragma unroll
     for (int q = 0; q < 4; q++) {
@@ -529,6 +548,85 @@ void rlnc_encode_kernel(const uint8_t *__restrict__ src, size_t n, const uint8_t
     }
 }
 
+// Encode as a persistent sweep: G = gridDim.x resident workgroups; workgroup b encodes tiles b, b + G,
+// b + 2G, ... of the whole batch (chunkset-major), so at any moment the tiles in flight are about G
+// consecutive ones — the order of one-tile workgroups in dispatch order, the fastest access pattern
+// of the encode at the kernels' occupancy (tools/layoutbench, r02n: 5.7-5.9 TB/s against 5.4-5.5 for
+// units of 4 tiles per XCD eighth) — without a workgroup start per tile: the next tile's coefficient
+// bytes and inputs are loaded while this tile computes (rolling prefetch across the chunkset change)
+// and its tables are built into the other of two LDS table buffers, one LDS barrier per tile. The edge
+// columns of chunksets b, b + G, ... are done first, outside the tile loop, so the loop issues the same
+// memory operations on every path (stream_range's vmcnt picture: inputs waited for, never stores).
+template <int DW, int WAVES, bool MSG>
+__global__ __launch_bounds__(WG, WAVES) __attribute__((amdgpu_waves_per_eu(WAVES, WAVES)))
+void rlnc_encode_sweep_kernel(const uint8_t *__restrict__ src, size_t n, const uint8_t *__restrict__ coeffs,
+                              uint8_t *__restrict__ dst, size_t pitch, uint32_t phase, uint32_t poly, uint32_t marker) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    constexpr uint32_t T = TILES<DW>;
+    uint32_t ioff[K], ooff[N];
+#pragma unroll
+    for (int i = 0; i < (int)K; i++) ioff[i] = (uint32_t)(i * L);
+#pragma unroll
+    for (int j = 0; j < (int)N; j++) ooff[j] = (uint32_t)(j * pitch + K);
+    // 1. coding-vector prefixes and edge columns of chunksets b, b + gridDim, ... (tables in buffer 1)
+    for (size_t cs = blockIdx.x; cs < n; cs += gridDim.x) {
+        const uint8_t *M = coeffs + cs * N * K;
+        const uint8_t *ibase = src + cs * CS;
+        uint8_t *obase = dst + cs * N * pitch;
+        const uint32_t cw = table_coeffs<K, N>(M, K);
+        lds_barrier();
+        build_tables<K, N>(lds + LDS_BYTES, cw, poly);
+        lds_barrier();
+        for (uint32_t idx = threadIdx.x; idx < N * K; idx += WG) obase[(idx / K) * pitch + idx % K] = M[idx];
+        for (uint32_t idx = threadIdx.x; idx < edge_cols<DW, MSG>(phase) * N; idx += WG) {
+            const uint32_t j = idx % N, col = edge_col<DW, MSG>(idx / N, phase);
+            uint32_t y = 0;
+#pragma unroll
+            for (uint32_t i = 0; i < K; i++) {
+                const uint64_t p = (uint64_t)i * L + col;
+                const uint32_t xv = p < CS ? ibase[p] : (p == CS ? marker : 0u);
+                y ^= tbl_mul(lds + LDS_BYTES, i, j, xv);
+            }
+            obase[j * pitch + K + col] = (uint8_t)y;
+        }
+    }
+    // 2. the sweep over tiles blockIdx.x, + G, ... (sweeps per XCD eighth measured slower, r02p)
+    const uint64_t total = (uint64_t)n * T;
+    const uint32_t G = gridDim.x;
+    uint32_t t = blockIdx.x;
+    if (t >= total) return;
+    auto col_of = [&](uint32_t tt) { return tile_col<DW, MSG>(tt % T, T, phase); };
+    uint32_t cs = t / T;
+    // prologue = the loop's memory-counter picture at its head: this tile's coefficient bytes, its
+    // inputs, then 16 dropped stores
+    uint32_t cw = table_coeffs_all<K, N>(coeffs + (size_t)cs * N * K, K);
+    Vec<DW> x[K];
+    load_block<K, DW>(x, src + (size_t)cs * CS, ioff, col_of(t));
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int j = 0; j < (int)N; j++) strow<DW>(dst, OOB_COL + ooff[j], Vec<DW>{});
+    // One tile per iteration: build its tables from the coefficient bytes the previous iteration
+    // loaded (issued before that iteration's stores, so the build waits for them alone), barrier, load
+    // the next tile's coefficient bytes, then the lookups with the rolling prefetch of the next tile's
+    // inputs and this tile's stores, and a barrier before the tables are rebuilt.
+    lds_barrier();  // the edge pass's table readers are done
+    uint32_t more;
+#pragma unroll 1
+    do {
+        build_tables<K, N>(lds, cw, poly);
+        lds_barrier();
+        const uint32_t tn = t + G;
+        more = tn < total;
+        const uint32_t csn = more ? tn / T : cs;
+        cw = table_coeffs_all<K, N>(coeffs + (size_t)csn * N * K, K);
+        combine_block<K, N, DW>(x, dst + (size_t)cs * N * pitch, ooff, col_of(t), src + (size_t)csn * CS, ioff,
+                                more ? col_of(tn) : OOB_COL);
+        lds_barrier();
+        t = tn;
+        cs = csn;
+    } while (more);
+}
+
 // Decode: workgroup = UNIT consecutive tiles of one chunkset. The accepted rows of chunkset cs are
 // rows plan.sel[k] of its 16-row group at coded + cs*16*pitch, or — gather form, in_bases != NULL —
 // rows plan.sel[k] at in_bases[cs] + sel*pitch, written to out_bases[cs] (the incremental
@@ -770,46 +868,60 @@ static uint32_t row_phase(const uint8_t *rows, size_t pitch) {
 // fused ChunkSet::new: 16-column blocks at 2 waves per SIMD (units of 4 tiles), or 8-column blocks
 // at 3 waves per SIMD (units of 8 tiles: one more workgroup per CU streams while another hashes)
 #ifndef DECDS_FUSE_DW
-#define DECDS_FUSE_DW 4
+#define DECDS_FUSE_DW 2  // r02m: 1.05 vs 1.12 ms at cfg2, 2.67 vs 2.84 ms at 256 chunksets
 #endif
 #define ENC_COMMIT rlnc_encode_kernel<16384 / (TILE_BLOCKS * 4 * DECDS_FUSE_DW), true, DECDS_FUSE_DW, (DECDS_FUSE_DW == 4 ? 2 : 3), true, true>
 // 16-byte-aligned rows (phase MSG_PHASE with 16-column blocks) take the message-tiled kernels
 constexpr bool MSG_OK = DECDS_ENC_DW == 4;
+#define ENC_SWEEP(MSG) rlnc_encode_sweep_kernel<DECDS_ENC_DW, DECDS_ENC_WAVES, MSG>
 
 hipError_t configure_kernels() {
     const void *fns[] = {reinterpret_cast<const void *>(ENC_KERNEL(ENC_UNIT, DECDS_ENC_ORDER != 0, false)),
                          reinterpret_cast<const void *>(ENC_KERNEL(ENC_UNIT, DECDS_ENC_ORDER != 0, MSG_OK)),
-                         reinterpret_cast<const void *>(ENC_KERNEL(1, false, false)),
-                         reinterpret_cast<const void *>(ENC_KERNEL(1, false, MSG_OK)),
+                         reinterpret_cast<const void *>(ENC_SWEEP(false)), reinterpret_cast<const void *>(ENC_SWEEP(MSG_OK)),
                          reinterpret_cast<const void *>(ENC_COMMIT),
                          reinterpret_cast<const void *>(rlnc_decode_kernel<DEC_UNIT>)};
     for (const void *f : fns) {
-        hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+        hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * LDS_BYTES);
         if (e != hipSuccess) return e;
     }
     return hipSuccess;
 }
 
-hipError_t launch_encode(const LaunchGeom &, const uint8_t *src, size_t n, const uint8_t *coeffs, uint8_t *dst,
+// resident workgroups of the sweep kernel on this device (occupancy x CUs), once per process
+static uint32_t sweep_grid(const LaunchGeom &g) {
+    static uint32_t grid = 0;
+    if (!grid) {
+        int per_cu = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void *>(ENC_SWEEP(false)), WG,
+                                                         2 * LDS_BYTES) != hipSuccess || per_cu < 1)
+            per_cu = DECDS_ENC_WAVES;
+        grid = (uint32_t)per_cu * (uint32_t)(g.num_cus > 0 ? g.num_cus : 256);
+    }
+    return grid;
+}
+
+hipError_t launch_encode(const LaunchGeom &geom, const uint8_t *src, size_t n, const uint8_t *coeffs, uint8_t *dst,
                          size_t pitch, uint32_t poly, uint32_t marker, hipStream_t stream) {
     if (n == 0) return hipSuccess;
     const uint32_t phase = row_phase<DECDS_ENC_DW>(dst, pitch);
     const bool msg = MSG_OK && phase == MSG_PHASE;
     constexpr uint32_t T = TILES<DECDS_ENC_DW>;
-    const bool small = n <= ENC_SMALL_N;
-    const dim3 grid((uint32_t)(small ? n * T : n * (T / ENC_UNIT)));
-    const void *args_fn;
-    if (small)
-        args_fn = msg ? reinterpret_cast<const void *>(ENC_KERNEL(1, false, MSG_OK))
-                      : reinterpret_cast<const void *>(ENC_KERNEL(1, false, false));
-    else
-        args_fn = msg ? reinterpret_cast<const void *>(ENC_KERNEL(ENC_UNIT, DECDS_ENC_ORDER != 0, MSG_OK))
-                      : reinterpret_cast<const void *>(ENC_KERNEL(ENC_UNIT, DECDS_ENC_ORDER != 0, false));
+    if (n <= ENC_SWEEP_MAX_N) {  // small batches too: with fewer tiles than resident slots it is one tile each
+        const uint32_t grid = (uint32_t)std::min<uint64_t>((uint64_t)n * T, sweep_grid(geom));
+        const void *fn = msg ? reinterpret_cast<const void *>(ENC_SWEEP(MSG_OK)) : reinterpret_cast<const void *>(ENC_SWEEP(false));
+        void *args[] = {&src, &n, &coeffs, &dst, &pitch, const_cast<uint32_t *>(&phase), &poly, &marker};
+        return hipLaunchKernel(fn, dim3(grid), dim3(WG), args, 2 * LDS_BYTES, stream);
+    }
+    const void *fn = msg ? reinterpret_cast<const void *>(ENC_KERNEL(ENC_UNIT, DECDS_ENC_ORDER != 0, MSG_OK))
+                         : reinterpret_cast<const void *>(ENC_KERNEL(ENC_UNIT, DECDS_ENC_ORDER != 0, false));
     uint64_t first = 0;
     uint32_t *sub = nullptr;
     void *args[] = {&src, &n, &coeffs, &dst, &pitch, const_cast<uint32_t *>(&phase), &poly, &marker, &first, &sub};
-    return hipLaunchKernel(args_fn, grid, dim3(WG), args, LDS_BYTES, stream);
+    return hipLaunchKernel(fn, dim3((uint32_t)(n * (T / ENC_UNIT))), dim3(WG), args, LDS_BYTES, stream);
 }
+
+const char *encode_kernel_name(size_t n) { return n <= ENC_SWEEP_MAX_N ? "rlnc_encode_sweep_kernel" : "rlnc_encode_kernel"; }
 
 bool encode_commit_fusable(const uint8_t *dst, size_t pitch) { return row_phase<4>(dst, pitch) == MSG_PHASE; }
 static_assert(MSG_PHASE < COLS<2>, "16-byte-aligned rows have the message phase for both block widths");

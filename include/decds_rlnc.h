@@ -97,6 +97,10 @@ int decds_device_status(const decds_ctx *ctx);
 int decds_encode_batch(decds_ctx *ctx, const uint8_t *src, size_t n_chunksets,
                        const uint8_t *coeffs, uint8_t *dst, size_t dst_pitch, void *stream);
 
+/* name of the gfx950 kernel decds_encode_batch launches for n chunksets (for profiles: batches of up
+ * to 256 chunksets run the persistent sweep, larger ones units of 4 tiles per XCD eighth) */
+const char *decds_encode_kernel_name(size_t n_chunksets);
+
 /* Replaces the incremental rank logic of RepairingChunkSet::add_chunk_unvalidated ->
  * Decoder::decode (chunkset.rs:173-184) and is_ready_to_repair (chunkset.rs:187-189) for a batch:
  *   cand     : n x 16 coded-row indices in arrival order, DECDS_NO_CANDIDATE-terminated

@@ -16,6 +16,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <string>
 #include <vector>
 
 #define CK(x)                                                            \
@@ -37,7 +38,9 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void *p) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), 0, 0x80000000u, 0x00020000);
 }
 
-// workgroup -> unit: ORDER 0 dispatcher order, 1 each XCD sweeps one contiguous eighth
+// workgroup -> unit: ORDER 0 dispatcher order, 1 each XCD sweeps one contiguous eighth, 2 dispatcher
+// order with a unit's tiles strided (tile r + k * 256/UNIT of its chunkset: the resident workgroups
+// sweep every chunkset's rows together)
 template <int ORDER>
 __device__ __forceinline__ uint32_t unit_of() {
     uint32_t u = blockIdx.x;
@@ -51,12 +54,15 @@ __device__ __forceinline__ uint32_t unit_of() {
 // encode pattern: inputs = pieces of the contiguous chunkset (i * L), outputs in layout TM
 template <int UNIT, int ORDER, bool TM>
 __global__ __launch_bounds__(256) void enc_k(const uint8_t *__restrict__ in, uint8_t *__restrict__ out, size_t n) {
+    extern __shared__ uint8_t lds[];
     const uint32_t t0 = unit_of<ORDER>() * UNIT, cs = t0 / TILES, tile0 = t0 % TILES;
     if (cs >= n) return;
     const auto ri = rsrc(in + cs * CSB);
     const auto ro = rsrc(out + cs * (TM ? TM_CS : 16 * PITCH));
     u32x4 acc = {0, 0, 0, 0};
-    for (uint32_t t = tile0; t < tile0 + UNIT; t++) {
+    constexpr uint32_t UPC = TILES / UNIT;  // units per chunkset
+    for (uint32_t k = 0; k < UNIT; k++) {
+        const uint32_t t = ORDER == 2 ? (tile0 / UNIT) + k * UPC : tile0 + k;
         const uint32_t b = t * 256 + threadIdx.x;
         const uint32_t col = b < BLOCKS ? b * 16 : 0x80000000u;
         u32x4 x[10];
@@ -70,6 +76,7 @@ __global__ __launch_bounds__(256) void enc_k(const uint8_t *__restrict__ in, uin
         for (int j = 0; j < 16; j++)
             __builtin_amdgcn_raw_buffer_store_b128(acc + (uint32_t)j, ro, obase + (uint32_t)(j * (TM ? TILE_COLS : PITCH)), 0, 0);
     }
+    if (acc.x == 0x9E3779B9u && threadIdx.x == 999) lds[0] = 1;  // keeps the LDS allocation referenced
 }
 
 // decode pattern: inputs = 10 of the 16 coded rows (rows 0, 2, 3, 5, 6, 8, 9, 11, 13, 15) in layout
@@ -136,9 +143,11 @@ void run(const char *name, size_t n, double bytes, F f, const Args &a) {
 
 int main(int argc, char **argv) {
     Args a;
+    std::string only;
     for (int i = 1; i < argc; i++) {
         if (!std::strcmp(argv[i], "--warm-ms")) a.warm_ms = std::atoi(argv[++i]);
         if (!std::strcmp(argv[i], "--reps")) a.reps = std::atoi(argv[++i]);
+        if (!std::strcmp(argv[i], "--only")) only = argv[++i];
     }
     const size_t nmax = 1024;
     uint8_t *src, *coded, *rep;
@@ -147,9 +156,23 @@ int main(int argc, char **argv) {
     CK(hipMalloc(&rep, nmax * CSB + 4096));
     CK(hipMemset(src, 0x3c, nmax * CSB));
     CK(hipMemset(coded, 0x5a, nmax * 16 * PITCH));
+    constexpr uint32_t LDS2 = 80 * 1024;  // 2 workgroups per CU, as the codec kernels' VGPRs allow
+    for (const void *f : {(const void *)enc_k<4, 1, false>, (const void *)enc_k<4, 0, false>, (const void *)enc_k<4, 2, false>,
+                          (const void *)enc_k<2, 0, false>, (const void *)enc_k<1, 0, false>, (const void *)enc_k<8, 2, false>})
+        CK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, LDS2));
     for (size_t n : {103, 256, 1024}) {
         const double eb = (double)n * (CSB + 16 * FB), db = (double)n * (10 * FB + CSB);
-        const unsigned g4 = (unsigned)(n * TILES / 4), g1 = (unsigned)(n * TILES);
+        const unsigned g4 = (unsigned)(n * TILES / 4), g1 = (unsigned)(n * TILES), g2 = g1 / 2, g8 = g1 / 8;
+        if (only.empty() || only == "occ") {
+            run("enc_u4_xcd_2wg", n, eb, [&] { enc_k<4, 1, false><<<g4, 256, LDS2>>>(src, coded, n); }, a);
+            run("enc_u4_disp_2wg", n, eb, [&] { enc_k<4, 0, false><<<g4, 256, LDS2>>>(src, coded, n); }, a);
+            run("enc_u4_strided_2wg", n, eb, [&] { enc_k<4, 2, false><<<g4, 256, LDS2>>>(src, coded, n); }, a);
+            run("enc_u8_strided_2wg", n, eb, [&] { enc_k<8, 2, false><<<g8, 256, LDS2>>>(src, coded, n); }, a);
+            run("enc_u2_disp_2wg", n, eb, [&] { enc_k<2, 0, false><<<g2, 256, LDS2>>>(src, coded, n); }, a);
+            run("enc_u1_disp_2wg", n, eb, [&] { enc_k<1, 0, false><<<g1, 256, LDS2>>>(src, coded, n); }, a);
+            run("enc_u4_strided", n, eb, [&] { enc_k<4, 2, false><<<g4, 256>>>(src, coded, n); }, a);
+            if (!only.empty()) continue;
+        }
         run("enc_rows_u4_xcd", n, eb, [&] { enc_k<4, 1, false><<<g4, 256>>>(src, coded, n); }, a);
         run("enc_rows_u1_disp", n, eb, [&] { enc_k<1, 0, false><<<g1, 256>>>(src, coded, n); }, a);
         run("enc_tilemajor_u4_xcd", n, eb, [&] { enc_k<4, 1, true><<<g4, 256>>>(src, coded, n); }, a);
