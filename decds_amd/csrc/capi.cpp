@@ -110,6 +110,11 @@ int decds_ctx_create(int device, decds_ctx **out) {
     c->marker = (uint8_t)MARKER_DEFAULT;
     c->gen = host_gf_generator(POLY_DEFAULT);
     c->geom.num_cus = prop.multiProcessorCount;
+    if ((e = hipMalloc(reinterpret_cast<void **>(&c->geom.counters),
+                       LaunchGeom::N_COUNTERS * LaunchGeom::COUNTER_STRIDE * sizeof(uint32_t))) != hipSuccess) {
+        delete c;
+        return decds_hip_error(e, "hipMalloc (tile counters)");
+    }
     *out = c;
     return DECDS_OK;
 }
@@ -119,6 +124,10 @@ int decds_ctx_destroy(decds_ctx *ctx) {
     (void)hipSetDevice(ctx->device);
     decds_lanes_destroy(ctx);
     if (ctx->host_scratch) (void)hipFree(ctx->host_scratch);
+    if (ctx->geom.counters) {
+        (void)hipDeviceSynchronize();  // no launch may still count on them
+        (void)hipFree(ctx->geom.counters);
+    }
     delete ctx;
     return DECDS_OK;
 }

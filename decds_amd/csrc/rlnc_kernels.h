@@ -4,10 +4,17 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include <atomic>
+
 namespace decds {
 
 struct LaunchGeom {
     int num_cus;  // CUs on the device (256 on MI355X)
+    // tile counters of the queue-fed encode sweep: one 128-byte line each, a launch takes the next
+    // one round robin (concurrent launches on other streams never share one) and zeroes it first
+    uint32_t *counters = nullptr;
+    mutable std::atomic<uint32_t> counter_next{0};
+    static constexpr uint32_t N_COUNTERS = 256, COUNTER_STRIDE = 32;  // in uint32_t
 };
 
 hipError_t launch_encode(const LaunchGeom &g, const uint8_t *src, size_t n, const uint8_t *coeffs,

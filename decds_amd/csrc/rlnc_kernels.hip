@@ -38,14 +38,15 @@ constexpr uint32_t TILE_BLOCKS = WG;                          // one 16-col bloc
 constexpr uint32_t ROW_BYTES = 16;                            // one nibble row: 16 outputs' products
 constexpr uint32_t TABLE_BYTES = 16 * ROW_BYTES;              // 16 nibble rows = 256 B = the 64 banks once
 constexpr uint32_t LDS_BYTES = K * 2 * TABLE_BYTES;           // 5 KiB
+constexpr uint32_t SWEEP_LDS = 2 * LDS_BYTES + 16;             // two table buffers + the next-tile slot
 constexpr uint32_t NXCD = 8;
 
 // Work units (tiles per workgroup) of the non-persistent launches and the workgroup order
 // (DESIGN.md §5.1, §8). Tuning constants, overridable at build time for in-process A/B
-// (tools/abbench.py); the shipped values are the defaults here. Encode: batches of up to
-// ENC_SWEEP_MAX_N chunksets as a persistent sweep (rlnc_encode_sweep_kernel: +5 % at 103 chunksets,
-// ±0 at 256, r02o/p); larger ones in units of 4 tiles with each XCD sweeping one contiguous eighth
-// of the batch (the sweep's workgroups drift apart over many tiles: −5…−8 % at 1024-1639). Decode:
+// (tools/abbench.py); the shipped values are the defaults here. Encode: every batch as a persistent
+// sweep fed by a tile counter (rlnc_encode_sweep_kernel<QUEUE>: 0.69-0.71 of 8 TB/s at 103-1639
+// chunksets against 0.64-0.66 for units of 4 tiles per XCD eighth, r02r; a fixed-stride sweep drifts
+// apart: −3…−4 % at 512-1639). ENC_SWEEP_MAX_N caps it for A/B builds (units of 4 above). Decode:
 // units of 1 tile (+3…+11 % against 8 once the tables stopped being replicated, r02e).
 #ifndef DECDS_ENC_UNIT
 #define DECDS_ENC_UNIT 4
@@ -62,7 +63,7 @@ constexpr uint32_t NXCD = 8;
 constexpr uint32_t ENC_UNIT = DECDS_ENC_UNIT;
 constexpr uint32_t DEC_UNIT = DECDS_DEC_UNIT;
 #ifndef DECDS_ENC_SWEEP_MAX_N
-#define DECDS_ENC_SWEEP_MAX_N 256
+#define DECDS_ENC_SWEEP_MAX_N ((size_t)1 << 24)  // the C-ABI's batch limit: always the sweep
 #endif
 constexpr size_t ENC_SWEEP_MAX_N = DECDS_ENC_SWEEP_MAX_N;
 
@@ -557,11 +558,18 @@ void rlnc_encode_kernel(const uint8_t *__restrict__ src, size_t n, const uint8_t
 // and its tables are built into the other of two LDS table buffers, one LDS barrier per tile. The edge
 // columns of chunksets b, b + G, ... are done first, outside the tile loop, so the loop issues the same
 // memory operations on every path (stream_range's vmcnt picture: inputs waited for, never stores).
-template <int DW, int WAVES, bool MSG>
+// QUEUE: after the first G tiles (tile = blockIdx.x) every next tile comes from a tile counter
+// (one atomic add per workgroup and tile, issued a tile ahead), so the tiles in flight stay one
+// resident grid wide however the workgroups' speeds differ — a fixed stride lets them drift apart.
+template <int DW, int WAVES, bool MSG, bool QUEUE = false>
 __global__ __launch_bounds__(WG, WAVES) __attribute__((amdgpu_waves_per_eu(WAVES, WAVES)))
 void rlnc_encode_sweep_kernel(const uint8_t *__restrict__ src, size_t n, const uint8_t *__restrict__ coeffs,
-                              uint8_t *__restrict__ dst, size_t pitch, uint32_t phase, uint32_t poly, uint32_t marker) {
+                              uint8_t *__restrict__ dst, size_t pitch, uint32_t phase, uint32_t poly, uint32_t marker,
+                              uint32_t *__restrict__ counter) {
+    // no static __shared__ here: the lookups' inline-asm ds_reads address the tables from LDS byte 0,
+    // so everything lives in the dynamic allocation (2 table buffers, then the next-tile slot)
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    uint32_t &s_next = *reinterpret_cast<uint32_t *>(lds + 2 * LDS_BYTES);
     constexpr uint32_t T = TILES<DW>;
     uint32_t ioff[K], ooff[N];
 #pragma unroll
@@ -602,6 +610,18 @@ void rlnc_encode_sweep_kernel(const uint8_t *__restrict__ src, size_t n, const u
     uint32_t cw = table_coeffs_all<K, N>(coeffs + (size_t)cs * N * K, K);
     Vec<DW> x[K];
     load_block<K, DW>(x, src + (size_t)cs * CS, ioff, col_of(t));
+    // The tile counter is bumped by inline asm: a compiler-visible atomic's result becomes a phi at the
+    // end of the lane-0 branch, where hipcc waits for it with vmcnt(0) — i.e. for every store in
+    // flight. Here it is waited for explicitly, a step later, with vmcnt(16): this step's 16 stores
+    // may stay in flight. (The compiler's own counts then miss one operation, which only ever makes
+    // its waits stricter.)
+    auto grab_next = [&]() -> uint32_t {
+        uint32_t r = 0;
+        if (QUEUE && threadIdx.x == 0)
+            asm volatile("global_atomic_add %0, %1, %2, off sc0" : "=v"(r) : "v"(counter), "v"(1u) : "memory");
+        return r;
+    };
+    uint32_t grab = grab_next();  // -> the tile after the next
     asm volatile("" ::: "memory");
 #pragma unroll
     for (int j = 0; j < (int)N; j++) strow<DW>(dst, OOB_COL + ooff[j], Vec<DW>{});
@@ -614,8 +634,13 @@ void rlnc_encode_sweep_kernel(const uint8_t *__restrict__ src, size_t n, const u
 #pragma unroll 1
     do {
         build_tables<K, N>(lds, cw, poly);
+        if constexpr (QUEUE) {
+            asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+            if (threadIdx.x == 0) s_next = G + grab;
+        }
         lds_barrier();
-        const uint32_t tn = t + G;
+        const uint32_t tn = QUEUE ? s_next : t + G;
+        grab = grab_next();
         more = tn < total;
         const uint32_t csn = more ? tn / T : cs;
         cw = table_coeffs_all<K, N>(coeffs + (size_t)csn * N * K, K);
@@ -873,7 +898,10 @@ static uint32_t row_phase(const uint8_t *rows, size_t pitch) {
 #define ENC_COMMIT rlnc_encode_kernel<16384 / (TILE_BLOCKS * 4 * DECDS_FUSE_DW), true, DECDS_FUSE_DW, (DECDS_FUSE_DW == 4 ? 2 : 3), true, true>
 // 16-byte-aligned rows (phase MSG_PHASE with 16-column blocks) take the message-tiled kernels
 constexpr bool MSG_OK = DECDS_ENC_DW == 4;
-#define ENC_SWEEP(MSG) rlnc_encode_sweep_kernel<DECDS_ENC_DW, DECDS_ENC_WAVES, MSG>
+#ifndef DECDS_ENC_QUEUE
+#define DECDS_ENC_QUEUE 1
+#endif
+#define ENC_SWEEP(MSG) rlnc_encode_sweep_kernel<DECDS_ENC_DW, DECDS_ENC_WAVES, MSG, (DECDS_ENC_QUEUE != 0)>
 
 hipError_t configure_kernels() {
     const void *fns[] = {reinterpret_cast<const void *>(ENC_KERNEL(ENC_UNIT, DECDS_ENC_ORDER != 0, false)),
@@ -882,7 +910,7 @@ hipError_t configure_kernels() {
                          reinterpret_cast<const void *>(ENC_COMMIT),
                          reinterpret_cast<const void *>(rlnc_decode_kernel<DEC_UNIT>)};
     for (const void *f : fns) {
-        hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * LDS_BYTES);
+        hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, SWEEP_LDS);
         if (e != hipSuccess) return e;
     }
     return hipSuccess;
@@ -894,7 +922,7 @@ static uint32_t sweep_grid(const LaunchGeom &g) {
     if (!grid) {
         int per_cu = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void *>(ENC_SWEEP(false)), WG,
-                                                         2 * LDS_BYTES) != hipSuccess || per_cu < 1)
+                                                         SWEEP_LDS) != hipSuccess || per_cu < 1)
             per_cu = DECDS_ENC_WAVES;
         grid = (uint32_t)per_cu * (uint32_t)(g.num_cus > 0 ? g.num_cus : 256);
     }
@@ -910,8 +938,15 @@ hipError_t launch_encode(const LaunchGeom &geom, const uint8_t *src, size_t n, c
     if (n <= ENC_SWEEP_MAX_N) {  // small batches too: with fewer tiles than resident slots it is one tile each
         const uint32_t grid = (uint32_t)std::min<uint64_t>((uint64_t)n * T, sweep_grid(geom));
         const void *fn = msg ? reinterpret_cast<const void *>(ENC_SWEEP(MSG_OK)) : reinterpret_cast<const void *>(ENC_SWEEP(false));
-        void *args[] = {&src, &n, &coeffs, &dst, &pitch, const_cast<uint32_t *>(&phase), &poly, &marker};
-        return hipLaunchKernel(fn, dim3(grid), dim3(WG), args, 2 * LDS_BYTES, stream);
+        uint32_t *counter = nullptr;
+        if (DECDS_ENC_QUEUE) {
+            if (!geom.counters) return hipErrorInvalidValue;
+            counter = geom.counters + (geom.counter_next.fetch_add(1) % LaunchGeom::N_COUNTERS) * LaunchGeom::COUNTER_STRIDE;
+            hipError_t e = hipMemsetAsync(counter, 0, sizeof(uint32_t), stream);
+            if (e != hipSuccess) return e;
+        }
+        void *args[] = {&src, &n, &coeffs, &dst, &pitch, const_cast<uint32_t *>(&phase), &poly, &marker, &counter};
+        return hipLaunchKernel(fn, dim3(grid), dim3(WG), args, SWEEP_LDS, stream);
     }
     const void *fn = msg ? reinterpret_cast<const void *>(ENC_KERNEL(ENC_UNIT, DECDS_ENC_ORDER != 0, MSG_OK))
                          : reinterpret_cast<const void *>(ENC_KERNEL(ENC_UNIT, DECDS_ENC_ORDER != 0, false));

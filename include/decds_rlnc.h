@@ -97,8 +97,8 @@ int decds_device_status(const decds_ctx *ctx);
 int decds_encode_batch(decds_ctx *ctx, const uint8_t *src, size_t n_chunksets,
                        const uint8_t *coeffs, uint8_t *dst, size_t dst_pitch, void *stream);
 
-/* name of the gfx950 kernel decds_encode_batch launches for n chunksets (for profiles: batches of up
- * to 256 chunksets run the persistent sweep, larger ones units of 4 tiles per XCD eighth) */
+/* name of the gfx950 kernel decds_encode_batch launches for n chunksets (for profiles and traces:
+ * the persistent, tile-counter-fed sweep, rlnc_encode_sweep_kernel) */
 const char *decds_encode_kernel_name(size_t n_chunksets);
 
 /* Replaces the incremental rank logic of RepairingChunkSet::add_chunk_unvalidated ->
