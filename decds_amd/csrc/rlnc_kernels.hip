@@ -561,6 +561,7 @@ void rlnc_encode_kernel(const uint8_t *__restrict__ src, size_t n, const uint8_t
 // QUEUE: after the first G tiles (tile = blockIdx.x) every next tile comes from a tile counter
 // (one atomic add per workgroup and tile, issued a tile ahead), so the tiles in flight stay one
 // resident grid wide however the workgroups' speeds differ — a fixed stride lets them drift apart.
+// counter == NULL (batches of at most G tiles): one tile per workgroup, no counter.
 template <int DW, int WAVES, bool MSG, bool QUEUE = false>
 __global__ __launch_bounds__(WG, WAVES) __attribute__((amdgpu_waves_per_eu(WAVES, WAVES)))
 void rlnc_encode_sweep_kernel(const uint8_t *__restrict__ src, size_t n, const uint8_t *__restrict__ coeffs,
@@ -617,7 +618,7 @@ void rlnc_encode_sweep_kernel(const uint8_t *__restrict__ src, size_t n, const u
     // its waits stricter.)
     auto grab_next = [&]() -> uint32_t {
         uint32_t r = 0;
-        if (QUEUE && threadIdx.x == 0)
+        if (QUEUE && counter && threadIdx.x == 0)
             asm volatile("global_atomic_add %0, %1, %2, off sc0" : "=v"(r) : "v"(counter), "v"(1u) : "memory");
         return r;
     };
@@ -938,8 +939,8 @@ hipError_t launch_encode(const LaunchGeom &geom, const uint8_t *src, size_t n, c
     if (n <= ENC_SWEEP_MAX_N) {  // small batches too: with fewer tiles than resident slots it is one tile each
         const uint32_t grid = (uint32_t)std::min<uint64_t>((uint64_t)n * T, sweep_grid(geom));
         const void *fn = msg ? reinterpret_cast<const void *>(ENC_SWEEP(MSG_OK)) : reinterpret_cast<const void *>(ENC_SWEEP(false));
-        uint32_t *counter = nullptr;
-        if (DECDS_ENC_QUEUE) {
+        uint32_t *counter = nullptr;  // none when every workgroup has one tile: no counter reset to launch
+        if (DECDS_ENC_QUEUE && (uint64_t)n * T > grid) {
             if (!geom.counters) return hipErrorInvalidValue;
             counter = geom.counters + (geom.counter_next.fetch_add(1) % LaunchGeom::N_COUNTERS) * LaunchGeom::COUNTER_STRIDE;
             hipError_t e = hipMemsetAsync(counter, 0, sizeof(uint32_t), stream);

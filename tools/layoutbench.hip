@@ -81,8 +81,9 @@ __global__ __launch_bounds__(256) void enc_k(const uint8_t *__restrict__ in, uin
 
 // decode pattern: inputs = 10 of the 16 coded rows (rows 0, 2, 3, 5, 6, 8, 9, 11, 13, 15) in layout
 // TM, outputs = pieces of the contiguous chunkset
-template <int UNIT, bool TM>
+template <int UNIT, bool TM, uint64_t OROW = LB>
 __global__ __launch_bounds__(256) void dec_k(const uint8_t *__restrict__ in, uint8_t *__restrict__ out, size_t n) {
+    extern __shared__ uint8_t lds[];
     const uint32_t t0 = blockIdx.x * UNIT, cs = t0 / TILES, tile0 = t0 % TILES;
     if (cs >= n) return;
     constexpr uint32_t sel[10] = {0, 2, 3, 5, 6, 8, 9, 11, 13, 15};
@@ -100,8 +101,9 @@ __global__ __launch_bounds__(256) void dec_k(const uint8_t *__restrict__ in, uin
 #pragma unroll
         for (int k = 0; k < 10; k++) acc ^= x[k];
 #pragma unroll
-        for (int i = 0; i < 10; i++) __builtin_amdgcn_raw_buffer_store_b128(acc + (uint32_t)i, ro, (uint32_t)(i * LB) + col, 0, 0);
+        for (int i = 0; i < 10; i++) __builtin_amdgcn_raw_buffer_store_b128(acc + (uint32_t)i, ro, (uint32_t)(i * OROW) + col, 0, 0);
     }
+    if (acc.x == 0x9E3779B9u && threadIdx.x == 999) lds[0] = 1;
 }
 
 __global__ __launch_bounds__(256) void copy_flat(const u32x4 *__restrict__ s, u32x4 *__restrict__ d, size_t n16) {
@@ -157,7 +159,7 @@ int main(int argc, char **argv) {
     CK(hipMemset(src, 0x3c, nmax * CSB));
     CK(hipMemset(coded, 0x5a, nmax * 16 * PITCH));
     constexpr uint32_t LDS2 = 80 * 1024;  // 2 workgroups per CU, as the codec kernels' VGPRs allow
-    for (const void *f : {(const void *)enc_k<4, 1, false>, (const void *)enc_k<4, 0, false>, (const void *)enc_k<4, 2, false>,
+    for (const void *f : {(const void *)dec_k<1, false>, (const void *)dec_k<1, false, 1u << 20>, (const void *)enc_k<4, 1, false>, (const void *)enc_k<4, 0, false>, (const void *)enc_k<4, 2, false>,
                           (const void *)enc_k<2, 0, false>, (const void *)enc_k<1, 0, false>, (const void *)enc_k<8, 2, false>})
         CK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, LDS2));
     for (size_t n : {103, 256, 1024}) {
@@ -171,6 +173,16 @@ int main(int argc, char **argv) {
             run("enc_u2_disp_2wg", n, eb, [&] { enc_k<2, 0, false><<<g2, 256, LDS2>>>(src, coded, n); }, a);
             run("enc_u1_disp_2wg", n, eb, [&] { enc_k<1, 0, false><<<g1, 256, LDS2>>>(src, coded, n); }, a);
             run("enc_u4_strided", n, eb, [&] { enc_k<4, 2, false><<<g4, 256>>>(src, coded, n); }, a);
+            if (!only.empty()) continue;
+        }
+        if (only.empty() || only == "dec") {
+            // decode outputs: the chunkset's pieces at i*L (byte-misaligned by i, the real layout) or
+            // 1 MiB apart (16-byte aligned), at the decode kernel's occupancy (3 workgroups per CU) and free
+            constexpr uint32_t LDS3 = 52 * 1024;
+            run("dec_u1_3wg", n, db, [&] { dec_k<1, false><<<g1, 256, LDS3>>>(coded, rep, n); }, a);
+            run("dec_u1_outA_3wg", n, db, [&] { dec_k<1, false, 1u << 20><<<g1, 256, LDS3>>>(coded, rep, n); }, a);
+            run("dec_u1", n, db, [&] { dec_k<1, false><<<g1, 256>>>(coded, rep, n); }, a);
+            run("dec_u1_outA", n, db, [&] { dec_k<1, false, 1u << 20><<<g1, 256>>>(coded, rep, n); }, a);
             if (!only.empty()) continue;
         }
         run("enc_rows_u4_xcd", n, eb, [&] { enc_k<4, 1, false><<<g4, 256>>>(src, coded, n); }, a);
