@@ -115,6 +115,12 @@ int decds_ctx_create(int device, decds_ctx **out) {
         delete c;
         return decds_hip_error(e, "hipMalloc (tile counters)");
     }
+    if ((e = hipMemset(c->geom.counters, 0, LaunchGeom::N_COUNTERS * LaunchGeom::COUNTER_STRIDE * sizeof(uint32_t))) !=
+        hipSuccess) {
+        (void)hipFree(c->geom.counters);
+        delete c;
+        return decds_hip_error(e, "hipMemset (tile counters)");
+    }
     *out = c;
     return DECDS_OK;
 }

@@ -10,8 +10,9 @@ namespace decds {
 
 struct LaunchGeom {
     int num_cus;  // CUs on the device (256 on MI355X)
-    // tile counters of the queue-fed encode sweep: one 128-byte line each, a launch takes the next
-    // one round robin (concurrent launches on other streams never share one) and zeroes it first
+    // tile counters of the queue-fed encode sweep: one 128-byte line each (tile counter, exit count),
+    // zeroed at context creation; a launch takes the next one round robin (concurrent launches on
+    // other streams never share one) and its last workgroup zeroes it again
     uint32_t *counters = nullptr;
     mutable std::atomic<uint32_t> counter_next{0};
     static constexpr uint32_t N_COUNTERS = 256, COUNTER_STRIDE = 32;  // in uint32_t

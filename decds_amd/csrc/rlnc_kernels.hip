@@ -562,7 +562,9 @@ void rlnc_encode_kernel(const uint8_t *__restrict__ src, size_t n, const uint8_t
 // QUEUE: after the first G tiles (tile = blockIdx.x) every next tile comes from a tile counter
 // (one atomic add per workgroup and tile, issued a tile ahead), so the tiles in flight stay one
 // resident grid wide however the workgroups' speeds differ — a fixed stride lets them drift apart.
-// counter == NULL (batches of at most G tiles): one tile per workgroup, no counter.
+// counter == NULL (batches of at most G tiles): one tile per workgroup, no counter. counter[0] is the
+// tile counter, counter[1] the exit count; both start at 0 (zeroed with the context) and the last
+// workgroup to finish zeroes them again.
 template <int DW, int WAVES, bool MSG, bool QUEUE = false>
 __global__ __launch_bounds__(WG, WAVES) __attribute__((amdgpu_waves_per_eu(WAVES, WAVES)))
 void rlnc_encode_sweep_kernel(const uint8_t *__restrict__ src, size_t n, const uint8_t *__restrict__ coeffs,
@@ -652,6 +654,14 @@ void rlnc_encode_sweep_kernel(const uint8_t *__restrict__ src, size_t n, const u
         t = tn;
         cs = csn;
     } while (more);
+    // the last workgroup out resets the counter pair (tile counter, exit count) for the next launch
+    // that takes this slot: no reset launch on the stream (a hipMemsetAsync was ~5 µs per encode)
+    if (QUEUE && counter && threadIdx.x == 0) {
+        if (atomicAdd(counter + 1, 1u) == G - 1) {
+            __atomic_store_n(counter, 0u, __ATOMIC_RELAXED);
+            __atomic_store_n(counter + 1, 0u, __ATOMIC_RELAXED);
+        }
+    }
 }
 
 // Decode: workgroup = UNIT consecutive tiles of one chunkset. The accepted rows of chunkset cs are
@@ -946,8 +956,6 @@ hipError_t launch_encode(const LaunchGeom &geom, const uint8_t *src, size_t n, c
         if (DECDS_ENC_QUEUE && (uint64_t)n * T > grid) {
             if (!geom.counters) return hipErrorInvalidValue;
             counter = geom.counters + (geom.counter_next.fetch_add(1) % LaunchGeom::N_COUNTERS) * LaunchGeom::COUNTER_STRIDE;
-            hipError_t e = hipMemsetAsync(counter, 0, sizeof(uint32_t), stream);
-            if (e != hipSuccess) return e;
         }
         void *args[] = {&src, &n, &coeffs, &dst, &pitch, const_cast<uint32_t *>(&phase), &poly, &marker, &counter};
         return hipLaunchKernel(fn, dim3(grid), dim3(WG), args, SWEEP_LDS, stream);
