@@ -96,18 +96,25 @@ int encode_range(decds_ctx *ctx, const uint8_t *blob, size_t blob_len, const uin
     HostUse uin(blob, blob_len), ucv(coeffs, n * N * K), uout(coded, n * N * F);
     HostUse urt(cm ? cm->roots : nullptr, n * 32), uprf(cm ? cm->proofs : nullptr, n * PRF);
     std::lock_guard<std::mutex> lock(ctx->host_mu);
-    const size_t sz[6] = {align256(batch * CS), align256(batch * N * F), align256(batch * N * K),
-                          cm ? align256(batch * N * 32) : 0, cm ? align256(batch * 32) : 0, cm ? align256(batch * PRF) : 0};
-    const size_t per = sz[0] + sz[1] + sz[2] + sz[3] + sz[4] + sz[5];
-    uint8_t *base, *din[SLOTS], *dout[SLOTS], *dcv[SLOTS], *ddig[SLOTS], *drt[SLOTS], *dprf[SLOTS];
+    // the coding vectors of the whole range go over in one copy ahead of the first batch (160 bytes
+    // per chunkset): staged per batch from pageable memory, each small copy held a ring piece and
+    // stalled the host's run-ahead (blob encode 15-17 GiB/s against 29 with them registered, r02zd)
+    const size_t cv_all = align256(n * N * K);
+    const size_t sz[5] = {align256(batch * CS), align256(batch * N * F), cm ? align256(batch * N * 32) : 0,
+                          cm ? align256(batch * 32) : 0, cm ? align256(batch * PRF) : 0};
+    const size_t per = sz[0] + sz[1] + sz[2] + sz[3] + sz[4];
+    uint8_t *base, *dcv, *din[SLOTS], *dout[SLOTS], *ddig[SLOTS], *drt[SLOTS], *dprf[SLOTS];
     hipError_t e;
-    if ((e = decds_ctx_scratch(ctx, SLOTS * per, &base))) return decds_hip_error(e, "hipMalloc");
+    if ((e = decds_ctx_scratch(ctx, cv_all + SLOTS * per, &base))) return decds_hip_error(e, "hipMalloc");
+    dcv = base, base += cv_all;
     for (int i = 0; i < SLOTS; i++) {
-        uint8_t **dst[6] = {&din[i], &dout[i], &dcv[i], &ddig[i], &drt[i], &dprf[i]};
-        for (int j = 0; j < 6; j++) *dst[j] = base, base += sz[j];
+        uint8_t **dst[5] = {&din[i], &dout[i], &ddig[i], &drt[i], &dprf[i]};
+        for (int j = 0; j < 5; j++) *dst[j] = base, base += sz[j];
     }
     Pipe pp;
     if ((e = pp.init())) return decds_hip_error(e, "stream/event setup");
+    if ((e = copy_h2d(dcv, coeffs, n * N * K, ucv.pinned(), ctx->in_ring, pp.h2d)))
+        return finish_call(ctx, pp, decds_hip_error(e, "H2D"));
     auto issue_d2h = [&](int k, size_t b0, size_t nb) -> int {
         if ((e = hipStreamWaitEvent(pp.d2h, pp.k_done[k], 0)) ||
             (e = copy_d2h(coded + b0 * N * F, dout[k], nb * N * F, uout.pinned(), ctx->out_ring, pp.d2h)) ||
@@ -127,7 +134,6 @@ int encode_range(decds_ctx *ctx, const uint8_t *blob, size_t blob_len, const uin
         if ((e = hipStreamWaitEvent(pp.h2d, pp.k_done[k], 0)) ||
             (e = copy_h2d(din[k], blob + off, have, uin.pinned(), ctx->in_ring, pp.h2d)) ||
             (have < nb * CS && (e = hipMemsetAsync(din[k] + have, 0, nb * CS - have, pp.h2d))) ||  // blob.rs:254 zero pad
-            (e = copy_h2d(dcv[k], coeffs + b0 * N * K, nb * N * K, ucv.pinned(), ctx->in_ring, pp.h2d)) ||
             (e = hipEventRecord(pp.in_done[k], pp.h2d))) {
             rc = decds_hip_error(e, "H2D");
             break;
@@ -137,7 +143,7 @@ int encode_range(decds_ctx *ctx, const uint8_t *blob, size_t blob_len, const uin
             rc = decds_hip_error(e, "hipStreamWaitEvent");
             break;
         }
-        if ((rc = decds_encode_batch(ctx, din[k], nb, dcv[k], dout[k], F, pp.comp))) break;
+        if ((rc = decds_encode_batch(ctx, din[k], nb, dcv + b0 * N * K, dout[k], F, pp.comp))) break;
         if (cm && (rc = decds_commit_batch(ctx, dout[k], F, nb, cm->first_id + b0, ddig[k], drt[k], dprf[k], pp.comp)))
             break;
         if ((e = hipEventRecord(pp.k_done[k], pp.comp))) {
@@ -182,7 +188,7 @@ int repair_range(decds_ctx *ctx, const uint8_t *coded_host, size_t n, const uint
         }
     } pin;
     {
-        hipError_t pe = hipHostMalloc(&pin.p, SLOTS * batch * (N + sizeof(int32_t)), hipHostMallocDefault);
+        hipError_t pe = hipHostMalloc(&pin.p, SLOTS * batch * (N + sizeof(int32_t)), DECDS_HOST_MALLOC_FLAGS);
         if (pe) return decds_hip_error(pe, "hipHostMalloc");
     }
     uint8_t *cand_h[SLOTS];
@@ -664,7 +670,7 @@ int decds_repairing_blob_new(decds_ctx *ctx, uint64_t byte_length, uint64_t num_
     hipError_t e;
     if ((e = hipStreamCreateWithFlags(&rb->s, hipStreamNonBlocking)) ||
         (e = hipMalloc(reinterpret_cast<void **>(&rb->d_small), RB_SM_BYTES)) ||
-        (e = hipHostMalloc(reinterpret_cast<void **>(&rb->h_small), RB_SM_BYTES, hipHostMallocDefault)) ||
+        (e = hipHostMalloc(reinterpret_cast<void **>(&rb->h_small), RB_SM_BYTES, DECDS_HOST_MALLOC_FLAGS)) ||
         (e = hipMalloc(reinterpret_cast<void **>(&rb->d_hdr), (num_chunksets + 1) * 32)) ||
         (e = hipMemcpyAsync(rb->d_hdr, chunkset_roots, num_chunksets * 32, hipMemcpyHostToDevice, rb->s)) ||
         (e = hipMemcpyAsync(rb->d_hdr + num_chunksets * 32, root, 32, hipMemcpyHostToDevice, rb->s)) ||

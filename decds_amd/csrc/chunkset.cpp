@@ -47,8 +47,8 @@ struct Lane {
         if (s) (void)hipStreamSynchronize(s);
         for (uint8_t *p : {d_cs, d_coded, d_small})
             if (p) (void)hipFree(p);
-        for (uint8_t *p : {h_big, h_small})
-            if (p) (void)hipHostFree(p);
+        host_pinned_free(h_big, N * F);
+        if (h_small) (void)hipHostFree(h_small);
         if (s) (void)hipStreamDestroy(s);
     }
     hipError_t init() {
@@ -56,8 +56,8 @@ struct Lane {
         if ((e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking)) || (e = hipMalloc(reinterpret_cast<void **>(&d_cs), CS)) ||
             (e = hipMalloc(reinterpret_cast<void **>(&d_coded), N * F)) ||
             (e = hipMalloc(reinterpret_cast<void **>(&d_small), SM_BYTES)) ||
-            (e = hipHostMalloc(reinterpret_cast<void **>(&h_big), N * F, hipHostMallocDefault)) ||
-            (e = hipHostMalloc(reinterpret_cast<void **>(&h_small), SM_BYTES, hipHostMallocDefault)))
+            (e = host_pinned_alloc(N * F, reinterpret_cast<void **>(&h_big))) ||
+            (e = hipHostMalloc(reinterpret_cast<void **>(&h_small), SM_BYTES, DECDS_HOST_MALLOC_FLAGS)))
             return e;
         return hipSuccess;
     }

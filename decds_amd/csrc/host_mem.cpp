@@ -28,7 +28,7 @@ struct Entry {
     size_t len;
     int regs;
     int uses;
-    bool alloc;  // from decds_host_alloc (hipHostMalloc): freed, not unregistered
+    bool alloc;  // from decds_host_alloc (host_pinned_alloc): freed, not unregistered
 };
 std::mutex g_reg_mu;
 std::map<uintptr_t, Entry> g_reg;
@@ -38,7 +38,7 @@ void finalize_if_idle(std::map<uintptr_t, Entry>::iterator it) {
     if (it->second.regs > 0 || it->second.uses > 0) return;
     void *p = reinterpret_cast<void *>(it->first);
     if (it->second.alloc)
-        (void)hipHostFree(p);
+        host_pinned_free(p, it->second.len);
     else
         (void)hipHostUnregister(p);
     g_reg.erase(it);
@@ -162,6 +162,17 @@ HostUse::~HostUse() {
     finalize_if_idle(it);
 }
 
+hipError_t host_pinned_alloc(size_t n, void **out) {
+    *out = nullptr;
+    hipError_t e = hipHostMalloc(out, n ? n : 1, DECDS_HOST_MALLOC_FLAGS);
+    if (e != hipSuccess) (void)hipGetLastError();  // this call's own error, returned
+    return e;
+}
+
+void host_pinned_free(void *p, size_t) {
+    if (p) (void)hipHostFree(p);
+}
+
 void host_parallel(size_t n, const std::function<void(size_t)> &fn) { Pool::get().run(n, fn); }
 
 void par_memcpy(void *dst, const void *src, size_t n) {
@@ -183,7 +194,7 @@ void par_memcpy(void *dst, const void *src, size_t n) {
 hipError_t BounceRing::init() {
     for (int i = 0; i < R; i++) {
         hipError_t e;
-        if (!buf[i] && (e = hipHostMalloc(reinterpret_cast<void **>(&buf[i]), PIECE, hipHostMallocDefault))) return e;
+        if (!buf[i] && (e = host_pinned_alloc(PIECE, reinterpret_cast<void **>(&buf[i])))) return e;
         if (!ev[i] && (e = hipEventCreateWithFlags(&ev[i], hipEventDisableTiming))) return e;
     }
     return hipSuccess;
@@ -255,7 +266,7 @@ BounceRing::~BounceRing() {
     abandon();
     for (int i = 0; i < R; i++) {
         if (ev[i]) (void)hipEventDestroy(ev[i]);
-        if (buf[i]) (void)hipHostFree(buf[i]);
+        if (buf[i]) host_pinned_free(buf[i], PIECE);
     }
 }
 
@@ -310,11 +321,8 @@ int decds_host_alloc(size_t len, void **out) {
     if (!out || !len) return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "null out pointer or empty size");
     *out = nullptr;
     void *p = nullptr;
-    hipError_t e = hipHostMalloc(&p, len, hipHostMallocDefault);
-    if (e != hipSuccess) {
-        (void)hipGetLastError();
-        return decds_hip_error(e, "hipHostMalloc");
-    }
+    hipError_t e = host_pinned_alloc(len, &p);
+    if (e != hipSuccess) return decds_hip_error(e, "page-locked allocation");
     std::lock_guard<std::mutex> g(g_reg_mu);
     g_reg.emplace(reinterpret_cast<uintptr_t>(p), Entry{len, 1, 0, true});
     *out = p;

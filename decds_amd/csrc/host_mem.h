@@ -14,7 +14,19 @@
 
 #include <functional>
 
+// Page-locked memory of the library (rings, lane staging, statuses, plans): non-coherent
+// (coarse-grained) hipHostMalloc memory.
+#ifndef DECDS_HOST_MALLOC_FLAGS
+#define DECDS_HOST_MALLOC_FLAGS hipHostMallocNonCoherent
+#endif
+
 namespace decds {
+
+// Large page-locked buffers (staging rings, lane staging, decds_host_alloc). Huge-page anonymous
+// memory + hipHostRegister was measured against hipHostMalloc here and moved data at the same rate
+// (blob host paths 28.7 / 35 GiB/s either way, r02zd-ze), so these stay hipHostMalloc memory.
+hipError_t host_pinned_alloc(size_t n, void **out);
+void host_pinned_free(void *p, size_t n);
 
 // A use of [p, p+n) by one call: pinned() is true iff the whole range lies in one registered
 // range, which then stays locked until the use ends (an unregister meanwhile is deferred).

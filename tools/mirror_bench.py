@@ -22,6 +22,9 @@ def main():
     ap.add_argument("--threads", default="1,4,8,16")
     ap.add_argument("--seconds", type=float, default=2.0)
     ap.add_argument("--blob-gib", type=float, default=2.0)
+    ap.add_argument("--reps", type=int, default=5, help="timed blob-path repetitions per mode (median)")
+    ap.add_argument("--modes", default="pageable,host_alloc,host_register")
+    ap.add_argument("--blob-only", action="store_true")
     a = ap.parse_args()
     import numpy as np
     import decds_amd
@@ -29,7 +32,7 @@ def main():
     from decds_amd._capi import CHUNKSET_BYTES as CS, K, N
 
     ctx = decds_amd.Context(0)
-    for T in [int(t) for t in a.threads.split(",")]:
+    for T in ([] if a.blob_only else [int(t) for t in a.threads.split(",")]):
         datas = [codec.fill_random_host(0x77 + t, CS).tobytes() for t in range(T)]
         coeffs = [codec.fill_random_host(0x88 + t, N * K).tobytes() for t in range(T)]
         # one warm call per thread slot (lane creation: stream, device buffers, pinned staging)
@@ -76,14 +79,15 @@ def main():
         print(json.dumps({"path": "decds_repairing_chunkset_repair (add 10 chunks + repair)", "threads": T,
                           "chunksets": sum(counts), "GiBps": round(sum(counts) * CS / GIB / dt, 2)}), flush=True)
 
-    # blob-level host paths over the same kind of data, pageable and registered
+    # blob-level host paths over the same kind of data: pageable (staged through the library's rings),
+    # library page-locked memory (decds_host_alloc) and registered caller memory (decds_host_register)
     n = max(1, int(a.blob_gib * GIB) // CS)
     blob = codec.fill_random_host(0x99, n * CS)
     cv = codec.fill_random_host(0x9A, n * N * K)
     cand = np.stack([np.random.default_rng(c).permutation(N) for c in range(n)]).astype(np.uint8)
-    for mode in ("pageable", "registered"):
-        bufs = []
-        if mode == "registered":
+    for mode in a.modes.split(","):
+        bufs, regs = [], []
+        if mode == "host_alloc":
             hb = [decds_amd.HostBuffer(blob.nbytes), decds_amd.HostBuffer(n * N * codec.CODED_PIECE_BYTES),
                   decds_amd.HostBuffer(blob.nbytes)]
             hb[0].array[:] = blob
@@ -91,18 +95,29 @@ def main():
             bufs = hb
         else:
             b_in, coded_out, rep_out = blob, np.empty((n * N, codec.CODED_PIECE_BYTES), np.uint8), np.empty(blob.nbytes, np.uint8)
+            coded_out[:] = 0
+            rep_out[:] = 0
+            if mode == "host_register":
+                regs = [blob, coded_out, rep_out]
+                for r in regs:
+                    codec.host_register(r)
         codec.blob_encode_host(ctx, b_in, cv, out=coded_out)  # warm (slot buffers, rings)
-        t0 = time.perf_counter()
-        codec.blob_encode_host(ctx, b_in, cv, out=coded_out)
-        te = time.perf_counter() - t0
         codec.blob_repair_host(ctx, coded_out, cand, blob.nbytes, out=rep_out)
-        t0 = time.perf_counter()
-        _, st = codec.blob_repair_host(ctx, coded_out, cand, blob.nbytes, out=rep_out)
-        tr = time.perf_counter() - t0
+        te, tr = [], []
+        for _ in range(a.reps):
+            t0 = time.perf_counter()
+            codec.blob_encode_host(ctx, b_in, cv, out=coded_out)
+            te.append(time.perf_counter() - t0)
+            t0 = time.perf_counter()
+            _, st = codec.blob_repair_host(ctx, coded_out, cand, blob.nbytes, out=rep_out)
+            tr.append(time.perf_counter() - t0)
         assert (st == 0).all() and np.array_equal(rep_out, blob)
-        print(json.dumps({"path": "decds_blob_encode_host / _repair_host", "memory": mode, "chunksets": n,
+        te, tr = float(np.median(te)), float(np.median(tr))
+        print(json.dumps({"path": "decds_blob_encode_host / _repair_host", "memory": mode, "chunksets": n, "reps": a.reps,
                           "encode_GiBps": round(n * CS / GIB / te, 2), "repair_GiBps": round(n * CS / GIB / tr, 2)}),
               flush=True)
+        for r in regs:
+            codec.host_unregister(r)
         for b in bufs:
             b.free()
 
