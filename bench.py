@@ -290,7 +290,7 @@ def main():
     dec_gbs = dec_bytes / (dec_ms * 1e-3) / 1e9
     enc_kernel = _lib().decds_encode_kernel_name(n).decode()
     dominant = enc_kernel if enc_ms >= dec_ms else "rlnc_decode_kernel"
-    achieved = enc_gbs if dominant == "rlnc_encode_kernel" else dec_gbs
+    achieved = enc_gbs if dominant == enc_kernel else dec_gbs
     traffic = None
     try:
         with open(args.traffic_json) as f:
@@ -335,7 +335,7 @@ def main():
             "breakdown": {"encode_ms": round(enc_ms, 4), "plan_ms": round(plan_ms, 4), "decode_ms": round(dec_ms, 4),
                           "encode_GBps": round(enc_gbs, 1), "decode_GBps": round(dec_gbs, 1),
                           "encode_blob_GiBps": round(n * CS / GIB / (enc_ms * 1e-3), 1),
-                          "repair_blob_GiBps": round(n * CS / GIB / ((plan_ms + dec_ms) * 1e-3), 1),
+                          "repair_blob_GiBps": round(rep_len / GIB / ((plan_ms + dec_ms) * 1e-3), 1),
                           "ready_chunksets": n_ready, "not_ready_chunksets": n - n_ready},
             "commitment": commit,
             "encode_batch_sweep": sweep,
