@@ -81,7 +81,42 @@ __global__ __launch_bounds__(256) void enc_k(const uint8_t *__restrict__ in, uin
 
 // decode pattern: inputs = 10 of the 16 coded rows (rows 0, 2, 3, 5, 6, 8, 9, 11, 13, 15) in layout
 // TM, outputs = pieces of the contiguous chunkset
-template <int UNIT, bool TM, uint64_t OROW = LB>
+// SPLIT: the piece stores of the real (byte-misaligned) layout cut at 4-byte boundaries inside each
+// lane — a 12-byte store of the lane's dword-aligned middle plus 1-2 byte / short stores of its head
+// and tail, no cross-lane exchange; A4: one 16-byte store 4-byte aligned (address rounded down, wrong
+// bytes: the pattern of a dword-aligned realignment)
+enum : int { ST_PLAIN = 0, ST_SPLIT = 1, ST_A4 = 2 };
+typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
+template <int ST>
+__device__ __forceinline__ void piece_store(u32x4 v, __amdgpu_buffer_rsrc_t ro, uint32_t o, uint32_t r) {
+    if (ST == ST_PLAIN || r == 0) {
+        __builtin_amdgcn_raw_buffer_store_b128(v, ro, o, 0, 0);
+    } else if (ST == ST_A4) {
+        __builtin_amdgcn_raw_buffer_store_b128(v, ro, o - r, 0, 0);
+    } else {
+        const uint32_t h = 4 - r;
+        uint32_t w[5] = {v.x, v.y, v.z, v.w, 0};
+        u32x3 mid;
+        mid.x = __builtin_amdgcn_alignbyte(w[1], w[0], h);
+        mid.y = __builtin_amdgcn_alignbyte(w[2], w[1], h);
+        mid.z = __builtin_amdgcn_alignbyte(w[3], w[2], h);
+        __builtin_amdgcn_raw_buffer_store_b96(mid, ro, o + h, 0, 0);
+        if (r == 1) {
+            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)w[0], ro, o, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(w[0] >> 8), ro, o + 1, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(w[3] >> 24), ro, o + 15, 0, 0);
+        } else if (r == 2) {
+            __builtin_amdgcn_raw_buffer_store_b16((uint16_t)w[0], ro, o, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(w[3] >> 16), ro, o + 14, 0, 0);
+        } else {
+            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)w[0], ro, o, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(w[3] >> 8), ro, o + 13, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(w[3] >> 24), ro, o + 15, 0, 0);
+        }
+    }
+}
+
+template <int UNIT, bool TM, uint64_t OROW = LB, int ST = ST_PLAIN>
 __global__ __launch_bounds__(256) void dec_k(const uint8_t *__restrict__ in, uint8_t *__restrict__ out, size_t n) {
     extern __shared__ uint8_t lds[];
     const uint32_t t0 = blockIdx.x * UNIT, cs = t0 / TILES, tile0 = t0 % TILES;
@@ -101,7 +136,7 @@ __global__ __launch_bounds__(256) void dec_k(const uint8_t *__restrict__ in, uin
 #pragma unroll
         for (int k = 0; k < 10; k++) acc ^= x[k];
 #pragma unroll
-        for (int i = 0; i < 10; i++) __builtin_amdgcn_raw_buffer_store_b128(acc + (uint32_t)i, ro, (uint32_t)(i * OROW) + col, 0, 0);
+        for (int i = 0; i < 10; i++) piece_store<ST>(acc + (uint32_t)i, ro, (uint32_t)(i * OROW) + col, (uint32_t)(i * OROW) & 3);
     }
     if (acc.x == 0x9E3779B9u && threadIdx.x == 999) lds[0] = 1;
 }
@@ -159,7 +194,9 @@ int main(int argc, char **argv) {
     CK(hipMemset(src, 0x3c, nmax * CSB));
     CK(hipMemset(coded, 0x5a, nmax * 16 * PITCH));
     constexpr uint32_t LDS2 = 80 * 1024;  // 2 workgroups per CU, as the codec kernels' VGPRs allow
-    for (const void *f : {(const void *)dec_k<1, false>, (const void *)dec_k<1, false, 1u << 20>, (const void *)enc_k<4, 1, false>, (const void *)enc_k<4, 0, false>, (const void *)enc_k<4, 2, false>,
+    for (const void *f : {(const void *)dec_k<1, false>, (const void *)dec_k<1, false, 1u << 20>, (const void *)dec_k<1, false, LB, ST_SPLIT>,
+                          (const void *)dec_k<1, false, (1u << 20) + 16>,
+                          (const void *)dec_k<1, false, LB, ST_A4>, (const void *)enc_k<4, 1, false>, (const void *)enc_k<4, 0, false>, (const void *)enc_k<4, 2, false>,
                           (const void *)enc_k<2, 0, false>, (const void *)enc_k<1, 0, false>, (const void *)enc_k<8, 2, false>})
         CK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, LDS2));
     for (size_t n : {103, 256, 1024}) {
@@ -181,8 +218,12 @@ int main(int argc, char **argv) {
             constexpr uint32_t LDS3 = 52 * 1024;
             run("dec_u1_3wg", n, db, [&] { dec_k<1, false><<<g1, 256, LDS3>>>(coded, rep, n); }, a);
             run("dec_u1_outA_3wg", n, db, [&] { dec_k<1, false, 1u << 20><<<g1, 256, LDS3>>>(coded, rep, n); }, a);
+            run("dec_u1_outA16_3wg", n, db, [&] { dec_k<1, false, (1u << 20) + 16><<<g1, 256, LDS3>>>(coded, rep, n); }, a);
+            run("dec_u1_split_3wg", n, db, [&] { dec_k<1, false, LB, ST_SPLIT><<<g1, 256, LDS3>>>(coded, rep, n); }, a);
+            run("dec_u1_a4_3wg", n, db, [&] { dec_k<1, false, LB, ST_A4><<<g1, 256, LDS3>>>(coded, rep, n); }, a);
             run("dec_u1", n, db, [&] { dec_k<1, false><<<g1, 256>>>(coded, rep, n); }, a);
             run("dec_u1_outA", n, db, [&] { dec_k<1, false, 1u << 20><<<g1, 256>>>(coded, rep, n); }, a);
+            run("dec_u1_split", n, db, [&] { dec_k<1, false, LB, ST_SPLIT><<<g1, 256>>>(coded, rep, n); }, a);
             if (!only.empty()) continue;
         }
         run("enc_rows_u4_xcd", n, eb, [&] { enc_k<4, 1, false><<<g4, 256>>>(src, coded, n); }, a);
