@@ -229,7 +229,8 @@ def main():
         stream.synchronize()
         c_ms = cev[0].elapsed_time(cev[-1]) / args.steps
         # ChunkSet::new as one call (encode + commitment, chunkset.rs:37-63): on rows 16 bytes past a
-        # 128-byte boundary the chunk hashing is fused into the encode kernel (+ commit_fold_kernel)
+        # 128-byte boundary the chunk hashing is fused into the encode kernel (rlnc_encode_hash_kernel:
+        # every coded 128-byte step hashed from LDS right behind its stores) + commit_fold_kernel
         with torch.cuda.stream(stream):
             mbuf = torch.empty(n * N * codec.CODED_PITCH_ALIGNED + 256, dtype=torch.uint8, device=dev)
             moff = (16 - mbuf.data_ptr()) % 128
@@ -252,7 +253,7 @@ def main():
                   "chunkset_new": {"what": "ChunkSet::new = encode + commitment (decds_encode_commit_batch)",
                                    "separate_ms": round(enc_ms + c_ms, 4),
                                    "fused_ms": round(f_ms, 4),
-                                   "fused_kernels": "rlnc_encode_kernel<COMMIT> + commit_fold_kernel + chunkset_merkle_kernel",
+                                   "fused_kernels": "rlnc_encode_hash_kernel + commit_fold_kernel + chunkset_merkle_kernel",
                                    "fused_blob_GiBps": round(n * CS / GIB / (f_ms * 1e-3), 1)}}
 
     # encode batch sweep beside the headline step (north_star: "at batch >= 256"):

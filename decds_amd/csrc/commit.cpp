@@ -166,7 +166,7 @@ int decds_commit_batch(decds_ctx *ctx, const uint8_t *coded, size_t pitch, size_
     return e == hipSuccess ? DECDS_OK : decds_hip_error(e, "commit kernels launch");
 }
 
-size_t decds_encode_commit_workspace_bytes(size_t n) { return n * N * 64 * 32; }
+size_t decds_encode_commit_workspace_bytes(size_t n) { return n * N * encode_commit_subtrees() * 32; }
 
 int decds_encode_commit_batch(decds_ctx *ctx, const uint8_t *src, size_t n, const uint8_t *coeffs, uint8_t *dst,
                               size_t pitch, uint64_t first_chunkset_id, uint8_t *digests, uint8_t *roots,
@@ -186,8 +186,8 @@ int decds_encode_commit_batch(decds_ctx *ctx, const uint8_t *src, size_t n, cons
     auto *sub = static_cast<uint32_t *>(workspace);
     hipError_t e = launch_encode_commit(src, n, coeffs, dst, pitch, ctx->poly, ctx->marker, first_chunkset_id, sub,
                                         (hipStream_t)stream);
-    if (e) return decds_hip_error(e, "rlnc_encode_kernel<COMMIT> launch");
-    e = launch_commit_fold(dst, pitch, n, sub, digests, roots, proofs, (hipStream_t)stream);
+    if (e) return decds_hip_error(e, "fused encode + chunk hashing launch");
+    e = launch_commit_fold(dst, pitch, n, sub, encode_commit_subtrees(), digests, roots, proofs, (hipStream_t)stream);
     return e == hipSuccess ? DECDS_OK : decds_hip_error(e, "commit_fold_kernel launch");
 }
 

@@ -174,26 +174,32 @@ __global__ __launch_bounds__(DG_WG) void chunk_digest_kernel(const uint8_t *__re
     }
 }
 
-// Digest of each coded row from the fused encode's 64 subtree values (rlnc_encode_kernel<COMMIT>):
-// one wave per row, lane i holds subtree i (chunks 16i .. 16i+15); six PARENT levels fold them into
-// the 1024-chunk left tree, then the 27-byte 1025th chunk joins under ROOT, as chunk_digest_kernel.
-constexpr uint32_t SUBTREES = FULL_CHUNKS / 16;  // 64
-__global__ __launch_bounds__(SUBTREES) void commit_fold_kernel(const uint8_t *__restrict__ coded, size_t pitch,
-                                                               const uint32_t *__restrict__ sub,
-                                                               uint8_t *__restrict__ digests) {
+// Digest of each coded row from the fused encode's 256 aligned 4-chunk subtree values
+// (rlnc_encode_hash_kernel). One wave per row: lane i folds subtrees 4i .. 4i+3 into the 16-chunk
+// subtree i, six PARENT levels fold those into the 1024-chunk left tree, then the 27-byte 1025th
+// chunk joins under ROOT, as chunk_digest_kernel.
+constexpr uint32_t FOLD_LANES = 64, SUB_PER_ROW = FULL_CHUNKS / 4;  // 256
+__global__ __launch_bounds__(FOLD_LANES) void commit_fold_kernel(const uint8_t *__restrict__ coded, size_t pitch,
+                                                                 const uint32_t *__restrict__ sub,
+                                                                 uint8_t *__restrict__ digests) {
     const size_t row = blockIdx.x;
     const uint32_t i = threadIdx.x;
-    uint32_t cv[8];
-    const uint32_t *p = sub + (row * SUBTREES + i) * 8;
+    const uint32_t *p = sub + (row * SUB_PER_ROW + 4 * i) * 8;
+    uint32_t a[8], b[8], lo[8], hi[8], cv[8];
 #pragma unroll
-    for (int w = 0; w < 8; w++) cv[w] = p[w];
+    for (int w = 0; w < 8; w++) a[w] = p[w], b[w] = p[8 + w];
+    b3::parent(a, b, 0, lo);
+#pragma unroll
+    for (int w = 0; w < 8; w++) a[w] = p[16 + w], b[w] = p[24 + w];
+    b3::parent(a, b, 0, hi);
+    b3::parent(lo, hi, 0, cv);
 #pragma unroll
     for (uint32_t k = 0; k < 6; k++) {
-        uint32_t sib[8], lo[8], hi[8];
+        uint32_t sib[8];
         const bool right = (i >> k) & 1u;
 #pragma unroll
         for (int w = 0; w < 8; w++) {
-            sib[w] = __shfl_xor(cv[w], 1 << k, SUBTREES);
+            sib[w] = __shfl_xor(cv[w], 1 << k, FOLD_LANES);
             lo[w] = right ? sib[w] : cv[w];
             hi[w] = right ? cv[w] : sib[w];
         }
@@ -316,10 +322,11 @@ hipError_t launch_commit(const uint8_t *coded, size_t pitch, size_t n, uint64_t 
     return hipGetLastError();
 }
 
-hipError_t launch_commit_fold(const uint8_t *coded, size_t pitch, size_t n, const uint32_t *sub, uint8_t *digests,
-                              uint8_t *roots, uint8_t *proofs, hipStream_t stream) {
+hipError_t launch_commit_fold(const uint8_t *coded, size_t pitch, size_t n, const uint32_t *sub, uint32_t per_row,
+                              uint8_t *digests, uint8_t *roots, uint8_t *proofs, hipStream_t stream) {
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(commit_fold_kernel, dim3((uint32_t)(n * N)), dim3(SUBTREES), 0, stream, coded, pitch, sub, digests);
+    if (per_row != SUB_PER_ROW) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(commit_fold_kernel, dim3((uint32_t)(n * N)), dim3(FOLD_LANES), 0, stream, coded, pitch, sub, digests);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(chunkset_merkle_kernel, dim3((uint32_t)((n * N + MK_WG - 1) / MK_WG)), dim3(MK_WG), 0, stream,

@@ -22,9 +22,11 @@ hipError_t launch_encode(const LaunchGeom &g, const uint8_t *src, size_t n, cons
                          uint8_t *dst, size_t pitch, uint32_t poly, uint32_t marker,
                          hipStream_t stream);
 // ChunkSet::new's encode with the commitment's chunk hashing fused (rows at a 16-byte-aligned pitch
-// and base only: encode_commit_fusable). sub: n x 16 x 64 x 32 B of 16-chunk subtree values, completed
-// into digests / roots / proofs by launch_commit_fold.
+// and base only: encode_commit_fusable). sub: n x 16 x encode_commit_subtrees() x 32 B of aligned
+// subtree values (256 of 4 chunks per row, or 64 of 16 with the unit-hash form), completed into
+// digests / roots / proofs by launch_commit_fold.
 bool encode_commit_fusable(const uint8_t *dst, size_t pitch);
+uint32_t encode_commit_subtrees();
 hipError_t launch_encode_commit(const uint8_t *src, size_t n, const uint8_t *coeffs, uint8_t *dst, size_t pitch,
                                 uint32_t poly, uint32_t marker, uint64_t first_id, uint32_t *sub, hipStream_t stream);
 hipError_t launch_repair_plan(const uint8_t *coded, size_t pitch, size_t n, const uint8_t *cand,

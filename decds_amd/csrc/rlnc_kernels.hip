@@ -195,13 +195,13 @@ __device__ __forceinline__ Vec<DW> ldrow(const uint8_t *base, uint32_t off) {
         return __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0);
 }
 
-template <int DW>
+template <int DW, int AUX = 0>
 __device__ __forceinline__ void strow(uint8_t *base, uint32_t off, Vec<DW> v) {
     const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, 0, BUF_RECORDS, 0x00020000);
     if constexpr (DW == 4)
-        __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, AUX);
     else
-        __builtin_amdgcn_raw_buffer_store_b64(v, r, off, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b64(v, r, off, 0, AUX);
 }
 
 template <int NIN, int DW>
@@ -297,10 +297,15 @@ __device__ __forceinline__ void lookups(std::integer_sequence<int, Gs...>, uint3
 // One lane block of 4*DW columns: out_j[col0 ..) = sum_i M[j][i] * in_i[col0 ..), tables at LDS
 // byte TB. x holds this block's inputs on entry and on exit the inputs at column ncol0 of the rows
 // at ibase + ioff (the next block's: the same chunkset's rows, or the next tile's chunkset's).
-template <int NIN, int NOUT, int DW, uint32_t TB = 0>
+// sink(j, v): also hand output j's bytes elsewhere (the fused commitment's LDS message slots)
+struct NoSink {
+    template <typename V>
+    __device__ void operator()(int, const V &) const {}
+};
+template <int NIN, int NOUT, int DW, uint32_t TB = 0, typename Sink = NoSink, int SAUX = 0>
 __device__ __forceinline__ void combine_block(Vec<DW> (&x)[NIN], uint8_t *obase, const uint32_t (&ooff)[NOUT],
                                               uint32_t col0, const uint8_t *ibase, const uint32_t (&ioff)[NIN],
-                                              uint32_t ncol0) {
+                                              uint32_t ncol0, Sink sink = Sink{}) {
     uint32_t acc[4 * DW][4];  // acc[column][output group]: byte b = output 4*group + b
 #pragma unroll
     for (int c = 0; c < 4 * DW; c++)
@@ -322,7 +327,10 @@ __device__ __forceinline__ void combine_block(Vec<DW> (&x)[NIN], uint8_t *obase,
             Vec<DW> v;
 #pragma unroll
             for (int w = 0; w < DW; w++) v[w] = o[b][w];
-            if (j < NOUT) strow<DW>(obase, ooff[j] + col0, v);
+            if (j < NOUT) {
+                strow<DW, SAUX>(obase, ooff[j] + col0, v);
+                sink(j, v);
+            }
         }
     }
 }
@@ -338,9 +346,9 @@ __device__ __forceinline__ void combine_block(Vec<DW> (&x)[NIN], uint8_t *obase,
 // le64 ids (16 B) || row, so payload column p is message byte p + 26 and a block starting at column
 // 16m - 26 is message block m. Tiles then start MSG_SHIFT = 2 blocks early (tile t = message blocks
 // [256t, 256t + 256), its first two lanes idle in tile 0) and the last block joins the edge columns
-// (6 head + 27 tail): a tile is exactly 4 BLAKE3 chunks of every row, which the fused commitment
-// (rlnc_encode_kernel<COMMIT>) hashes right behind the stores. On rows at 16 mod 128 every wave's
-// 1 KiB store run is then 128-byte aligned.
+// (6 head + 27 tail): a tile is exactly 4 BLAKE3 chunks of every row, and the fused commitment
+// (rlnc_encode_hash_kernel) walks the same geometry in 128-byte steps. On rows at 16 mod 128 every
+// wave's store run is then 128-byte aligned.
 constexpr uint32_t MAX_FULL_PHASE = (uint32_t)(CS - (K - 1) * L) - MAIN_COLS;
 static_assert(MAX_FULL_PHASE == 7, "layout");
 template <int DW> constexpr uint32_t COLS = 4 * DW;
@@ -411,85 +419,15 @@ __device__ __forceinline__ uint32_t xcd_eighth_unit() {
     return x * per + (x < rem ? x : rem) + q;
 }
 
-// ---- fused commitment (ChunkSet::new, chunkset.rs:43-63) ---------------------------------------
-// With message tiling a unit of 4 tiles is BLAKE3 chunks [16u, 16u + 16) of every one of the
-// chunkset's 16 rows: 256 chunks, one per lane. Right behind its own row stores (still in L2) the
-// workgroup hashes them — lane l: row l / 16, chunk 16u + l % 16, 16 compressions over 64-byte
-// blocks read back with sc0 loads (line-aligned on 16-mod-128 rows) — and folds each row's 16 chunk
-// values into their subtree (an aligned subtree of the row's 1024-chunk left tree), written to
-// sub[(row * 64 + u) * 8]. commit_fold_kernel (commit_kernels.hip) then completes every row's digest
-// (64 subtrees + the 27-byte 1025th chunk) and the Merkle trees. The hashing is VALU work that runs
-// while the CU's other workgroup streams: it overlaps the encode's HBM time instead of following it.
-constexpr uint32_t FUSED_UNITS = 64;  // units of 16 BLAKE3 chunks per row (1024 full chunks)
-struct Msg64 {
-    uint32_t w[16];
-};
-
-__device__ __forceinline__ Msg64 ld_msg(__amdgpu_buffer_rsrc_t r, uint32_t off) {
-    Msg64 m;
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, off + 16 * k, 0, 1);  // sc0: bypass the L1
-        m.w[4 * k] = v.x, m.w[4 * k + 1] = v.y, m.w[4 * k + 2] = v.z, m.w[4 * k + 3] = v.w;
-    }
-    return m;
-}
-
-__device__ __forceinline__ void hash_unit(uint8_t *obase, size_t pitch, uint32_t u, uint64_t cs_id,
-                                          uint32_t *__restrict__ sub_cs) {
-    __syncthreads();  // s_waitcnt vmcnt(0) + barrier: every row store of this workgroup is in L2
-    const uint32_t l = threadIdx.x, j = l >> 4, q = l & 15u, c = u * 16 + q;
-    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(obase, 0, BUF_RECORDS, 0x00020000);
-    // message byte 1024c of row j sits at row + 1024c - 16; for c == 0 the first 16 bytes are the ids
-    // (that offset wraps past the descriptor's range for row 0: the load returns zeros, replaced below)
-    const uint32_t off = (uint32_t)(j * pitch) + c * b3::CHUNK - 16u;
-    uint32_t cv[8];
-#pragma unroll
-    for (int i = 0; i < 8; i++) cv[i] = b3::K3.iv[i];
-    Msg64 m = ld_msg(r, off);
-    if (c == 0) {
-        const uint64_t chunk_id = cs_id * N + j;  // chunkset.rs:47
-        m.w[0] = (uint32_t)cs_id, m.w[1] = (uint32_t)(cs_id >> 32);
-        m.w[2] = (uint32_t)chunk_id, m.w[3] = (uint32_t)(chunk_id >> 32);
-    }
-#pragma unroll 1
-    for (uint32_t b = 0; b < 16; b++) {
-        const Msg64 nxt = ld_msg(r, off + b3::BLOCK * (b < 15 ? b + 1 : b));  // in flight across the compression
-        const uint32_t flags = (b == 0 ? b3::CHUNK_START : 0u) | (b == 15 ? b3::CHUNK_END : 0u);
-        b3::compress(cv, m.w, c, b3::BLOCK, flags, cv);
-        m = nxt;
-    }
-    // 16 chunks of row j (lanes 16j .. 16j+15) -> their subtree: level k pairs lanes q, q ^ 2^k
-#pragma unroll
-    for (uint32_t k = 0; k < 4; k++) {
-        uint32_t sib[8], lo[8], hi[8];
-        const bool right = (q >> k) & 1u;
-#pragma unroll
-        for (int i = 0; i < 8; i++) {
-            sib[i] = __shfl_xor(cv[i], 1 << k, 16);
-            lo[i] = right ? sib[i] : cv[i];
-            hi[i] = right ? cv[i] : sib[i];
-        }
-        b3::parent(lo, hi, 0, cv);
-    }
-    if (q == 0) {
-        uint32_t *o = sub_cs + (j * FUSED_UNITS + u) * 8;
-#pragma unroll
-        for (int i = 0; i < 8; i++) o[i] = cv[i];
-    }
-}
-
-// Encode: workgroup = UNIT consecutive tiles of one chunkset (TILES<DW> tiles per chunkset).
+// Encode: workgroup = UNIT consecutive tiles of one chunkset (TILES<DW> tiles per chunkset); the
+// launcher's form for batches above ENC_SWEEP_MAX_N (A/B builds only: the default limit is the C-ABI's).
 // The unit is walked as "segments up to the next chunkset boundary" although it never crosses one
 // (UNIT divides TILES): with that loop hipcc allocated 228 VGPRs and no spills, the straight-line
 // form of the same work 256 VGPRs + 53 spilled (-Rpass-analysis=kernel-resource-usage).
-// COMMIT (UNIT 4, DW 4, message tiling): hash_unit after the unit's tiles; first_id = the batch's
-// first chunkset id, sub = n x 16 x 64 subtree chaining values.
-template <uint32_t UNIT, bool XCD_ORDER, int DW, int WAVES, bool MSG, bool COMMIT = false>
+template <uint32_t UNIT, bool XCD_ORDER, int DW, int WAVES, bool MSG>
 __global__ __launch_bounds__(WG, WAVES) __attribute__((amdgpu_waves_per_eu(WAVES, WAVES)))
 void rlnc_encode_kernel(const uint8_t *__restrict__ src, size_t n, const uint8_t *__restrict__ coeffs,
-                        uint8_t *__restrict__ dst, size_t pitch, uint32_t phase, uint32_t poly, uint32_t marker,
-                        uint64_t first_id, uint32_t *__restrict__ sub) {
+                        uint8_t *__restrict__ dst, size_t pitch, uint32_t phase, uint32_t poly, uint32_t marker) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     constexpr uint32_t T = TILES<DW>;
     static_assert(T % UNIT == 0, "a workgroup's tiles stay in one chunkset");
@@ -532,21 +470,161 @@ void rlnc_encode_kernel(const uint8_t *__restrict__ src, size_t n, const uint8_t
     const uint64_t total = (uint64_t)n * T;
     uint32_t t0 = (XCD_ORDER ? xcd_eighth_unit() : blockIdx.x) * UNIT;
     const uint32_t t1 = (uint32_t)(t0 + UNIT < total ? t0 + UNIT : total);
-    [[maybe_unused]] const uint32_t unit0 = t0;
     while (t0 < t1) {
         const uint32_t cs_end = (t0 / T + 1) * T;
         const uint32_t te = cs_end < t1 ? cs_end : t1;
         segment(t0, te);
         t0 = te;
     }
-    if constexpr (COMMIT) {
-        static_assert(MSG && UNIT * TILE_BLOCKS * COLS<DW> == 16 * b3::CHUNK && T / UNIT == FUSED_UNITS,
-                      "a commit unit is 16 BLAKE3 chunks of every row");
-        if (unit0 < t1) {
-            const uint32_t cs = unit0 / T;
-            hash_unit(dst + (size_t)cs * N * pitch, pitch, (unit0 % T) / UNIT, first_id + cs,
-                      sub + (size_t)cs * N * FUSED_UNITS * 8);
+}
+
+// ---- fused commitment, wave-step form (ChunkSet::new, chunkset.rs:43-63) ------------------------
+// The unit-hash form above re-reads each unit's 256 KiB of coded rows after its stores (no longer in
+// L2 by then: 1.7 GB of extra traffic at cfg2). Here no coded byte is read back. A wave owns BLAKE3
+// chunks [4U, 4U + 4) of all 16 rows of one chunkset — 64 chunks, one per lane (lane h: row h >> 2,
+// chunk 4U + (h & 3)) — and walks them in steps of STEP = 16 lane blocks of message bytes (128 with
+// 8-column blocks, 256 with 16-column blocks): the step's 4 x STEP coded columns (4 runs of 16 lane
+// blocks) are encoded, stored to HBM in whole 128-byte lines (rows 16 bytes past a 128-byte boundary:
+// message byte m of a row sits at m mod 128 of a line) and written into the wave's LDS slots, from
+// which each lane reads its chunk's STEP / 64 blocks and compresses them. The next step's inputs are
+// in flight across the compressions (the rolling prefetch of combine_block). After the last step lanes
+// fold their row's 4 chunk values into the aligned 4-chunk subtree; commit_fold_kernel<256> finishes.
+// LDS: chunk slot h = STEP bytes at h * STEP, its 16-byte pieces XOR-swizzled by key(h) so that the
+// 16 lanes of every ds_read_b128 group read 16 distinct bank quads and every store group fills whole
+// bank rows without conflicts.
+constexpr uint32_t FH_WAVE_CHUNKS = 4;                                 // chunks per row per wave
+constexpr uint32_t FH_WAVE_UNITS = 1024 / FH_WAVE_CHUNKS;              // 256 wave units per chunkset
+constexpr uint32_t FH_WAVES = WG / 64;                                 // 4
+constexpr uint32_t FH_WG_UNITS = FH_WAVE_UNITS / FH_WAVES;             // 64 workgroups per chunkset
+constexpr uint32_t MSG_HEAD = 16 + K + MSG_PHASE;                      // message byte of the first lane block
+static_assert(MSG_HEAD == 32, "message tiling");
+// coded-row stores non-temporal: the rows are never read back here, and out of L2 they leave it to the
+// input lines whose second half the next step reads (PMC reads 1.69 -> 1.44 GB per cfg2 launch, -0.6 %)
+constexpr int FH_STORE_AUX = 2;
+template <int DW> constexpr uint32_t FH_STEP = 16 * COLS<DW>;           // 128 / 256 message bytes per chunk
+template <int DW> constexpr uint32_t FH_LDS = LDS_BYTES + FH_WAVES * 64 * FH_STEP<DW>;  // 37 / 69 KiB
+template <int DW>
+__device__ __forceinline__ uint32_t fh_key(uint32_t slot) {
+    constexpr uint32_t R = 256 / FH_STEP<DW>, P = FH_STEP<DW> / 16;  // slots per bank row, pieces per slot
+    return (slot / R) & (P - 1);
+}
+
+template <int DW, int WAVES>
+__global__ __launch_bounds__(WG, WAVES) __attribute__((amdgpu_waves_per_eu(WAVES, WAVES)))
+void rlnc_encode_hash_kernel(const uint8_t *__restrict__ src, size_t n, const uint8_t *__restrict__ coeffs,
+                             uint8_t *__restrict__ dst, size_t pitch, uint32_t poly, uint32_t marker,
+                             uint64_t first_id, uint32_t *__restrict__ sub) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    constexpr uint32_t STEP = FH_STEP<DW>, STEPS = b3::CHUNK / STEP, BPS = STEP / b3::BLOCK;  // blocks per step
+    const uint32_t cs = blockIdx.x / FH_WG_UNITS, gu = blockIdx.x % FH_WG_UNITS;
+    if (cs >= n) return;
+    const uint32_t h = threadIdx.x & 63u;
+    const uint32_t U = __builtin_amdgcn_readfirstlane(gu * FH_WAVES + (threadIdx.x >> 6));
+    const uint8_t *M = coeffs + (size_t)cs * N * K;
+    const uint8_t *ibase = src + (size_t)cs * CS;
+    uint8_t *obase = dst + (size_t)cs * N * pitch;
+    uint32_t ioff[K], ooff[N];
+#pragma unroll
+    for (int i = 0; i < (int)K; i++) ioff[i] = (uint32_t)(i * L);
+#pragma unroll
+    for (int j = 0; j < (int)N; j++) ooff[j] = (uint32_t)(j * pitch + K);
+    // encode lane: run eq = h >> 4 (chunk 4U + eq), lane block eb = h & 15 of the step's STEP bytes;
+    // message byte m is payload column m - 26 (ids 16 B, coding vector 10 B); m < 32 are not lane columns
+    const uint32_t eq = h >> 4, eb = h & 15u;
+    const uint32_t m0 = (FH_WAVE_CHUNKS * U + eq) * b3::CHUNK + COLS<DW> * eb;
+    auto col = [&](uint32_t st) {
+        const uint32_t m = m0 + st * STEP;
+        return st < STEPS && m >= MSG_HEAD ? m - (16 + K) : OOB_COL;
+    };
+    const uint32_t cw = table_coeffs<K, N>(M, K);
+    Vec<DW> x[K];
+    load_block<K, DW>(x, ibase, ioff, col(0));
+    build_tables<K, N>(lds, cw, poly);
+    lds_barrier();
+    if (gu == 0) {  // the chunkset's first workgroup: coding-vector prefixes and the edge columns
+        for (uint32_t idx = threadIdx.x; idx < N * K; idx += WG) obase[(idx / K) * pitch + idx % K] = M[idx];
+        for (uint32_t idx = threadIdx.x; idx < edge_cols<DW, true>(MSG_PHASE) * N; idx += WG) {
+            const uint32_t j = idx % N, c = edge_col<DW, true>(idx / N, MSG_PHASE);
+            uint32_t y = 0;
+#pragma unroll
+            for (uint32_t i = 0; i < K; i++) {
+                const uint64_t p = (uint64_t)i * L + c;
+                const uint32_t xv = p < CS ? ibase[p] : (p == CS ? marker : 0u);
+                y ^= tbl_mul(lds, i, j, xv);
+            }
+            obase[j * pitch + K + c] = (uint8_t)y;
         }
+        __syncthreads();  // the edge bytes are in L2 before wave 0 reads row bytes 0..15 back
+    }
+    const uint32_t j = h >> 2, c = FH_WAVE_CHUNKS * U + (h & 3u);  // this lane's chunk: row j, chunk c
+    // chunk 0's first block = ids || row bytes 0..15 (coding vector, 6 head edge columns)
+    u32x4 head = {0, 0, 0, 0};
+    if (U == 0)
+        head = __builtin_amdgcn_raw_buffer_load_b128(
+            __builtin_amdgcn_make_buffer_rsrc(obase, 0, BUF_RECORDS, 0x00020000), j * (uint32_t)pitch, 0, 1);
+    asm volatile("" ::: "memory");  // the loop's memory-counter picture: inputs, then 16 dropped stores
+#pragma unroll
+    for (int jj = 0; jj < (int)N; jj++) strow<DW>(obase, OOB_COL + ooff[jj], Vec<DW>{});
+    uint8_t *wl = lds + LDS_BYTES + (threadIdx.x >> 6) * 64 * STEP;
+    // encode lane's LDS address for rows jj = jm (mod 4) (the swizzle key of slot 4jj + eq depends on
+    // jj mod 4 only); row jj adds 4 jj slots
+    uint32_t wx[4];
+#pragma unroll
+    for (uint32_t jm = 0; jm < 4; jm++) {
+        const uint32_t piece = DW == 4 ? eb : eb >> 1, half = DW == 4 ? 0u : (eb & 1u);
+        wx[jm] = STEP * eq + 16 * (piece ^ fh_key<DW>(4 * jm + eq)) + 8 * half;
+    }
+    const uint32_t rbase = h * STEP + 16 * fh_key<DW>(h);
+    auto sink = [&](int jj, const Vec<DW> &v) { *reinterpret_cast<Vec<DW> *>(wl + wx[jj & 3] + 4 * STEP * jj) = v; };
+    uint32_t cv[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) cv[i] = b3::K3.iv[i];
+    const uint64_t cs_id = first_id + cs, chunk_id = cs_id * N + j;  // chunkset.rs:47
+    uint32_t st = 0;
+#pragma unroll 1
+    do {
+        combine_block<K, N, DW, 0, decltype(sink), FH_STORE_AUX>(x, obase, ooff, col(st), ibase, ioff, col(st + 1), sink);
+        // one wave: its LDS accesses complete in order, no barrier between the slot writes and reads
+#pragma unroll
+        for (uint32_t kb = 0; kb < BPS; kb++) {
+            uint32_t mw[16];
+#pragma unroll
+            for (uint32_t w = 0; w < 4; w++) {
+                const u32x4 v = *reinterpret_cast<const u32x4 *>(wl + (rbase ^ (16 * (4 * kb + w))));
+                mw[4 * w] = v.x, mw[4 * w + 1] = v.y, mw[4 * w + 2] = v.z, mw[4 * w + 3] = v.w;
+            }
+            if (kb == 0 && U == 0 && st == 0) {
+                const bool c0 = c == 0;
+                mw[0] = c0 ? (uint32_t)cs_id : mw[0];
+                mw[1] = c0 ? (uint32_t)(cs_id >> 32) : mw[1];
+                mw[2] = c0 ? (uint32_t)chunk_id : mw[2];
+                mw[3] = c0 ? (uint32_t)(chunk_id >> 32) : mw[3];
+                mw[4] = c0 ? head.x : mw[4];
+                mw[5] = c0 ? head.y : mw[5];
+                mw[6] = c0 ? head.z : mw[6];
+                mw[7] = c0 ? head.w : mw[7];
+            }
+            const uint32_t k = st * BPS + kb;  // block of the chunk
+            b3::compress(cv, mw, c, b3::BLOCK, (k == 0 ? b3::CHUNK_START : 0u) | (k == 15 ? b3::CHUNK_END : 0u), cv);
+        }
+    } while (++st < STEPS);
+    // row j's 4 chunk values (lanes 4j .. 4j+3) -> their subtree: level k pairs lanes q, q ^ 2^k
+#pragma unroll
+    for (uint32_t k = 0; k < 2; k++) {
+        uint32_t sib[8], lo[8], hi[8];
+        const bool right = (h >> k) & 1u;
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            sib[i] = __shfl_xor(cv[i], 1 << k, 4);
+            lo[i] = right ? sib[i] : cv[i];
+            hi[i] = right ? cv[i] : sib[i];
+        }
+        b3::parent(lo, hi, 0, cv);
+    }
+    if ((h & 3u) == 0) {
+        uint32_t *o = sub + (((size_t)cs * N + j) * FH_WAVE_UNITS + U) * 8;
+#pragma unroll
+        for (int i = 0; i < 8; i++) o[i] = cv[i];
     }
 }
 
@@ -904,12 +982,15 @@ static uint32_t row_phase(const uint8_t *rows, size_t pitch) {
 #define DECDS_ENC_WAVES 2
 #endif
 #define ENC_KERNEL(UNIT, ORDER, MSG) rlnc_encode_kernel<UNIT, ORDER, DECDS_ENC_DW, DECDS_ENC_WAVES, MSG>
-// fused ChunkSet::new: 16-column blocks at 2 waves per SIMD (units of 4 tiles), or 8-column blocks
-// at 3 waves per SIMD (units of 8 tiles: one more workgroup per CU streams while another hashes)
-#ifndef DECDS_FUSE_DW
-#define DECDS_FUSE_DW 2  // r02m: 1.05 vs 1.12 ms at cfg2, 2.67 vs 2.84 ms at 256 chunksets
+// fused ChunkSet::new (rlnc_encode_hash_kernel): 8-column blocks (128-byte steps) at 3 waves per SIMD;
+// 16-column blocks (256-byte steps) at 2 waves per SIMD measured 9 % slower (r03d)
+#ifndef DECDS_FH_DW
+#define DECDS_FH_DW 2
 #endif
-#define ENC_COMMIT rlnc_encode_kernel<16384 / (TILE_BLOCKS * 4 * DECDS_FUSE_DW), true, DECDS_FUSE_DW, (DECDS_FUSE_DW == 4 ? 2 : 3), true, true>
+#ifndef DECDS_FH_WAVES
+#define DECDS_FH_WAVES 3
+#endif
+#define ENC_HASH rlnc_encode_hash_kernel<DECDS_FH_DW, DECDS_FH_WAVES>
 // 16-byte-aligned rows (phase MSG_PHASE with 16-column blocks) take the message-tiled kernels
 constexpr bool MSG_OK = DECDS_ENC_DW == 4;
 #ifndef DECDS_ENC_QUEUE
@@ -921,10 +1002,10 @@ hipError_t configure_kernels() {
     const void *fns[] = {reinterpret_cast<const void *>(ENC_KERNEL(ENC_UNIT, DECDS_ENC_ORDER != 0, false)),
                          reinterpret_cast<const void *>(ENC_KERNEL(ENC_UNIT, DECDS_ENC_ORDER != 0, MSG_OK)),
                          reinterpret_cast<const void *>(ENC_SWEEP(false)), reinterpret_cast<const void *>(ENC_SWEEP(MSG_OK)),
-                         reinterpret_cast<const void *>(ENC_COMMIT),
+                         reinterpret_cast<const void *>(ENC_HASH),
                          reinterpret_cast<const void *>(rlnc_decode_kernel<DEC_UNIT>)};
     for (const void *f : fns) {
-        hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, SWEEP_LDS);
+        hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, std::max(SWEEP_LDS, FH_LDS<DECDS_FH_DW>));
         if (e != hipSuccess) return e;
     }
     return hipSuccess;
@@ -962,9 +1043,7 @@ hipError_t launch_encode(const LaunchGeom &geom, const uint8_t *src, size_t n, c
     }
     const void *fn = msg ? reinterpret_cast<const void *>(ENC_KERNEL(ENC_UNIT, DECDS_ENC_ORDER != 0, MSG_OK))
                          : reinterpret_cast<const void *>(ENC_KERNEL(ENC_UNIT, DECDS_ENC_ORDER != 0, false));
-    uint64_t first = 0;
-    uint32_t *sub = nullptr;
-    void *args[] = {&src, &n, &coeffs, &dst, &pitch, const_cast<uint32_t *>(&phase), &poly, &marker, &first, &sub};
+    void *args[] = {&src, &n, &coeffs, &dst, &pitch, const_cast<uint32_t *>(&phase), &poly, &marker};
     return hipLaunchKernel(fn, dim3((uint32_t)(n * (T / ENC_UNIT))), dim3(WG), args, LDS_BYTES, stream);
 }
 
@@ -973,12 +1052,14 @@ const char *encode_kernel_name(size_t n) { return n <= ENC_SWEEP_MAX_N ? "rlnc_e
 bool encode_commit_fusable(const uint8_t *dst, size_t pitch) { return row_phase<4>(dst, pitch) == MSG_PHASE; }
 static_assert(MSG_PHASE < COLS<2>, "16-byte-aligned rows have the message phase for both block widths");
 
+uint32_t encode_commit_subtrees() { return FH_WAVE_UNITS; }
+
 hipError_t launch_encode_commit(const uint8_t *src, size_t n, const uint8_t *coeffs, uint8_t *dst, size_t pitch,
                                 uint32_t poly, uint32_t marker, uint64_t first_id, uint32_t *sub, hipStream_t stream) {
     if (n == 0) return hipSuccess;
     if (!encode_commit_fusable(dst, pitch)) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((ENC_COMMIT), dim3((uint32_t)(n * FUSED_UNITS)), dim3(WG), LDS_BYTES, stream, src, n, coeffs,
-                       dst, pitch, MSG_PHASE, poly, marker, first_id, sub);
+    hipLaunchKernelGGL((ENC_HASH), dim3((uint32_t)(n * FH_WG_UNITS)), dim3(WG), FH_LDS<DECDS_FH_DW>, stream, src, n,
+                       coeffs, dst, pitch, poly, marker, first_id, sub);
     return hipGetLastError();
 }
 

@@ -65,12 +65,12 @@ def _aligned_rows(n, row_offset):
     return buf[off:off + (n * N - 1) * P + F], P
 
 
-@pytest.mark.parametrize("row_offset", [16, 48, 0, 118])
-def test_encode_commit_fused_matches_oracle(ctx, row_offset):
+@pytest.mark.parametrize("row_offset,first", [(16, 1000), (48, 1000), (0, (1 << 33) + 5), (118, 1000)])
+def test_encode_commit_fused_matches_oracle(ctx, row_offset, first):
     # ChunkSet::new (chunkset.rs:37-63) in one call: rows at 16 mod 16 take the fused kernel (chunk
-    # hashing behind the encode stores + commit_fold_kernel), 118 the unfused fallback; both must give
-    # the oracle's coded rows, digests, roots and proofs
-    n, first = 3, 1000
+    # hashing from LDS right behind the encode + commit_fold_kernel), 118 the unfused fallback; both
+    # must give the oracle's coded rows, digests, roots and proofs (ids above 2^32: both id words)
+    n = 3
     data = o.fill_random(0xC011B + row_offset, n * CS)
     coeffs = o.fill_random(0xC011C + row_offset, n * N * K)
     coded, pitch = _aligned_rows(n, row_offset)

@@ -48,7 +48,7 @@ def main():
     dig = torch.empty(n * N * 32, dtype=torch.uint8, device="cuda")
     roots = torch.empty(n * 32, dtype=torch.uint8, device="cuda")
     proofs = torch.empty(n * N * 128, dtype=torch.uint8, device="cuda")
-    ws = torch.empty(builds[0]["lib"].decds_encode_commit_workspace_bytes(n), dtype=torch.uint8, device="cuda")
+    ws = torch.empty(max(b["lib"].decds_encode_commit_workspace_bytes(n) for b in builds), dtype=torch.uint8, device="cuda")
     ptrs = [vp(t.data_ptr()) for t in (src, cv, coded, dig, roots, proofs, ws)]
 
     def fused(b):

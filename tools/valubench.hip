@@ -50,6 +50,23 @@ constexpr int ITERS = 8192;
                    "+v"(r[6]), "+v"(r[7])                                                       \
                  : "v"(k));
 #define OP8_E64(INS) OP8(INS)
+#define OP8_B3                                                                                 \
+    asm volatile("v_bitop3_b32 %0, %0, %8, %1 bitop3:0x96\n\tv_bitop3_b32 %1, %1, %8, %2 bitop3:0x96\n\t" \
+                 "v_bitop3_b32 %2, %2, %8, %3 bitop3:0x96\n\tv_bitop3_b32 %3, %3, %8, %4 bitop3:0x96\n\t" \
+                 "v_bitop3_b32 %4, %4, %8, %5 bitop3:0x96\n\tv_bitop3_b32 %5, %5, %8, %6 bitop3:0x96\n\t" \
+                 "v_bitop3_b32 %6, %6, %8, %7 bitop3:0x96\n\tv_bitop3_b32 %7, %7, %8, %0 bitop3:0x96"    \
+                 : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]), "+v"(r[4]), "+v"(r[5]),      \
+                   "+v"(r[6]), "+v"(r[7])                                                       \
+                 : "v"(k));
+#define SDWB " dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_1 src1_sel:DWORD"
+#define OP8_SDWB                                                                               \
+    asm volatile("v_and_b32_sdwa %0, %0, %8" SDWB "\n\tv_and_b32_sdwa %1, %1, %8" SDWB                \
+                 "\n\tv_and_b32_sdwa %2, %2, %8" SDWB "\n\tv_and_b32_sdwa %3, %3, %8" SDWB              \
+                 "\n\tv_and_b32_sdwa %4, %4, %8" SDWB "\n\tv_and_b32_sdwa %5, %5, %8" SDWB              \
+                 "\n\tv_and_b32_sdwa %6, %6, %8" SDWB "\n\tv_and_b32_sdwa %7, %7, %8" SDWB              \
+                 : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]), "+v"(r[4]), "+v"(r[5]),      \
+                   "+v"(r[6]), "+v"(r[7])                                                       \
+                 : "v"(k));
 #define SDW " dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_0 src1_sel:WORD_0"
 #define OP8_SDWA                                                                               \
     asm volatile("v_xor_b32_sdwa %0, %0, %8" SDW "\n\tv_xor_b32_sdwa %1, %1, %8" SDW                \
@@ -80,6 +97,9 @@ __global__ __launch_bounds__(256) void valu_kernel(uint32_t *out, uint64_t *tick
         if constexpr (OP == 10) OP8("v_lshlrev_b32")
         if constexpr (OP == 11) OP8_V3("v_lshl_or_b32")
         if constexpr (OP == 12) OP8_E64("v_xor_b32_e64")
+        if constexpr (OP == 13) OP8_B3
+        if constexpr (OP == 14) OP8_SDWB
+        if constexpr (OP == 15) OP8("v_pk_add_u16")
     }
     const uint64_t t1 = __builtin_amdgcn_s_memtime();
     uint32_t x = 0;
@@ -93,14 +113,15 @@ int main() {
     CK(hipGetDeviceProperties(&prop, 0));
     const int cus = prop.multiProcessorCount;
     const char *names[] = {"v_xor_b32", "v_add_u32", "v_add3_u32", "v_alignbit_b32", "v_perm_b32", "v_add_f32",
-                           "v_xad_u32", "v_xor_b32_sdwa", "v_add_u32+literal", "v_fma_f32", "v_lshlrev_b32", "v_lshl_or_b32", "v_xor_b32_e64"};
+                           "v_xad_u32", "v_xor_b32_sdwa", "v_add_u32+literal", "v_fma_f32", "v_lshlrev_b32", "v_lshl_or_b32", "v_xor_b32_e64",
+                           "v_bitop3_b32", "v_and_b32_sdwa(byte)", "v_pk_add_u16"};
     for (int wps : {8}) {   // waves per SIMD
         const int blocks = cus * wps; // 4 waves per block = one per SIMD
         uint32_t *out;
         uint64_t *ticks;
         CK(hipMalloc(&out, blocks * 256 * 4));
         CK(hipMalloc(&ticks, blocks * 4 * 8));
-        for (int op = 0; op < 13; op++) {
+        for (int op = 0; op < 16; op++) {
             auto launch = [&] {
                 switch (op) {
                     case 0: valu_kernel<0><<<blocks, 256>>>(out, ticks); break;
@@ -116,6 +137,9 @@ int main() {
                     case 10: valu_kernel<10><<<blocks, 256>>>(out, ticks); break;
                     case 11: valu_kernel<11><<<blocks, 256>>>(out, ticks); break;
                     case 12: valu_kernel<12><<<blocks, 256>>>(out, ticks); break;
+                    case 13: valu_kernel<13><<<blocks, 256>>>(out, ticks); break;
+                    case 14: valu_kernel<14><<<blocks, 256>>>(out, ticks); break;
+                    case 15: valu_kernel<15><<<blocks, 256>>>(out, ticks); break;
                 }
             };
             launch();
