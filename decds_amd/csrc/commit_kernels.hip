@@ -20,125 +20,96 @@ constexpr uint32_t FULL_CHUNKS = MSG_BYTES / b3::CHUNK;            // 1024
 constexpr uint32_t LAST_BYTES = MSG_BYTES - FULL_CHUNKS * b3::CHUNK;  // 27
 static_assert(FULL_CHUNKS == 1024 && LAST_BYTES == 27, "BLAKE3 tree shape of a coded chunk message");
 
-#ifndef DECDS_DG_PREFETCH
-#define DECDS_DG_PREFETCH 1  // 1: block b+1's loads issued before block b's compression
-#endif
-constexpr uint32_t CPT = 4;                       // consecutive BLAKE3 chunks per thread
-constexpr uint32_t DG_WG = FULL_CHUNKS / CPT;     // 256 threads per row
+constexpr uint32_t DG_WG = FULL_CHUNKS / 4;  // 256 threads per row, 4 consecutive chunks each
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-struct Block {
-    uint32_t w[16];
-};
-
-// One 64-byte message block (block b of full chunk c of a row). Message bytes 0..15 are the two
-// little-endian u64 ids, so piece offset = message offset - 16 (≡ 0 mod 16): every block starts at
-// the row's own misalignment s = piece mod 16. Byte-misaligned dwordx4 loads in this lane-per-chunk
-// order run at a third of the aligned rate (tools/hashmem.hip: 2.3 vs 5.5 TB/s), so each block is
-// read as 16-byte-ALIGNED words — four, plus a fifth when s != 0 — and funnel-shifted into place:
-// dword shift Q = s / 4 is a template parameter (the row picks the instantiation once, a
-// wave-uniform branch), byte shift r = s % 4 one v_alignbyte per message word. Q = -1: s == 0.
-// The fifth word of the last block of a row with s in 1..4 reaches up to 4 bytes past the row —
-// inside the same 16-byte granule as the row's last byte, so never a separate page.
-template <int Q>
-__device__ __forceinline__ Block load_block(const uint8_t *piece, const uint8_t *abase, uint32_t r, uint32_t c,
-                                            uint32_t b, uint64_t cs_id, uint64_t chunk_id) {
-    Block m;
-    const int64_t off = (int64_t)c * b3::CHUNK + b * b3::BLOCK - 16;
-    if (off >= 0) {
-        const uint4 *pa = reinterpret_cast<const uint4 *>(abase + off);
-        uint32_t w[20];
-#pragma unroll
-        for (int k = 0; k < (Q < 0 ? 4 : 5); k++) {
-            const uint4 v = pa[k];
-            w[4 * k] = v.x, w[4 * k + 1] = v.y, w[4 * k + 2] = v.z, w[4 * k + 3] = v.w;
-        }
-#pragma unroll
-        for (int i = 0; i < 16; i++) {
-            if constexpr (Q < 0)
-                m.w[i] = w[i];
-            else
-                m.w[i] = __builtin_amdgcn_alignbyte(w[i + Q + 1], w[i + Q], r);
-        }
-    } else {
-        // block 0 of chunk 0: ids, then piece bytes 0..47. The address is wave-uniform here: spelled
-        // byte-wise so it cannot become a scalar (s_load) access, which drops misalignment
-        m.w[0] = (uint32_t)cs_id, m.w[1] = (uint32_t)(cs_id >> 32);
-        m.w[2] = (uint32_t)chunk_id, m.w[3] = (uint32_t)(chunk_id >> 32);
-#pragma unroll
-        for (int i = 4; i < 16; i++) {
-            const uint8_t *p = piece + 4 * (i - 4);
-            m.w[i] = p[0] | (uint32_t)p[1] << 8 | (uint32_t)p[2] << 16 | (uint32_t)p[3] << 24;
-        }
-    }
-    return m;
-}
-
-// chaining value of full chunk c of a row (16 blocks)
-template <int Q>
-__device__ __forceinline__ void chunk_cv(const uint8_t *piece, const uint8_t *abase, uint32_t r, uint32_t c,
-                                         uint64_t cs_id, uint64_t chunk_id, uint32_t cv[8]) {
-#pragma unroll
-    for (int i = 0; i < 8; i++) cv[i] = b3::K3.iv[i];
-#if DECDS_DG_PREFETCH
-    Block m = load_block<Q>(piece, abase, r, c, 0, cs_id, chunk_id);
-#pragma unroll 1
-    for (uint32_t b = 0; b < 16; b++) {
-        const Block nxt = load_block<Q>(piece, abase, r, c, b < 15 ? b + 1 : b, cs_id, chunk_id);
-        const uint32_t flags = (b == 0 ? b3::CHUNK_START : 0u) | (b == 15 ? b3::CHUNK_END : 0u);
-        b3::compress(cv, m.w, c, b3::BLOCK, flags, cv);
-        m = nxt;
-    }
-#else
-#pragma unroll 1
-    for (uint32_t b = 0; b < 16; b++) {
-        const Block m = load_block<Q>(piece, abase, r, c, b, cs_id, chunk_id);
-        const uint32_t flags = (b == 0 ? b3::CHUNK_START : 0u) | (b == 15 ? b3::CHUNK_END : 0u);
-        b3::compress(cv, m.w, c, b3::BLOCK, flags, cv);
-    }
-#endif
-}
-
-// thread t: chunks 4t..4t+3 folded into the chaining value of their 4-chunk subtree (all lanes busy)
-template <int Q>
-__device__ __forceinline__ void subtree4_cv(const uint8_t *piece, uint32_t t, uint64_t cs_id, uint64_t chunk_id,
-                                            uint32_t acc[8]) {
-    const uint32_t s = (uint32_t)(reinterpret_cast<uintptr_t>(piece) & 15);
-    const uint8_t *abase = piece - s;
-    const uint32_t r = s & 3;
-    uint32_t a[8], b[8], lo[8], hi[8];
-    chunk_cv<Q>(piece, abase, r, 4 * t, cs_id, chunk_id, a);
-    chunk_cv<Q>(piece, abase, r, 4 * t + 1, cs_id, chunk_id, b);
-    b3::parent(a, b, 0, lo);
-    chunk_cv<Q>(piece, abase, r, 4 * t + 2, cs_id, chunk_id, a);
-    chunk_cv<Q>(piece, abase, r, 4 * t + 3, cs_id, chunk_id, b);
-    b3::parent(a, b, 0, hi);
-    b3::parent(lo, hi, 0, acc);
-}
-
-// Digest of one coded row per 256-thread workgroup: 4-chunk subtrees in registers, the 256
-// subtree values folded in LDS (8 PARENT levels), then thread 0 adds the 27-byte 1025th chunk under
-// the ROOT parent.
+// Digest of one coded row per 256-thread workgroup: thread t hashes chunks 4t .. 4t+3 one after the
+// other and folds them into their 4-chunk subtree in registers; the 256 subtree values fold in LDS
+// (8 PARENT levels), then thread 0 adds the 27-byte 1025th chunk under the ROOT parent.
 // ids == NULL: row = c*16 + j of a freshly encoded batch, chunkset_id = first + c and chunk_id =
 // chunkset_id*16 + j (chunkset.rs:47); else the row's claimed (chunkset_id, chunk_id) = ids[2row..].
+// Message blocks are staged through LDS (DG_LDS): a wave walks its 64 lanes' chunks in 32 steps of
+// 128 message bytes (4 chunks x 8 steps per lane); per step it loads the 64 segments cooperatively —
+// 8 lanes per 128-byte segment, 8 segments per load instruction, unaligned 16-byte buffer loads —
+// writes them to one 128-byte LDS slot per lane and each lane reads its own two blocks back (slots
+// XOR-swizzled: every ds_read_b128 group hits 16 distinct bank quads). The next step's loads are in
+// flight across this step's compressions. (The lane-per-chunk form loaded 5 aligned words per block
+// and funnel-shifted them: 64 distinct lines per load instruction, 0.68-0.75 ms at cfg2.)
+constexpr uint32_t DG_STEP = 128;                       // message bytes per chunk per step
+constexpr uint32_t DG_STEPS = 4 * b3::CHUNK / DG_STEP;  // 32: 4 chunks per lane
+__device__ __forceinline__ uint32_t dg_slot(uint32_t t, uint32_t piece) {
+    return t * DG_STEP + 16 * (piece ^ ((t >> 1) & 7u));
+}
+
 __global__ __launch_bounds__(DG_WG) void chunk_digest_kernel(const uint8_t *__restrict__ coded, size_t pitch,
                                                              uint64_t first_chunkset_id,
                                                              const uint64_t *__restrict__ ids,
                                                              uint8_t *__restrict__ digests) {
-    __shared__ uint32_t cvs[DG_WG][8];
+    __shared__ __attribute__((aligned(16))) uint8_t slots[DG_WG * DG_STEP];  // 32 KiB; the fold reuses it
     const uint32_t row = blockIdx.x;
     const uint64_t cs_id = ids ? ids[2 * (size_t)row] : first_chunkset_id + row / N;
     const uint64_t chunk_id = ids ? ids[2 * (size_t)row + 1] : cs_id * N + row % N;
     const uint8_t *piece = coded + (size_t)row * pitch;
-    const uint32_t t = threadIdx.x;
-    uint32_t acc[8];
-    switch ((uint32_t)(reinterpret_cast<uintptr_t>(piece) & 15) >> 2 |
-            ((reinterpret_cast<uintptr_t>(piece) & 15) == 0 ? 4u : 0u)) {
-        case 0: subtree4_cv<0>(piece, t, cs_id, chunk_id, acc); break;
-        case 1: subtree4_cv<1>(piece, t, cs_id, chunk_id, acc); break;
-        case 2: subtree4_cv<2>(piece, t, cs_id, chunk_id, acc); break;
-        case 3: subtree4_cv<3>(piece, t, cs_id, chunk_id, acc); break;
-        default: subtree4_cv<-1>(piece, t, cs_id, chunk_id, acc); break;
+    const uint32_t t = threadIdx.x, l = t & 63u, wb = t & ~63u;
+    // load k of this lane: segment of thread lt = wb + 8k + l/8, its 16-byte piece l % 8; message byte m
+    // is piece byte m - 16 (block 0 of chunk 0 reads offset -16: out of range, zeros, ids patched in)
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(piece), 0, (int)F, 0x00020000);
+    const uint32_t lt0 = wb + (l >> 3), lp = l & 7u;
+    auto load_step = [&](u32x4 (&v)[8], uint32_t g) {  // step g: chunk 4 lt + g / 8, bytes 128 (g % 8) ..
+#pragma unroll
+        for (uint32_t k = 0; k < 8; k++) {
+            const uint32_t lt = lt0 + 8 * k;
+            const uint32_t off = (4 * lt + (g >> 3)) * b3::CHUNK + (g & 7u) * DG_STEP + 16 * lp - 16;
+            v[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
+        }
+    };
+    u32x4 pf[8];
+    load_step(pf, 0);
+    uint32_t cv[8], first[8], lo[8], acc[8];
+#pragma unroll 1
+    for (uint32_t g = 0; g < DG_STEPS; g++) {
+#pragma unroll
+        for (uint32_t k = 0; k < 8; k++) *reinterpret_cast<u32x4 *>(slots + dg_slot(lt0 + 8 * k, lp)) = pf[k];
+        if (g + 1 < DG_STEPS) load_step(pf, g + 1);  // in flight across this step's compressions
+        const uint32_t st = g & 7u, a = g >> 3, c = 4 * t + a;
+        if (st == 0)
+#pragma unroll
+            for (int i = 0; i < 8; i++) cv[i] = b3::K3.iv[i];
+        // one wave: its LDS accesses complete in order, no barrier between the slot writes and reads
+#pragma unroll
+        for (uint32_t kb = 0; kb < 2; kb++) {
+            uint32_t mw[16];
+#pragma unroll
+            for (uint32_t w = 0; w < 4; w++) {
+                const u32x4 v = *reinterpret_cast<const u32x4 *>(slots + dg_slot(t, 4 * kb + w));
+                mw[4 * w] = v.x, mw[4 * w + 1] = v.y, mw[4 * w + 2] = v.z, mw[4 * w + 3] = v.w;
+            }
+            if (kb == 0 && g == 0) {  // chunk 0's block 0 starts with the two ids (chunk.rs:40-46)
+                const bool c0 = t == 0;
+                mw[0] = c0 ? (uint32_t)cs_id : mw[0];
+                mw[1] = c0 ? (uint32_t)(cs_id >> 32) : mw[1];
+                mw[2] = c0 ? (uint32_t)chunk_id : mw[2];
+                mw[3] = c0 ? (uint32_t)(chunk_id >> 32) : mw[3];
+            }
+            const uint32_t k = 2 * st + kb;
+            b3::compress(cv, mw, c, b3::BLOCK, (k == 0 ? b3::CHUNK_START : 0u) | (k == 15 ? b3::CHUNK_END : 0u), cv);
+        }
+        if (st == 7) {  // chunk 4t + a done: fold into the 4-chunk subtree
+            if (a == 0 || a == 2) {
+#pragma unroll
+                for (int i = 0; i < 8; i++) first[i] = cv[i];
+            } else if (a == 1) {
+                b3::parent(first, cv, 0, lo);
+            } else {
+                uint32_t hi[8];
+                b3::parent(first, cv, 0, hi);
+                b3::parent(lo, hi, 0, acc);
+            }
+        }
     }
+    __syncthreads();  // every wave is done with its slots
+    uint32_t(*cvs)[8] = reinterpret_cast<uint32_t(*)[8]>(slots);
 #pragma unroll
     for (int i = 0; i < 8; i++) cvs[t][i] = acc[i];
     __syncthreads();
@@ -175,48 +146,62 @@ __global__ __launch_bounds__(DG_WG) void chunk_digest_kernel(const uint8_t *__re
 }
 
 // Digest of each coded row from the fused encode's 256 aligned 4-chunk subtree values
-// (rlnc_encode_hash_kernel). One wave per row: lane i folds subtrees 4i .. 4i+3 into the 16-chunk
-// subtree i, six PARENT levels fold those into the 1024-chunk left tree, then the 27-byte 1025th
-// chunk joins under ROOT, as chunk_digest_kernel.
+// (rlnc_encode_hash_kernel). One wave per row: lane i folds subtrees 4i .. 4i+3 (two independent
+// parents, then theirs) into the 16-chunk subtree i, six PARENT levels fold those into the 1024-chunk
+// left tree, then the 27-byte 1025th chunk joins under ROOT, as chunk_digest_kernel. Latency-bound
+// (one wave, a chain of compressions), so the 1025th chunk rides along in cross-lane level 0: lane 63
+// compresses it instead of the (62, 63) parent that lane 62 computes as well, and every later level
+// reads a sibling group's value from its lowest lane, which lane 63 never is.
 constexpr uint32_t FOLD_LANES = 64, SUB_PER_ROW = FULL_CHUNKS / 4;  // 256
 __global__ __launch_bounds__(FOLD_LANES) void commit_fold_kernel(const uint8_t *__restrict__ coded, size_t pitch,
                                                                  const uint32_t *__restrict__ sub,
                                                                  uint8_t *__restrict__ digests) {
     const size_t row = blockIdx.x;
     const uint32_t i = threadIdx.x;
-    const uint32_t *p = sub + (row * SUB_PER_ROW + 4 * i) * 8;
-    uint32_t a[8], b[8], lo[8], hi[8], cv[8];
+    const uint8_t *piece = coded + row * pitch;
+    const bool tail = i == FOLD_LANES - 1;
+    uint32_t tw[16];  // lane 63: the last chunk's 27 message bytes (the piece's final 27 bytes)
 #pragma unroll
-    for (int w = 0; w < 8; w++) a[w] = p[w], b[w] = p[8 + w];
-    b3::parent(a, b, 0, lo);
-#pragma unroll
-    for (int w = 0; w < 8; w++) a[w] = p[16 + w], b[w] = p[24 + w];
-    b3::parent(a, b, 0, hi);
-    b3::parent(lo, hi, 0, cv);
-#pragma unroll
-    for (uint32_t k = 0; k < 6; k++) {
-        uint32_t sib[8];
-        const bool right = (i >> k) & 1u;
-#pragma unroll
-        for (int w = 0; w < 8; w++) {
-            sib[w] = __shfl_xor(cv[w], 1 << k, FOLD_LANES);
-            lo[w] = right ? sib[w] : cv[w];
-            hi[w] = right ? cv[w] : sib[w];
-        }
-        b3::parent(lo, hi, 0, cv);
-    }
-    if (i == 0) {
-        const uint8_t *piece = coded + row * pitch;
-        uint32_t m[16], last[8], root[8];
-#pragma unroll
-        for (int w = 0; w < 16; w++) {
-            uint32_t x = 0;
+    for (int w = 0; w < 16; w++) {
+        uint32_t x = 0;
+        if (tail)
 #pragma unroll
             for (int k = 0; k < 4; k++)
                 if (4 * w + k < (int)LAST_BYTES) x |= (uint32_t)piece[FULL_CHUNKS * b3::CHUNK - 16 + 4 * w + k] << (8 * k);
-            m[w] = x;
+        tw[w] = x;
+    }
+    const uint32_t *p = sub + (row * SUB_PER_ROW + 4 * i) * 8;
+    uint32_t m[16], lo[8], hi[8], cv[8], last[8];
+#pragma unroll
+    for (int w = 0; w < 16; w++) m[w] = p[w];
+    b3::parent(m, m + 8, 0, lo);
+#pragma unroll
+    for (int w = 0; w < 16; w++) m[w] = p[16 + w];
+    b3::parent(m, m + 8, 0, hi);
+    b3::parent(lo, hi, 0, cv);
+#pragma unroll
+    for (uint32_t k = 0; k < 6; k++) {
+        const uint32_t sl = (i ^ (1u << k)) & ~((1u << k) - 1);  // the sibling group's lowest lane
+        const bool right = (i >> k) & 1u;
+#pragma unroll
+        for (int w = 0; w < 8; w++) {
+            const uint32_t sib = __shfl(cv[w], sl, FOLD_LANES);
+            m[w] = right ? sib : cv[w];
+            m[w + 8] = right ? cv[w] : sib;
         }
-        b3::compress(b3::K3.iv, m, FULL_CHUNKS, LAST_BYTES, b3::CHUNK_START | b3::CHUNK_END, last);
+        if (k == 0) {
+#pragma unroll
+            for (int w = 0; w < 16; w++) m[w] = tail ? tw[w] : m[w];
+            b3::compress(b3::K3.iv, m, tail ? FULL_CHUNKS : 0u, tail ? LAST_BYTES : b3::BLOCK,
+                         tail ? (b3::CHUNK_START | b3::CHUNK_END) : b3::PARENT, cv);
+#pragma unroll
+            for (int w = 0; w < 8; w++) last[w] = __shfl(cv[w], FOLD_LANES - 1, FOLD_LANES);
+        } else {
+            b3::parent(m, m + 8, 0, cv);
+        }
+    }
+    if (i == 0) {
+        uint32_t root[8];
         b3::parent(cv, last, b3::ROOT, root);
         uint32_t *d = reinterpret_cast<uint32_t *>(digests + row * 32);
 #pragma unroll
