@@ -1,6 +1,6 @@
 """BASELINE config 3/4 at full size on one GPU: a 16 GiB blob (1639 chunksets, the last one holding
 4 MiB of data) encoded in one batch, repaired from exactly 10 random survivors per chunkset, and
-committed + validated (rows f1, f2). Spot chunksets / rows are bit-exact against the oracle; every
+committed (separately and fused into the encode) + validated (rows f1, f2). Spot chunksets / rows are bit-exact against the oracle; every
 other check is a size-independent property (decode∘encode = id, rank-deficient sets reported
 not-ready exactly where the oracle's rank test says so, every row's proof verifies, a flipped byte
 does not)."""
@@ -57,7 +57,7 @@ def test_cfg3_16gib_encode_repair_commit_validate(ctx):
     assert 0 < int((st == 5).sum()) < 30     # ~0.39 % of 1639 are rank-deficient
     for c in np.nonzero(st == 0)[0].tolist():
         assert torch.equal(out[c * CS:(c + 1) * CS], src[c * CS:(c + 1) * CS]), c
-    del out, src
+    del out
 
     # commitment of every coded row, then the blob-level tree and validation of all 26,224 rows
     dig = torch.empty(n * N * 32, dtype=torch.uint8, device="cuda")
@@ -65,6 +65,19 @@ def test_cfg3_16gib_encode_repair_commit_validate(ctx):
     proofs = torch.empty(n * N * 128, dtype=torch.uint8, device="cuda")
     codec.commit_batch(ctx, coded, n, dig, roots, proofs)
     torch.cuda.synchronize()
+    # the fused ChunkSet::new at full size (rows 16 bytes past a 128-byte boundary): the same coded
+    # bytes, digests, roots and proofs as encode + commit
+    from decds_amd._capi import CODED_PITCH_ALIGNED as P
+    mbuf = torch.empty(n * N * P + 256, dtype=torch.uint8, device="cuda")
+    off = (16 - mbuf.data_ptr()) % 128
+    mcoded = mbuf[off:off + (n * N - 1) * P + F]
+    fo = [torch.empty_like(t) for t in (dig, roots, proofs)]
+    codec.encode_commit_batch(ctx, src, n, torch.from_numpy(coeffs).cuda(), mcoded, *fo, pitch=P)
+    torch.cuda.synchronize()
+    for a, b in zip(fo, (dig, roots, proofs)):
+        assert torch.equal(a, b)
+    assert torch.equal(mcoded.as_strided((n * N, F), (P, 1)), coded.view(n * N, F))
+    del mbuf, mcoded, fo, src
     d = dig.cpu().numpy()
     for row in (0, 1, 13107, n * N - 1):
         piece = coded[row * F:(row + 1) * F].cpu().numpy()
