@@ -290,7 +290,8 @@ def main():
     enc_gbs = enc_bytes / (enc_ms * 1e-3) / 1e9
     dec_gbs = dec_bytes / (dec_ms * 1e-3) / 1e9
     enc_kernel = _lib().decds_encode_kernel_name(n).decode()
-    dominant = enc_kernel if enc_ms >= dec_ms else "rlnc_decode_kernel"
+    dec_kernel = _lib().decds_decode_kernel_name(n).decode()
+    dominant = enc_kernel if enc_ms >= dec_ms else dec_kernel
     achieved = enc_gbs if dominant == enc_kernel else dec_gbs
     traffic = None
     try:
@@ -327,7 +328,7 @@ def main():
             "roofline": {"bound": "hbm", "kernel": dominant, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "copy_ceiling": HBM_COPY_GBS, "frac_of_copy": round(achieved / HBM_COPY_GBS, 4),
-                         "decode": {"kernel": "rlnc_decode_kernel", "achieved": round(dec_gbs, 1),
+                         "decode": {"kernel": dec_kernel, "achieved": round(dec_gbs, 1),
                                     "frac": round(dec_gbs / HBM_PEAK_GBS, 4),
                                     "bytes_per_launch": dec_bytes, "ms": round(dec_ms, 4)},
                          "encode": {"kernel": enc_kernel, "achieved": round(enc_gbs, 1),

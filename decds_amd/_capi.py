@@ -143,6 +143,7 @@ def _declare(L):
         "decds_repairing_blob_free": (None, [P]),
         "decds_encode_commit_workspace_bytes": (SZ, [SZ]),
         "decds_encode_kernel_name": (c.c_char_p, [SZ]),
+        "decds_decode_kernel_name": (c.c_char_p, [SZ]),
         "decds_encode_commit_batch": (c.c_int, [P, VP, SZ, VP, VP, SZ, c.c_uint64, VP, VP, VP, VP, VP]),
     }
     for name, (res, args) in sig.items():
@@ -173,6 +174,7 @@ EXPORTED = [
     "decds_repairing_blob_is_chunkset_ready_to_repair", "decds_repairing_blob_is_chunkset_already_repaired",
     "decds_repairing_blob_get_repaired_chunkset", "decds_repairing_blob_free",
     "decds_encode_commit_workspace_bytes", "decds_encode_commit_batch", "decds_encode_kernel_name",
+    "decds_decode_kernel_name",
 ]
 
 

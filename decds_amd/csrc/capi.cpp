@@ -192,6 +192,7 @@ int decds_encode_batch(decds_ctx *ctx, const uint8_t *src, size_t n, const uint8
 }
 
 const char *decds_encode_kernel_name(size_t n_chunksets) { return encode_kernel_name(n_chunksets); }
+const char *decds_decode_kernel_name(size_t n_chunksets) { return decode_kernel_name(n_chunksets); }
 
 int decds_repair_plan_batch(decds_ctx *ctx, const uint8_t *coded, size_t coded_pitch, size_t n,
                             const uint8_t *cand, uint8_t *plan, int8_t *verdicts, int32_t *status,

@@ -40,6 +40,7 @@ hipError_t launch_decode(const LaunchGeom &g, const uint8_t *coded, size_t pitch
 hipError_t launch_fill_random(uint64_t seed, uint64_t byte_offset, uint8_t *dst, size_t nbytes,
                               hipStream_t stream);
 const char *encode_kernel_name(size_t n);  // the kernel launch_encode runs for n chunksets
+const char *decode_kernel_name(size_t n);  // ... launch_decode
 hipError_t configure_kernels();  // raise the dynamic-LDS limit once per process
 
 }  // namespace decds

@@ -120,6 +120,10 @@ int decds_decode_batch(decds_ctx *ctx, const uint8_t *coded, size_t coded_pitch,
                        size_t n_chunksets, const uint8_t *plan, uint8_t *dst, int32_t *status,
                        void *stream);
 
+/* name of the gfx950 kernel decds_decode_batch launches for n chunksets (for profiles and traces:
+ * rlnc_decode_lines_kernel, whose piece stores fill whole 128-byte lines) */
+const char *decds_decode_kernel_name(size_t n_chunksets);
+
 /* plan + decode in one call (the RepairingBlob::add_chunk loop + get_repaired_chunkset,
  * blob.rs:373-394, 451-473, for candidates already resident on the device) */
 int decds_repair_batch(decds_ctx *ctx, const uint8_t *coded, size_t coded_pitch,

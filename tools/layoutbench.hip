@@ -141,6 +141,35 @@ __global__ __launch_bounds__(256) void dec_k(const uint8_t *__restrict__ in, uin
     if (acc.x == 0x9E3779B9u && threadIdx.x == 999) lds[0] = 1;
 }
 
+// decode pattern with line-aligned wave stores (the store side of a DPP-realigned decode): each wave
+// computes 57 consecutive lane blocks — lane 0 the block before its run, lanes 57..63 idle — and each
+// of lanes 1..56 stores one 16-byte granule per output piece: 7 whole 128-byte lines per wave and piece
+// (pieces 1 MiB apart). ALIGN false: the same runs at the real piece offsets i*L (byte-misaligned).
+template <bool ALIGN>
+__global__ __launch_bounds__(256) void dec_lines_k(const uint8_t *__restrict__ in, uint8_t *__restrict__ out, size_t n) {
+    extern __shared__ uint8_t lds[];
+    constexpr uint32_t PER_WAVE = 56, PER_TILE = 4 * PER_WAVE, T2 = (BLOCKS + PER_TILE - 1) / PER_TILE;
+    const uint32_t cs = blockIdx.x / T2, t = blockIdx.x % T2;
+    if (cs >= n) return;
+    constexpr uint32_t sel[10] = {0, 2, 3, 5, 6, 8, 9, 11, 13, 15};
+    const auto ri = rsrc(in + cs * 16 * PITCH);
+    const auto ro = rsrc(out + cs * CSB);
+    const uint32_t w = threadIdx.x >> 6, l = threadIdx.x & 63u;
+    const uint32_t g = t * PER_TILE + w * PER_WAVE + l - 1;  // wraps for the chunkset's first lane 0
+    const bool in_run = l <= PER_WAVE && g < BLOCKS;
+    const uint32_t col = in_run ? g * 16 : 0x80000000u;
+    u32x4 x[10], acc = {0, 0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < 10; k++) x[k] = __builtin_amdgcn_raw_buffer_load_b128(ri, 128 + col + sel[k] * (uint32_t)PITCH, 0, 0);
+#pragma unroll
+    for (int k = 0; k < 10; k++) acc ^= x[k];
+    const uint32_t ocol = (l >= 1 && in_run) ? g * 16 : 0x80000000u;
+#pragma unroll
+    for (int i = 0; i < 10; i++)
+        __builtin_amdgcn_raw_buffer_store_b128(acc + (uint32_t)i, ro, (uint32_t)(i * (ALIGN ? (1u << 20) : LB)) + ocol, 0, 0);
+    if (acc.x == 0x9E3779B9u && threadIdx.x == 999) lds[0] = 1;
+}
+
 __global__ __launch_bounds__(256) void copy_flat(const u32x4 *__restrict__ s, u32x4 *__restrict__ d, size_t n16) {
     const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
     if (i < n16) d[i] = s[i];
@@ -196,7 +225,7 @@ int main(int argc, char **argv) {
     constexpr uint32_t LDS2 = 80 * 1024;  // 2 workgroups per CU, as the codec kernels' VGPRs allow
     for (const void *f : {(const void *)dec_k<1, false>, (const void *)dec_k<1, false, 1u << 20>, (const void *)dec_k<1, false, LB, ST_SPLIT>,
                           (const void *)dec_k<1, false, (1u << 20) + 16>,
-                          (const void *)dec_k<1, false, LB, ST_A4>, (const void *)enc_k<4, 1, false>, (const void *)enc_k<4, 0, false>, (const void *)enc_k<4, 2, false>,
+                          (const void *)dec_k<1, false, LB, ST_A4>, (const void *)dec_lines_k<true>, (const void *)dec_lines_k<false>, (const void *)enc_k<4, 1, false>, (const void *)enc_k<4, 0, false>, (const void *)enc_k<4, 2, false>,
                           (const void *)enc_k<2, 0, false>, (const void *)enc_k<1, 0, false>, (const void *)enc_k<8, 2, false>})
         CK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, LDS2));
     for (size_t n : {103, 256, 1024}) {
@@ -211,6 +240,16 @@ int main(int argc, char **argv) {
             run("enc_u1_disp_2wg", n, eb, [&] { enc_k<1, 0, false><<<g1, 256, LDS2>>>(src, coded, n); }, a);
             run("enc_u4_strided", n, eb, [&] { enc_k<4, 2, false><<<g4, 256>>>(src, coded, n); }, a);
             if (!only.empty()) continue;
+        }
+        if (only == "declines") {
+            constexpr uint32_t LDS3 = 52 * 1024;
+            const unsigned gl = (unsigned)(n * ((BLOCKS + 223) / 224));
+            run("dec_u1_3wg", n, db, [&] { dec_k<1, false><<<g1, 256, LDS3>>>(coded, rep, n); }, a);
+            run("dec_u1_outA_3wg", n, db, [&] { dec_k<1, false, 1u << 20><<<g1, 256, LDS3>>>(coded, rep, n); }, a);
+            run("dec_lines56_aligned_3wg", n, db, [&] { dec_lines_k<true><<<gl, 256, LDS3>>>(coded, rep, n); }, a);
+            run("dec_lines56_real_3wg", n, db, [&] { dec_lines_k<false><<<gl, 256, LDS3>>>(coded, rep, n); }, a);
+            run("dec_lines56_aligned_2wg", n, db, [&] { dec_lines_k<true><<<gl, 256, LDS2>>>(coded, rep, n); }, a);
+            continue;
         }
         if (only.empty() || only == "dec") {
             // decode outputs: the chunkset's pieces at i*L (byte-misaligned by i, the real layout) or
