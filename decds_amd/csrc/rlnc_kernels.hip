@@ -40,33 +40,17 @@ constexpr uint32_t TABLE_BYTES = 16 * ROW_BYTES;              // 16 nibble rows 
 constexpr uint32_t LDS_BYTES = K * 2 * TABLE_BYTES;           // 5 KiB
 constexpr uint32_t SWEEP_LDS = 2 * LDS_BYTES + 16;             // two table buffers + the next-tile slot
 
-constexpr uint32_t NXCD = 8;
-
-// Work units (tiles per workgroup) of the non-persistent launches and the workgroup order
-// (DESIGN.md §5.1, §8). Tuning constants, overridable at build time for in-process A/B
-// (tools/abbench.py); the shipped values are the defaults here. Encode: every batch as a persistent
-// sweep fed by a tile counter (rlnc_encode_sweep_kernel<QUEUE>: 0.69-0.71 of 8 TB/s at 103-1639
-// chunksets against 0.64-0.66 for units of 4 tiles per XCD eighth, r02r; a fixed-stride sweep drifts
-// apart: −3…−4 % at 512-1639). ENC_SWEEP_MAX_N caps it for A/B builds (units of 4 above). Decode:
-// units of 1 tile (+3…+11 % against 8 once the tables stopped being replicated, r02e).
-#ifndef DECDS_ENC_UNIT
-#define DECDS_ENC_UNIT 4
-#endif
 #ifndef DECDS_DEC_UNIT
-#define DECDS_DEC_UNIT 1
-#endif
-#ifndef DECDS_ENC_ORDER
-#define DECDS_ENC_ORDER 1  // 1: each XCD sweeps one contiguous eighth of the units; 0: dispatcher order
+#define DECDS_DEC_UNIT 1  // decode tiles per workgroup (+3...+11 % against 8 once the tables stopped being replicated, r02e)
 #endif
 #ifndef DECDS_PREFETCH_FIRST
-#define DECDS_PREFETCH_FIRST 1  // 1: a workgroup's first tile loads are issued before its table build
+#define DECDS_PREFETCH_FIRST 1  // 1: a decode workgroup's first tile loads are issued before its table build
 #endif
-constexpr uint32_t ENC_UNIT = DECDS_ENC_UNIT;
 constexpr uint32_t DEC_UNIT = DECDS_DEC_UNIT;
-#ifndef DECDS_ENC_SWEEP_MAX_N
-#define DECDS_ENC_SWEEP_MAX_N ((size_t)1 << 24)  // the C-ABI's batch limit: always the sweep
-#endif
-constexpr size_t ENC_SWEEP_MAX_N = DECDS_ENC_SWEEP_MAX_N;
+// The shipped work splits: the encode is one persistent sweep fed by a tile
+// counter for every batch (0.69-0.73 of 8 TB/s at 103-1639 chunksets against 0.64-0.66 for round 2's
+// non-persistent units of 4 tiles per XCD eighth, r02r; that form is in git history, rlnc_kernels.hip
+// at 227db28); the decode runs non-persistent workgroups of one tile.
 
 // ---- GF(2^8) ----------------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t gf_mul(uint32_t a, uint32_t b, uint32_t poly) {
@@ -409,75 +393,6 @@ __device__ __forceinline__ void stream_range(uint32_t ta, uint32_t tb, uint32_t 
     } while (++t < tb);
 }
 
-// Non-persistent workgroup -> unit index. The dispatcher deals workgroups round-robin over the 8
-// XCDs (b runs on XCD b % 8, cdna_hip_programming.md T1); the encode remaps so that each XCD
-// sweeps one contiguous eighth of the batch (its q-th workgroup the q-th unit of that eighth):
-// -3…-9 % at 1639 chunksets on the boxes that reach the DRAM's fast mode.
-__device__ __forceinline__ uint32_t xcd_eighth_unit() {
-    const uint32_t g = gridDim.x, b = blockIdx.x, x = b % NXCD, q = b / NXCD;
-    const uint32_t per = g / NXCD, rem = g % NXCD;
-    return x * per + (x < rem ? x : rem) + q;
-}
-
-// Encode: workgroup = UNIT consecutive tiles of one chunkset (TILES<DW> tiles per chunkset); the
-// launcher's form for batches above ENC_SWEEP_MAX_N (A/B builds only: the default limit is the C-ABI's).
-// The unit is walked as "segments up to the next chunkset boundary" although it never crosses one
-// (UNIT divides TILES): with that loop hipcc allocated 228 VGPRs and no spills, the straight-line
-// form of the same work 256 VGPRs + 53 spilled (-Rpass-analysis=kernel-resource-usage).
-template <uint32_t UNIT, bool XCD_ORDER, int DW, int WAVES, bool MSG>
-__global__ __launch_bounds__(WG, WAVES) __attribute__((amdgpu_waves_per_eu(WAVES, WAVES)))
-void rlnc_encode_kernel(const uint8_t *__restrict__ src, size_t n, const uint8_t *__restrict__ coeffs,
-                        uint8_t *__restrict__ dst, size_t pitch, uint32_t phase, uint32_t poly, uint32_t marker) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    constexpr uint32_t T = TILES<DW>;
-    static_assert(T % UNIT == 0, "a workgroup's tiles stay in one chunkset");
-    uint32_t ioff[K], ooff[N];
-#pragma unroll
-    for (int i = 0; i < (int)K; i++) ioff[i] = (uint32_t)(i * L);              // piece i of the padded chunkset
-#pragma unroll
-    for (int j = 0; j < (int)N; j++) ooff[j] = (uint32_t)(j * pitch + K);      // payload of coded row j
-    Vec<DW> x[K];
-    auto segment = [&](uint32_t t0, uint32_t te) {
-        const uint32_t cs = t0 / T, tile0 = t0 % T;
-        const uint8_t *M = coeffs + (size_t)cs * N * K;
-        const uint8_t *ibase = src + (size_t)cs * CS;
-        uint8_t *obase = dst + (size_t)cs * N * pitch;
-        const uint32_t cw = table_coeffs<K, N>(M, K);
-        // the first tile's loads, in flight across the table build (issued after the coefficient loads;
-        // issuing them first, so both latencies overlap, measured no faster: r02h)
-        if constexpr (DECDS_PREFETCH_FIRST) load_block<K, DW>(x, ibase, ioff, tile_col<DW, MSG>(tile0, te - cs * T, phase));
-        lds_barrier();
-        build_tables<K, N>(lds, cw, poly);
-        lds_barrier();
-        if (tile0 == 0) {  // the whole workgroup: one pass over the edge columns
-            // coding-vector prefix of the 16 full coded pieces (rlnc layout: cv || payload)
-            for (uint32_t idx = threadIdx.x; idx < N * K; idx += WG) obase[(idx / K) * pitch + idx % K] = M[idx];
-            // piece 9 carries the boundary marker, then zero padding (Encoder::new, chunkset.rs:43)
-            for (uint32_t idx = threadIdx.x; idx < edge_cols<DW, MSG>(phase) * N; idx += WG) {
-                const uint32_t j = idx % N, col = edge_col<DW, MSG>(idx / N, phase);
-                uint32_t y = 0;
-#pragma unroll
-                for (uint32_t i = 0; i < K; i++) {
-                    const uint64_t p = (uint64_t)i * L + col;
-                    const uint32_t xv = p < CS ? ibase[p] : (p == CS ? marker : 0u);
-                    y ^= tbl_mul(lds, i, j, xv);
-                }
-                obase[j * pitch + K + col] = (uint8_t)y;
-            }
-        }
-        stream_range<K, N, DW, DECDS_PREFETCH_FIRST, MSG>(tile0, te - cs * T, phase, ibase, ioff, obase, ooff, x);
-    };
-    const uint64_t total = (uint64_t)n * T;
-    uint32_t t0 = (XCD_ORDER ? xcd_eighth_unit() : blockIdx.x) * UNIT;
-    const uint32_t t1 = (uint32_t)(t0 + UNIT < total ? t0 + UNIT : total);
-    while (t0 < t1) {
-        const uint32_t cs_end = (t0 / T + 1) * T;
-        const uint32_t te = cs_end < t1 ? cs_end : t1;
-        segment(t0, te);
-        t0 = te;
-    }
-}
-
 // ---- fused commitment, wave-step form (ChunkSet::new, chunkset.rs:43-63) ------------------------
 // The unit-hash form above re-reads each unit's 256 KiB of coded rows after its stores (no longer in
 // L2 by then: 1.7 GB of extra traffic at cfg2). Here no coded byte is read back. A wave owns BLAKE3
@@ -757,18 +672,6 @@ void rlnc_encode_sweep_kernel(const uint8_t *__restrict__ src, size_t n, const u
 #ifndef DECDS_DEC_WAVES
 #define DECDS_DEC_WAVES 2  // waves per SIMD (3 measured no faster, r02f)
 #endif
-// tiles per workgroup of the line-aligned decode: 1 up to DECDS_DL_SMALL_N chunksets, DECDS_DL_UNIT
-// above (r03o, one box: units of 1 / 2 / 4 at 103 chunksets 0.417 / 0.417 / 0.427 ms, at 1639 6.80 /
-// 6.67 / 6.54 ms; the plain decode 0.422 / 6.78)
-#ifndef DECDS_DL_UNIT
-#define DECDS_DL_UNIT 4
-#endif
-#ifndef DECDS_DL_SMALL_N
-#define DECDS_DL_SMALL_N 256
-#endif
-#ifndef DECDS_DEC_LINES
-#define DECDS_DEC_LINES 1  // 1: rlnc_decode_lines_kernel (line-aligned piece stores); 0: rlnc_decode_kernel
-#endif
 template <uint32_t UNIT>
 __global__ __launch_bounds__(WG, DECDS_DEC_WAVES) __attribute__((amdgpu_waves_per_eu(DECDS_DEC_WAVES, DECDS_DEC_WAVES)))
 void rlnc_decode_kernel(const uint8_t *__restrict__ coded, size_t pitch, size_t n, const RepairPlan *__restrict__ plan,
@@ -828,119 +731,6 @@ void rlnc_decode_kernel(const uint8_t *__restrict__ coded, size_t pitch, size_t 
     // (realigning the piece stores — pieces start i bytes past alignment — through LDS staging or a DPP
     // wave shift measured 4-5 % slower / spilled: r02v/w)
     stream_range<K, K, DW, DECDS_PREFETCH_FIRST>(tile0, tile0 + UNIT, phase, ibase, ioff, obase, ooff, x);
-}
-
-// Decode with line-aligned piece stores (round 3). Piece i of the repaired chunkset starts at i*L =
-// i*2^20 + i, so the plain decode's wave stores are 1 KiB runs i bytes past line boundaries; runs that
-// fill whole 128-byte lines measured 7-8 % faster as a pattern (tools/layoutbench --only declines, r03m).
-// Here a wave computes 57 consecutive lane blocks — lane 0 the block before its run, lanes 57..63
-// idle — and lanes 1..56 each store the ALIGNED 16-byte granule g of every piece: bytes [16 - i, 32 - i)
-// of (previous lane's block || own block), the previous lane's bytes moved over by a DPP wave shift
-// (v_mov_b32_dpp wave_shr:1) and joined with v_alignbyte. A wave stores 56 granules = 7 whole lines per
-// piece; a workgroup 224 blocks (DL_TILES = 293 workgroups per chunkset). Granule 0 of piece i > 0 also
-// covers piece i-1's last i columns (edge columns, zeros here): the chunkset's first workgroup writes
-// the edge columns only after its own stores (barrier). The last block's last i columns fall in no
-// granule: the edge pass covers columns [16 * BLOCKS - 9, L) (the lanes of the last workgroup write
-// some of the same bytes with the same values).
-constexpr uint32_t DL_RUN = 56;                                          // granules per wave: 7 lines
-constexpr uint32_t DL_TILE = (WG / 64) * DL_RUN;                         // 224 blocks per workgroup
-constexpr uint32_t DL_TILES = (BLOCKS<4> + DL_TILE - 1) / DL_TILE;       // 293 per chunkset
-constexpr uint32_t DL_EDGE0 = BLOCKS<4> * COLS<4> - (K - 1);             // first edge column
-constexpr uint32_t DL_EDGE = (uint32_t)L - DL_EDGE0;                     // 26 edge columns
-static_assert(DL_TILE % 8 == 0 && DL_RUN % 8 == 0, "wave runs start on 128-byte lines");
-
-// piece I's aligned granule from this lane's 16 columns (cur) and the previous lane's (DPP)
-__device__ __forceinline__ u32x4 realign(int I, const u32x4 &cur) {
-    if (I == 0) return cur;
-    const int q = (16 - I) / 4, b = (16 - I) % 4;
-    uint32_t z[8];
-#pragma unroll
-    for (int w = 0; w < 4; w++) z[4 + w] = cur[w];
-#pragma unroll
-    for (int w = 0; w < 4; w++)
-        if (w >= q) z[w] = __builtin_amdgcn_update_dpp(0u, cur[w], 0x138 /* wave_shr:1 */, 0xf, 0xf, false);
-    u32x4 r;
-#pragma unroll
-    for (int w = 0; w < 4; w++) r[w] = b == 0 ? z[q + w] : __builtin_amdgcn_alignbyte(z[q + w + 1], z[q + w], b);
-    return r;
-}
-
-template <uint32_t UNIT>
-__global__ __launch_bounds__(WG, DECDS_DEC_WAVES) __attribute__((amdgpu_waves_per_eu(DECDS_DEC_WAVES, DECDS_DEC_WAVES)))
-void rlnc_decode_lines_kernel(const uint8_t *__restrict__ coded, size_t pitch, size_t n,
-                              const RepairPlan *__restrict__ plan, uint8_t *__restrict__ dst,
-                              int32_t *__restrict__ status, const uint64_t *__restrict__ in_bases,
-                              const uint64_t *__restrict__ out_bases, uint32_t poly, uint32_t marker) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    constexpr int DW = 4;
-    constexpr uint32_t UPC = (DL_TILES + UNIT - 1) / UNIT;  // units per chunkset
-    const uint32_t cs = blockIdx.x / UPC, t0 = (blockIdx.x % UPC) * UNIT;
-    const uint32_t te = t0 + UNIT < DL_TILES ? t0 + UNIT : DL_TILES;
-    if (cs >= n) return;
-    const uint32_t *pw = reinterpret_cast<const uint32_t *>(plan + cs);
-    const uint32_t w0 = __builtin_amdgcn_readfirstlane(pw[0]);
-    const uint32_t w1 = __builtin_amdgcn_readfirstlane(pw[1]);
-    const uint32_t w2 = __builtin_amdgcn_readfirstlane(pw[2]);
-    if (((w2 >> 16) & 0xFFu) != K) return;  // RepairPlan::rank at byte 10: not ready
-    const uint32_t cw = table_coeffs<K, K>(plan[cs].inv, K);
-    const uint32_t sel[K] = {w0 & 0xFFu, (w0 >> 8) & 0xFFu, (w0 >> 16) & 0xFFu, w0 >> 24,
-                             w1 & 0xFFu, (w1 >> 8) & 0xFFu, (w1 >> 16) & 0xFFu, w1 >> 24,
-                             w2 & 0xFFu, (w2 >> 8) & 0xFFu};
-    uint32_t ioff[K], ooff[K];
-#pragma unroll
-    for (int k = 0; k < (int)K; k++) ioff[k] = (uint32_t)(sel[k] * pitch + K);
-#pragma unroll
-    for (int i = 0; i < (int)K; i++) ooff[i] = (uint32_t)(i * L);
-    const uint8_t *ibase;
-    uint8_t *obase;
-    if (in_bases) {
-        ibase = reinterpret_cast<const uint8_t *>(uniform_u64(in_bases[cs]));
-        obase = reinterpret_cast<uint8_t *>(uniform_u64(out_bases[cs]));
-    } else {
-        ibase = coded + (size_t)cs * N * pitch;
-        obase = dst + (size_t)cs * CS;
-    }
-    const uint32_t l = threadIdx.x & 63u;
-    // this lane's block of tile t (lanes 1..56 also store its aligned granule), or out of range
-    auto blk = [&](uint32_t t) { return t * DL_TILE + (threadIdx.x >> 6) * DL_RUN + l - 1; };  // wraps for lane 0 of tile 0
-    auto col = [&](uint32_t t) {
-        const uint32_t g = blk(t);
-        return t < te && l <= DL_RUN && g < BLOCKS<DW> ? g * COLS<DW> : OOB_COL;
-    };
-    Vec<DW> x[K];
-    load_block<K, DW>(x, ibase, ioff, col(t0));
-    build_tables<K, K>(lds, cw, poly);
-    lds_barrier();
-    uint32_t gcol = 0;
-    auto sink = [&](int i, const Vec<DW> &v) { strow<DW>(obase, ((uint32_t)i << 20) + gcol, realign(i, v)); };
-    asm volatile("" ::: "memory");  // the loop's memory-counter picture: inputs, then 10 dropped stores
-#pragma unroll
-    for (int i = 0; i < (int)K; i++) strow<DW>(obase, OOB_COL + ooff[i], Vec<DW>{});
-    uint32_t t = t0;
-#pragma unroll 1
-    do {
-        const uint32_t c = col(t);
-        gcol = l >= 1 ? c : OOB_COL;  // aligned granule of each piece
-        combine_block<K, K, DW, 0, decltype(sink), 0, false>(x, obase, ooff, c, ibase, ioff, col(t + 1), sink);
-    } while (++t < te);
-    if (t0 == 0) {  // the edge columns, after this workgroup's own stores (granule 0 overlaps them)
-        __syncthreads();
-        // piece 9's must decode to marker || zeros (rlnc get_decoded_data strips them; a mismatch is a
-        // repairing failure, chunkset.rs:202-204)
-        bool ok = true;
-        for (uint32_t idx = threadIdx.x; idx < DL_EDGE * K; idx += WG) {
-            const uint32_t i = idx % K, c = DL_EDGE0 + idx / K;
-            uint32_t z = 0;
-#pragma unroll
-            for (uint32_t k = 0; k < K; k++) z ^= tbl_mul(lds, k, i, ibase[ioff[k] + c]);
-            const uint64_t p = (uint64_t)i * L + c;
-            if (p < CS)
-                obase[p] = (uint8_t)z;
-            else
-                ok &= z == (p == CS ? marker : 0u);
-        }
-        if (__any(!ok) && (threadIdx.x & 63u) == 0) status[cs] = 6;  // DECDS_ERR_CHUNKSET_REPAIRING_FAILED
-    }
 }
 
 // One wave per chunkset. Replays rlnc's incremental rank test over the candidates' 10-byte coding
@@ -1107,14 +897,13 @@ static uint32_t row_phase(const uint8_t *rows, size_t pitch) {
 }
 
 // encode lane-block width and waves per SIMD: 16-column blocks, 2 waves (254 VGPRs). 8-column
-// blocks at 3 waves per SIMD (168 VGPRs) measured no faster at any unit size (r02g).
+// blocks at 3 waves per SIMD (168 VGPRs) measured no faster (r02g).
 #ifndef DECDS_ENC_DW
 #define DECDS_ENC_DW 4
 #endif
 #ifndef DECDS_ENC_WAVES
 #define DECDS_ENC_WAVES 2
 #endif
-#define ENC_KERNEL(UNIT, ORDER, MSG) rlnc_encode_kernel<UNIT, ORDER, DECDS_ENC_DW, DECDS_ENC_WAVES, MSG>
 // fused ChunkSet::new (rlnc_encode_hash_kernel): 8-column blocks (128-byte steps) at 3 waves per SIMD;
 // 16-column blocks (256-byte steps) at 2 waves per SIMD measured 9 % slower (r03d)
 #ifndef DECDS_FH_DW
@@ -1132,11 +921,8 @@ constexpr bool MSG_OK = DECDS_ENC_DW == 4;
 #define ENC_SWEEP(MSG) rlnc_encode_sweep_kernel<DECDS_ENC_DW, DECDS_ENC_WAVES, MSG, (DECDS_ENC_QUEUE != 0)>
 
 hipError_t configure_kernels() {
-    const void *fns[] = {reinterpret_cast<const void *>(ENC_KERNEL(ENC_UNIT, DECDS_ENC_ORDER != 0, false)),
-                         reinterpret_cast<const void *>(ENC_KERNEL(ENC_UNIT, DECDS_ENC_ORDER != 0, MSG_OK)),
-                         reinterpret_cast<const void *>(ENC_SWEEP(false)), reinterpret_cast<const void *>(ENC_SWEEP(MSG_OK)),
-                         reinterpret_cast<const void *>(ENC_HASH),
-                         reinterpret_cast<const void *>(rlnc_decode_kernel<DEC_UNIT>)};
+    const void *fns[] = {reinterpret_cast<const void *>(ENC_SWEEP(false)), reinterpret_cast<const void *>(ENC_SWEEP(MSG_OK)),
+                         reinterpret_cast<const void *>(ENC_HASH), reinterpret_cast<const void *>(rlnc_decode_kernel<DEC_UNIT>)};
     for (const void *f : fns) {
         hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, std::max(SWEEP_LDS, FH_LDS<DECDS_FH_DW>));
         if (e != hipSuccess) return e;
@@ -1163,26 +949,21 @@ hipError_t launch_encode(const LaunchGeom &geom, const uint8_t *src, size_t n, c
     const uint32_t phase = row_phase<DECDS_ENC_DW>(dst, pitch);
     const bool msg = MSG_OK && phase == MSG_PHASE;
     constexpr uint32_t T = TILES<DECDS_ENC_DW>;
-    if (n <= ENC_SWEEP_MAX_N) {  // small batches too: with fewer tiles than resident slots it is one tile each
-        const uint32_t grid = (uint32_t)std::min<uint64_t>((uint64_t)n * T, sweep_grid(geom));
-        const void *fn = msg ? reinterpret_cast<const void *>(ENC_SWEEP(MSG_OK)) : reinterpret_cast<const void *>(ENC_SWEEP(false));
-        uint32_t *counter = nullptr;  // none when every workgroup has one tile: no counter reset to launch
-        if (DECDS_ENC_QUEUE && (uint64_t)n * T > grid) {
-            if (!geom.counters) return hipErrorInvalidValue;
-            counter = geom.counters + (geom.counter_next.fetch_add(1) % LaunchGeom::N_COUNTERS) * LaunchGeom::COUNTER_STRIDE;
-        }
-        void *args[] = {&src, &n, &coeffs, &dst, &pitch, const_cast<uint32_t *>(&phase), &poly, &marker, &counter};
-        return hipLaunchKernel(fn, dim3(grid), dim3(WG), args, SWEEP_LDS, stream);
+    // small batches too: with fewer tiles than resident slots it is one tile each
+    const uint32_t grid = (uint32_t)std::min<uint64_t>((uint64_t)n * T, sweep_grid(geom));
+    const void *fn = msg ? reinterpret_cast<const void *>(ENC_SWEEP(MSG_OK)) : reinterpret_cast<const void *>(ENC_SWEEP(false));
+    uint32_t *counter = nullptr;  // none when every workgroup has one tile: no counter reset to launch
+    if (DECDS_ENC_QUEUE && (uint64_t)n * T > grid) {
+        if (!geom.counters) return hipErrorInvalidValue;
+        counter = geom.counters + (geom.counter_next.fetch_add(1) % LaunchGeom::N_COUNTERS) * LaunchGeom::COUNTER_STRIDE;
     }
-    const void *fn = msg ? reinterpret_cast<const void *>(ENC_KERNEL(ENC_UNIT, DECDS_ENC_ORDER != 0, MSG_OK))
-                         : reinterpret_cast<const void *>(ENC_KERNEL(ENC_UNIT, DECDS_ENC_ORDER != 0, false));
-    void *args[] = {&src, &n, &coeffs, &dst, &pitch, const_cast<uint32_t *>(&phase), &poly, &marker};
-    return hipLaunchKernel(fn, dim3((uint32_t)(n * (T / ENC_UNIT))), dim3(WG), args, LDS_BYTES, stream);
+    void *args[] = {&src, &n, &coeffs, &dst, &pitch, const_cast<uint32_t *>(&phase), &poly, &marker, &counter};
+    return hipLaunchKernel(fn, dim3(grid), dim3(WG), args, SWEEP_LDS, stream);
 }
 
-const char *decode_kernel_name(size_t) { return DECDS_DEC_LINES ? "rlnc_decode_lines_kernel" : "rlnc_decode_kernel"; }
+const char *decode_kernel_name(size_t) { return "rlnc_decode_kernel"; }
 
-const char *encode_kernel_name(size_t n) { return n <= ENC_SWEEP_MAX_N ? "rlnc_encode_sweep_kernel" : "rlnc_encode_kernel"; }
+const char *encode_kernel_name(size_t) { return "rlnc_encode_sweep_kernel"; }
 
 bool encode_commit_fusable(const uint8_t *dst, size_t pitch) { return row_phase<4>(dst, pitch) == MSG_PHASE; }
 static_assert(MSG_PHASE < COLS<2>, "16-byte-aligned rows have the message phase for both block widths");
@@ -1211,25 +992,10 @@ hipError_t launch_decode(const LaunchGeom &, const uint8_t *coded, size_t pitch,
                          uint32_t poly, uint32_t marker, hipStream_t stream) {
     if (n == 0) return hipSuccess;
     const RepairPlan *pl = reinterpret_cast<const RepairPlan *>(plan);
-    auto go = [&](auto unit) {
-        constexpr uint32_t U = decltype(unit)::value;
-        hipLaunchKernelGGL(rlnc_decode_kernel<U>, dim3((uint32_t)(n * (TILES<4> / U))), dim3(WG), LDS_BYTES,
-                           stream, coded, pitch, n, pl, dst, status, in_bases, out_bases, poly, marker);
-        return hipGetLastError();
-    };
-    if (DECDS_DEC_LINES) {
-        auto lines = [&](auto unit) {
-            constexpr uint32_t U = decltype(unit)::value;
-            hipLaunchKernelGGL(rlnc_decode_lines_kernel<U>, dim3((uint32_t)(n * ((DL_TILES + U - 1) / U))), dim3(WG),
-                               LDS_BYTES, stream, coded, pitch, n, pl, dst, status, in_bases, out_bases, poly, marker);
-        };
-        if (n <= DECDS_DL_SMALL_N)
-            lines(std::integral_constant<uint32_t, 1>{});
-        else
-            lines(std::integral_constant<uint32_t, DECDS_DL_UNIT>{});
-        return hipGetLastError();
-    }
-    return go(std::integral_constant<uint32_t, DEC_UNIT>{});
+    constexpr uint32_t U = DEC_UNIT;
+    hipLaunchKernelGGL(rlnc_decode_kernel<U>, dim3((uint32_t)(n * (TILES<4> / U))), dim3(WG), LDS_BYTES, stream, coded,
+                       pitch, n, pl, dst, status, in_bases, out_bases, poly, marker);
+    return hipGetLastError();
 }
 
 hipError_t launch_fill_random(uint64_t seed, uint64_t byte_offset, uint8_t *dst, size_t nbytes,

@@ -121,7 +121,7 @@ int decds_decode_batch(decds_ctx *ctx, const uint8_t *coded, size_t coded_pitch,
                        void *stream);
 
 /* name of the gfx950 kernel decds_decode_batch launches for n chunksets (for profiles and traces:
- * rlnc_decode_lines_kernel, whose piece stores fill whole 128-byte lines) */
+ * rlnc_decode_kernel) */
 const char *decds_decode_kernel_name(size_t n_chunksets);
 
 /* plan + decode in one call (the RepairingBlob::add_chunk loop + get_repaired_chunkset,

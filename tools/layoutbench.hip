@@ -141,6 +141,32 @@ __global__ __launch_bounds__(256) void dec_k(const uint8_t *__restrict__ in, uin
     if (acc.x == 0x9E3779B9u && threadIdx.x == 999) lds[0] = 1;
 }
 
+// encode pattern with line-aligned input runs (the load side of a DPP-realigned encode): each wave
+// loads 57 consecutive 16-byte input granules per piece — lanes 0..56, lanes 57..63 idle — and lanes
+// 0..55 store 56 blocks (7 whole lines) of each of the 16 coded rows (payload-aligned rows). ALIGN
+// true: pieces 1 MiB apart (granules line-aligned); false: the real pieces at i*L.
+template <bool ALIGN>
+__global__ __launch_bounds__(256) void enc_lines_k(const uint8_t *__restrict__ in, uint8_t *__restrict__ out, size_t n) {
+    extern __shared__ uint8_t lds[];
+    constexpr uint32_t PER_WAVE = 56, PER_TILE = 4 * PER_WAVE, T2 = (BLOCKS + PER_TILE - 1) / PER_TILE;
+    const uint32_t cs = blockIdx.x / T2, t = blockIdx.x % T2;
+    if (cs >= n) return;
+    const auto ri = rsrc(in + cs * CSB);
+    const auto ro = rsrc(out + cs * 16 * PITCH);
+    const uint32_t l = threadIdx.x & 63u;
+    const uint32_t g = t * PER_TILE + (threadIdx.x >> 6) * PER_WAVE + l;
+    const uint32_t col = l <= PER_WAVE && g < BLOCKS ? g * 16 : 0x80000000u;
+    u32x4 x[10], acc = {0, 0, 0, 0};
+#pragma unroll
+    for (int i = 0; i < 10; i++) x[i] = __builtin_amdgcn_raw_buffer_load_b128(ri, (uint32_t)(i * (ALIGN ? (1u << 20) : LB)) + col, 0, 0);
+#pragma unroll
+    for (int i = 0; i < 10; i++) acc ^= x[i];
+    const uint32_t ocol = l < PER_WAVE && g < BLOCKS ? 128 + g * 16 : 0x80000000u;
+#pragma unroll
+    for (int j = 0; j < 16; j++) __builtin_amdgcn_raw_buffer_store_b128(acc + (uint32_t)j, ro, ocol + (uint32_t)(j * PITCH), 0, 0);
+    if (acc.x == 0x9E3779B9u && threadIdx.x == 999) lds[0] = 1;
+}
+
 // decode pattern with line-aligned wave stores (the store side of a DPP-realigned decode): each wave
 // computes 57 consecutive lane blocks — lane 0 the block before its run, lanes 57..63 idle — and each
 // of lanes 1..56 stores one 16-byte granule per output piece: 7 whole 128-byte lines per wave and piece
@@ -225,7 +251,8 @@ int main(int argc, char **argv) {
     constexpr uint32_t LDS2 = 80 * 1024;  // 2 workgroups per CU, as the codec kernels' VGPRs allow
     for (const void *f : {(const void *)dec_k<1, false>, (const void *)dec_k<1, false, 1u << 20>, (const void *)dec_k<1, false, LB, ST_SPLIT>,
                           (const void *)dec_k<1, false, (1u << 20) + 16>,
-                          (const void *)dec_k<1, false, LB, ST_A4>, (const void *)dec_lines_k<true>, (const void *)dec_lines_k<false>, (const void *)enc_k<4, 1, false>, (const void *)enc_k<4, 0, false>, (const void *)enc_k<4, 2, false>,
+                          (const void *)dec_k<1, false, LB, ST_A4>, (const void *)dec_lines_k<true>, (const void *)dec_lines_k<false>,
+                          (const void *)enc_lines_k<true>, (const void *)enc_lines_k<false>, (const void *)enc_k<4, 1, false>, (const void *)enc_k<4, 0, false>, (const void *)enc_k<4, 2, false>,
                           (const void *)enc_k<2, 0, false>, (const void *)enc_k<1, 0, false>, (const void *)enc_k<8, 2, false>})
         CK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, LDS2));
     for (size_t n : {103, 256, 1024}) {
@@ -240,6 +267,17 @@ int main(int argc, char **argv) {
             run("enc_u1_disp_2wg", n, eb, [&] { enc_k<1, 0, false><<<g1, 256, LDS2>>>(src, coded, n); }, a);
             run("enc_u4_strided", n, eb, [&] { enc_k<4, 2, false><<<g4, 256>>>(src, coded, n); }, a);
             if (!only.empty()) continue;
+        }
+        if (only == "enclines") {
+            const unsigned gl = (unsigned)(n * ((BLOCKS + 223) / 224));
+            run("enc_u1_disp_2wg", n, eb, [&] { enc_k<1, 0, false><<<g1, 256, LDS2>>>(src, coded, n); }, a);
+            run("enc_lines56_inA_2wg", n, eb, [&] { enc_lines_k<true><<<gl, 256, LDS2>>>(src, coded, n); }, a);
+            run("enc_lines56_real_2wg", n, eb, [&] { enc_lines_k<false><<<gl, 256, LDS2>>>(src, coded, n); }, a);
+            run("copy_flat", n, 2.0 * n * CSB, [&] {
+                const size_t n16 = (size_t)n * CSB / 16;
+                copy_flat<<<(unsigned)((n16 + 255) / 256), 256>>>((const u32x4 *)src, (u32x4 *)rep, n16);
+            }, a);
+            continue;
         }
         if (only == "declines") {
             constexpr uint32_t LDS3 = 52 * 1024;
