@@ -11,7 +11,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libdecds_rlnc.so")
 SOURCES = ["rlnc_kernels.hip", "commit_kernels.hip", "capi.cpp", "host_util.cpp", "host_mem.cpp", "chunkset.cpp", "blob.cpp",
-           "commit.cpp", "wire.cpp"]
+           "commit.cpp", "wire.cpp", "blake3_host.cpp"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-result",
          "-Wno-unused-command-line-argument", "-I" + os.path.join(HERE, "..", "include")]

@@ -6,6 +6,7 @@
 #include <vector>
 
 #include "../../include/decds_rlnc.h"
+#include "blake3_host.h"
 #include "blake3_impl.h"
 #include "capi_internal.h"
 #include "commit_kernels.h"
@@ -47,6 +48,13 @@ void chunk_cv(const uint8_t *p, size_t len, uint64_t index, bool root, uint32_t 
 void subtree_cv(const uint8_t *p, size_t len, uint64_t first, bool root, uint32_t cv[8]) {
     if (len <= b3::CHUNK) {
         chunk_cv(p, len, first, root, cv);
+        return;
+    }
+    // complete power-of-two subtrees of 8 .. 1024 chunks: 8 chunks / parents per AVX2 compression
+    const size_t nch = len / b3::CHUNK;
+    if (!root && len % b3::CHUNK == 0 && (nch & (nch - 1)) == 0 && nch >= 8 && nch <= b3h::MAX_SIMD_SUBTREE &&
+        b3h::simd_available()) {
+        b3h::simd_subtree(p, nch, first, cv);
         return;
     }
     size_t left_chunks = 1;

@@ -43,7 +43,8 @@ def test_oracle_blake3_known_answers():
         assert o.blake3(mod251(n)).hex() == h
 
 
-@pytest.mark.parametrize("n", [0, 1, 63, 64, 65, 1023, 1024, 1025, 2048, 2049, 3073, 8192, 8193, 65537, 1048603])
+@pytest.mark.parametrize("n", [0, 1, 63, 64, 65, 1023, 1024, 1025, 2048, 2049, 3073, 8192, 8193, 16384, 16385, 49157,
+                               65537, 1048603, 3 * 2**20 + 11])
 def test_host_blake3_matches_oracle(n):
     msg = o.fill_random(n + 5, n).tobytes()
     assert host_blake3(msg) == o.blake3(msg)

@@ -1,0 +1,102 @@
+"""The reference's public blob API at the C-ABI, timed end to end from host memory (SURVEY.md §8a
+rows a9/a10): Blob::new over a random blob (whole-blob BLAKE3 on host threads, encode + commitment on
+the device, blob-level tree, chunks back in host memory), then the incremental RepairingBlob the way
+decds-bin's repair loop drives it (handle_repair.rs:41-92): per chunkset, chunks of 10 random shares
+one add_chunk call at a time (each validated: chunk digest + two Merkle paths on the host), then
+get_repaired_chunkset for every chunkset (ready chunksets decoded in device batches), checked
+against the blob. Also the batched add_chunks form (validation on the device). One JSON line.
+
+usage: python tools/blob_bench.py [--gib 1]"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gib", type=float, default=1.0)
+    a = ap.parse_args()
+    import numpy as np
+    import torch  # noqa: F401  (torch's HIP runtime first, as the other tools)
+    import decds_amd
+    from decds_amd import codec
+    from decds_amd._capi import CHUNKSET_BYTES as CS, CODED_PIECE_BYTES as F, K, N, check, lib
+    from decds_amd.blob import Blob, HostBuffer, RepairingBlob
+
+    L = lib()
+    ctx = decds_amd.Context(0)
+    size = int(a.gib * (1 << 30))
+    data = HostBuffer(size)
+    data.array[:] = codec.fill_random_host(0xB10B, size)
+    n = -(-size // CS)
+    res = {"blob_GiB": a.gib, "chunksets": n}
+
+    t0 = time.perf_counter()
+    blob = Blob(ctx, data.array)
+    res["blob_new_s"] = round(time.perf_counter() - t0, 3)
+    res["blob_new_GiBps"] = round(a.gib / res["blob_new_s"], 2)
+    header = blob.get_blob_header()
+    plen = blob.proof_len()
+    rng = np.random.default_rng(7)
+    picks = [rng.permutation(N)[:K] for _ in range(n)]
+    # pointers to every picked chunk inside the blob (zero-copy) and its proof
+    dp = ctypes.c_void_p()
+    chunks = []
+    for c in range(n):
+        for j in picks[c]:
+            proof = ctypes.create_string_buffer(32 * plen)
+            check(L.decds_blob_get_chunk(blob._h, c, int(j), ctypes.byref(dp), proof, len(proof)))
+            chunks.append((c, c * N + int(j), dp.value, proof))
+
+    def repair(batched):
+        rb = RepairingBlob(ctx, header)
+        t0 = time.perf_counter()
+        if batched:
+            m = len(chunks)
+            rows = np.empty((m, F), np.uint8)
+            ids = np.empty((m, 2), np.uint64)
+            prf = np.empty((m, plen * 32), np.uint8)
+            for i, (c, gid, p, proof) in enumerate(chunks):
+                rows[i] = np.ctypeslib.as_array((ctypes.c_uint8 * F).from_address(p))
+                ids[i] = (c, gid)
+                prf[i] = np.frombuffer(proof.raw, np.uint8)
+            t0 = time.perf_counter()  # the batch call alone (the row gather above is the caller's)
+            st = rb.add_rows(rows, ids, prf, plen)
+            assert (st == 0).sum() >= n * (K - 1), "too many rejected chunks"
+        else:
+            for c, gid, p, proof in chunks:
+                s = L.decds_repairing_blob_add_chunk(rb._h, c, gid, ctypes.c_void_p(p), F, proof, plen)
+                if s not in (0, 4):  # 4: ChunkDecodingFailed (a dependent chunk), which the reference tolerates
+                    check(s)
+        t_add = time.perf_counter() - t0
+        out = HostBuffer(CS)
+        t0 = time.perf_counter()
+        ok = 0
+        for c in range(n):
+            if not rb.is_chunkset_ready_to_repair(c):
+                continue
+            got = rb.get_repaired_chunkset(c, out=out.array)
+            lo = c * CS
+            assert np.array_equal(got, data.array[lo:lo + got.size]), c
+            ok += 1
+        t_get = time.perf_counter() - t0
+        out.free()
+        return t_add, t_get, ok
+
+    for name, batched in (("add_chunk", False), ("add_chunks_batch", True)):
+        t_add, t_get, ok = repair(batched)
+        gib_ok = ok * CS / (1 << 30)
+        res[name] = {"add_s": round(t_add, 3), "get_repaired_s": round(t_get, 3), "repaired_chunksets": ok,
+                     "GiBps": round(gib_ok / (t_add + t_get), 2),
+                     "per_chunk_add_us": round(t_add / len(chunks) * 1e6, 1)}
+    print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()
