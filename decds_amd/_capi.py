@@ -41,6 +41,8 @@ STATUS_NAMES = {
     13: "BlobHeaderDeserializationFailed",
     14: "ProofCarryingChunkSerializationFailed",
     15: "ProofCarryingChunkDeserializationFailed",
+    16: "InvalidStartBound",
+    17: "InvalidEndBound",
     -1: "HipError",
     -2: "InvalidArgument",
     -3: "NoDevice",

@@ -74,6 +74,8 @@ const char *decds_status_string(int s) {
         case DECDS_ERR_BLOB_HEADER_DESERIALIZATION_FAILED: return "failed to deserialize blob header";
         case DECDS_ERR_PCC_SERIALIZATION_FAILED: return "failed to serialize proof carrying chunk";
         case DECDS_ERR_PCC_DESERIALIZATION_FAILED: return "failed to deserialize proof carrying chunk";
+        case DECDS_ERR_INVALID_START_BOUND: return "invalid start bound";
+        case DECDS_ERR_INVALID_END_BOUND: return "invalid end bound";
         case DECDS_ERR_HIP: return "HIP runtime error";
         case DECDS_ERR_INVALID_ARGUMENT: return "invalid argument";
         case DECDS_ERR_NO_DEVICE: return "no gfx950 device";

@@ -3,7 +3,7 @@
 168-197), with the reference's method names."""
 import ctypes
 
-from ._capi import check, lib
+from ._capi import CHUNKSET_BYTES, N, STATUS, DecdsError, check, lib
 from .chunkset import Chunk
 
 
@@ -58,6 +58,63 @@ class BlobHeader:
 
     def get_root_commitment(self):
         return self.root_commitment
+
+    def get_num_chunks(self):
+        """blob.rs:38-40"""
+        return self.num_chunksets * N
+
+    def _check_id(self, chunkset_id):
+        if not 0 <= chunkset_id < self.num_chunksets:
+            raise DecdsError(STATUS["InvalidChunksetId"],
+                             "invalid chunkset id: %d (num_chunksets: %d)" % (chunkset_id, self.num_chunksets))
+
+    def get_chunkset_commitment(self, chunkset_id):
+        """blob.rs:65-71"""
+        self._check_id(chunkset_id)
+        return self.chunkset_root_commitments[chunkset_id]
+
+    def get_chunkset_size(self, chunkset_id):
+        """blob.rs:84-94: the chunkset's real byte count (the last one may be partial)"""
+        lo, hi = self.get_byte_range_for_chunkset(chunkset_id)
+        return hi - lo
+
+    def get_byte_range_for_chunkset(self, chunkset_id):
+        """blob.rs:108-117: [start, end) of the chunkset within the blob"""
+        self._check_id(chunkset_id)
+        lo = chunkset_id * CHUNKSET_BYTES
+        return lo, min(lo + CHUNKSET_BYTES, self.byte_length)
+
+    def get_chunkset_ids_for_byte_range(self, start=None, end=None, end_inclusive=False):
+        """blob.rs:132-160 with Rust's RangeBounds spelled out: start None = unbounded (0), else included;
+        end None = unbounded (InvalidEndBound(usize::MAX)), else excluded, or included if end_inclusive
+        (`a..b` -> (a, b); `a..=b` -> (a, b, True); `..` -> (None, None)). A Python range works too."""
+        if isinstance(start, range):
+            if start.step != 1:
+                raise ValueError("byte ranges have step 1")
+            start, end, end_inclusive = start.start, start.stop, False
+        if start is not None and start < 0:
+            raise DecdsError(STATUS["InvalidStartBound"], "invalid start bound")
+        first = 0 if start is None else start
+        if end is None:
+            raise DecdsError(STATUS["InvalidEndBound"], "invalid end bound: %d" % (2**64 - 1))
+        if end_inclusive:
+            last = end
+        else:
+            if end == 0:
+                raise DecdsError(STATUS["InvalidEndBound"], "invalid end bound: 0")
+            last = end - 1
+        a, b = first // CHUNKSET_BYTES, last // CHUNKSET_BYTES
+        if b >= self.num_chunksets:
+            raise DecdsError(STATUS["InvalidChunksetId"],
+                             "invalid chunkset id: %d (num_chunksets: %d)" % (b, self.num_chunksets))
+        return list(range(a, b + 1))
+
+    def validate_chunk(self, chunk):
+        """blob.rs:211-215: the chunk's blob-level path against the root, its chunkset id in range and its
+        chunkset-level path against that chunkset's root (host BLAKE3, chunk.rs:88-110)"""
+        cs = chunk.get_chunkset_id()
+        return (chunk.validate_inclusion_in_blob(self.root_commitment) and cs < self.num_chunksets
+                and chunk.validate_inclusion_in_chunkset(self.chunkset_root_commitments[cs]))
 
     def to_bytes(self):
         """BlobHeader::to_bytes (blob.rs:168-170)"""

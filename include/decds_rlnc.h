@@ -63,6 +63,8 @@ extern "C" {
 #define DECDS_ERR_BLOB_HEADER_DESERIALIZATION_FAILED 13  /* BlobHeaderDeserializationFailed   errors.rs:15 */
 #define DECDS_ERR_PCC_SERIALIZATION_FAILED 14            /* ProofCarryingChunkSerializationFailed   errors.rs:18 */
 #define DECDS_ERR_PCC_DESERIALIZATION_FAILED 15          /* ProofCarryingChunkDeserializationFailed errors.rs:20 */
+#define DECDS_ERR_INVALID_START_BOUND 16           /* InvalidStartBound               errors.rs:8 (byte-range queries, host) */
+#define DECDS_ERR_INVALID_END_BOUND 17             /* InvalidEndBound(end)            errors.rs:10 (byte-range queries, host) */
 #define DECDS_ERR_HIP (-1)                         /* HIP runtime failure (text: decds_last_error) */
 #define DECDS_ERR_INVALID_ARGUMENT (-2)
 #define DECDS_ERR_NO_DEVICE (-3)

@@ -57,6 +57,13 @@ def test_blob_new_matches_oracle(ctx):
             cproof = o.merkle(leaves[c])[1][j]
             assert ch.get_proof() == cproof + bproofs[c]                            # chunkset.rs:98-102
             assert o.merkle_verify(c * N + j, leaves[c][j], ch.get_proof(), broot)  # chunk.rs:88-90
+            assert h.validate_chunk(ch)                                              # blob.rs:211-215
+    # a flipped byte, or a chunk presented under another chunkset's id, fails validation
+    ch = blob.get_share(3)[1]
+    bad = bytearray(ch.get_erasure_coded_data())
+    bad[777] ^= 1
+    assert not h.validate_chunk(decds_amd.Chunk(1, N + 3, bytes(bad), ch.get_proof()))
+    assert not h.validate_chunk(decds_amd.Chunk(2, N + 3, ch.get_erasure_coded_data(), ch.get_proof()))
     _raises("InvalidErasureCodedShareId", blob.get_share, N)
     _raises("EmptyDataForBlob", decds_amd.Blob, ctx, b"")
     # a multi-context Blob (shards over two contexts of the one device) is identical

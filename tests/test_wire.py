@@ -10,7 +10,7 @@ import numpy as np
 import pytest
 
 from decds_amd import wire
-from decds_amd._capi import DecdsError, lib
+from decds_amd._capi import CHUNKSET_BYTES as CS, DecdsError, lib
 from decds_amd.chunkset import Chunk
 import oracle as o
 
@@ -101,3 +101,55 @@ def test_parallel_blake3_matches_oracle(n, threads):
     out = ctypes.create_string_buffer(32)
     lib().decds_blake3_parallel(msg, n, out, threads)
     assert out.raw == o.blake3(msg)
+
+
+def _header_2_5():
+    # a 2.5-chunkset blob's header (blob.rs:507-631 build theirs with Blob::new; the queries read
+    # only the sizes and roots)
+    from decds_amd.wire import BlobHeader
+    n = 3
+    roots = [bytes([i]) * 32 for i in range(n)]
+    return BlobHeader(2 * CS + CS // 2, n, b"\1" * 32, b"\2" * 32, roots)
+
+
+def _err(kind, fn, *a, **kw):
+    with pytest.raises(DecdsError) as e:
+        fn(*a, **kw)
+    assert e.value.kind == kind, e.value
+    return e.value
+
+
+def test_blob_header_chunkset_queries_like_reference():
+    h = _header_2_5()
+    assert h.get_num_chunks() == 48
+    # blob.rs:507-526 get_chunkset_commitment
+    assert h.get_chunkset_commitment(0) == b"\0" * 32 and h.get_chunkset_commitment(1) == b"\1" * 32
+    _err("InvalidChunksetId", h.get_chunkset_commitment, 3)
+    # blob.rs:529-551 get_chunkset_size
+    assert [h.get_chunkset_size(c) for c in range(3)] == [CS, CS, CS // 2]
+    _err("InvalidChunksetId", h.get_chunkset_size, 3)
+    # blob.rs:554-580 get_byte_range_for_chunkset
+    assert h.get_byte_range_for_chunkset(0) == (0, CS)
+    assert h.get_byte_range_for_chunkset(1) == (CS, 2 * CS)
+    assert h.get_byte_range_for_chunkset(2) == (2 * CS, 2 * CS + CS // 2)
+    _err("InvalidChunksetId", h.get_byte_range_for_chunkset, 3)
+
+
+def test_blob_header_chunkset_ids_for_byte_range_like_reference():
+    # blob.rs:583-631
+    h = _header_2_5()
+    blen = h.get_blob_size()
+    q = h.get_chunkset_ids_for_byte_range
+    assert q(0, 10) == [0] and q(range(0, 10)) == [0]
+    assert q(CS + 10, CS + 20) == [1]
+    assert q(10, CS + 10) == [0, 1]
+    assert q(10, blen) == [0, 1, 2]
+    assert q(0, CS) == [0]
+    assert q(0, CS - 1, end_inclusive=True) == [0]
+    _err("InvalidEndBound", q, 0, 0)
+    assert q(0, 0, end_inclusive=True) == [0]
+    beyond = blen + CS
+    e = _err("InvalidChunksetId", q, 0, beyond)
+    assert str((beyond - 1) // CS) in str(e)
+    _err("InvalidEndBound", q, None, None)
+    _err("InvalidEndBound", q, 0, None)
