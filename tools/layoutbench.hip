@@ -141,6 +141,38 @@ __global__ __launch_bounds__(256) void dec_k(const uint8_t *__restrict__ in, uin
     if (acc.x == 0x9E3779B9u && threadIdx.x == 999) lds[0] = 1;
 }
 
+// decode pattern with line-aligned stores and all 64 lanes busy: a workgroup's 4 waves store the 256
+// aligned granules of their tile (4 KiB per piece, 32 whole lines) — every lane its block's granule,
+// whose first i bytes belong to the previous block (another wave's lane 63 for lane 0: an LDS
+// exchange in the real kernel). At tile edges the granule reaches into the previous tile, so the
+// tile's first lane stores its block at the real (misaligned) offset instead and the tile's last lane
+// adds a misaligned store of its own block. The stores only, no arithmetic.
+__global__ __launch_bounds__(256) void dec_tile_lines_k(const uint8_t *__restrict__ in, uint8_t *__restrict__ out, size_t n) {
+    extern __shared__ uint8_t lds[];
+    const uint32_t cs = blockIdx.x / TILES, t = blockIdx.x % TILES;
+    if (cs >= n) return;
+    constexpr uint32_t sel[10] = {0, 2, 3, 5, 6, 8, 9, 11, 13, 15};
+    const auto ri = rsrc(in + cs * 16 * PITCH);
+    const auto ro = rsrc(out + cs * CSB);
+    const uint32_t g = t * 256 + threadIdx.x;
+    const uint32_t col = g < BLOCKS ? g * 16 : 0x80000000u;
+    u32x4 x[10], acc = {0, 0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < 10; k++) x[k] = __builtin_amdgcn_raw_buffer_load_b128(ri, 128 + col + sel[k] * (uint32_t)PITCH, 0, 0);
+#pragma unroll
+    for (int k = 0; k < 10; k++) acc ^= x[k];
+    const bool first = threadIdx.x == 0, last = threadIdx.x == 255 || g == BLOCKS - 1;
+#pragma unroll
+    for (int i = 0; i < 10; i++) {
+        const uint32_t off = first ? (uint32_t)(i * LB) + col : (uint32_t)(i << 20) + col;  // real offset : aligned granule
+        __builtin_amdgcn_raw_buffer_store_b128(acc + (uint32_t)i, ro, off, 0, 0);
+    }
+    if (last)
+#pragma unroll
+        for (int i = 0; i < 10; i++) __builtin_amdgcn_raw_buffer_store_b128(acc + (uint32_t)i, ro, (uint32_t)(i * LB) + col, 0, 0);
+    if (acc.x == 0x9E3779B9u && threadIdx.x == 999) lds[0] = 1;
+}
+
 // encode pattern with line-aligned input runs (the load side of a DPP-realigned encode): each wave
 // loads 57 consecutive 16-byte input granules per piece — lanes 0..56, lanes 57..63 idle — and lanes
 // 0..55 store 56 blocks (7 whole lines) of each of the 16 coded rows (payload-aligned rows). ALIGN
@@ -252,7 +284,7 @@ int main(int argc, char **argv) {
     for (const void *f : {(const void *)dec_k<1, false>, (const void *)dec_k<1, false, 1u << 20>, (const void *)dec_k<1, false, LB, ST_SPLIT>,
                           (const void *)dec_k<1, false, (1u << 20) + 16>,
                           (const void *)dec_k<1, false, LB, ST_A4>, (const void *)dec_lines_k<true>, (const void *)dec_lines_k<false>,
-                          (const void *)enc_lines_k<true>, (const void *)enc_lines_k<false>, (const void *)enc_k<4, 1, false>, (const void *)enc_k<4, 0, false>, (const void *)enc_k<4, 2, false>,
+                          (const void *)enc_lines_k<true>, (const void *)enc_lines_k<false>, (const void *)dec_tile_lines_k, (const void *)enc_k<4, 1, false>, (const void *)enc_k<4, 0, false>, (const void *)enc_k<4, 2, false>,
                           (const void *)enc_k<2, 0, false>, (const void *)enc_k<1, 0, false>, (const void *)enc_k<8, 2, false>})
         CK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, LDS2));
     for (size_t n : {103, 256, 1024}) {
@@ -287,6 +319,9 @@ int main(int argc, char **argv) {
             run("dec_lines56_aligned_3wg", n, db, [&] { dec_lines_k<true><<<gl, 256, LDS3>>>(coded, rep, n); }, a);
             run("dec_lines56_real_3wg", n, db, [&] { dec_lines_k<false><<<gl, 256, LDS3>>>(coded, rep, n); }, a);
             run("dec_lines56_aligned_2wg", n, db, [&] { dec_lines_k<true><<<gl, 256, LDS2>>>(coded, rep, n); }, a);
+            run("dec_tile_lines_3wg", n, db, [&] { dec_tile_lines_k<<<g1, 256, LDS3>>>(coded, rep, n); }, a);
+            run("dec_tile_lines_2wg", n, db, [&] { dec_tile_lines_k<<<g1, 256, LDS2>>>(coded, rep, n); }, a);
+            run("dec_u1_2wg", n, db, [&] { dec_k<1, false><<<g1, 256, LDS2>>>(coded, rep, n); }, a);
             continue;
         }
         if (only.empty() || only == "dec") {
