@@ -173,6 +173,33 @@ __global__ __launch_bounds__(256) void dec_tile_lines_k(const uint8_t *__restric
     if (acc.x == 0x9E3779B9u && threadIdx.x == 999) lds[0] = 1;
 }
 
+// decode pattern: a workgroup's 256 lanes compute 256 consecutive blocks, lane 0 the block before the
+// tile (recomputed), and lanes 1..248 store 248 aligned granules = 31 whole lines per piece (lanes
+// 249..255 idle): no straggler crosses a workgroup; wave runs (63 / 64 / 64 / 57 granules) meet inside
+// the workgroup at arbitrary 16-byte boundaries. The stores only.
+__global__ __launch_bounds__(256) void dec_wg248_k(const uint8_t *__restrict__ in, uint8_t *__restrict__ out, size_t n) {
+    extern __shared__ uint8_t lds[];
+    constexpr uint32_t PER = 248, T2 = (BLOCKS + PER - 1) / PER;
+    const uint32_t cs = blockIdx.x / T2, t = blockIdx.x % T2;
+    if (cs >= n) return;
+    constexpr uint32_t sel[10] = {0, 2, 3, 5, 6, 8, 9, 11, 13, 15};
+    const auto ri = rsrc(in + cs * 16 * PITCH);
+    const auto ro = rsrc(out + cs * CSB);
+    const uint32_t l = threadIdx.x;
+    const uint32_t g = t * PER + l - 1;
+    const bool live = l <= PER && g < BLOCKS;
+    const uint32_t col = live ? g * 16 : 0x80000000u;
+    u32x4 x[10], acc = {0, 0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < 10; k++) x[k] = __builtin_amdgcn_raw_buffer_load_b128(ri, 128 + col + sel[k] * (uint32_t)PITCH, 0, 0);
+#pragma unroll
+    for (int k = 0; k < 10; k++) acc ^= x[k];
+    const uint32_t ocol = l >= 1 && live ? g * 16 : 0x80000000u;
+#pragma unroll
+    for (int i = 0; i < 10; i++) __builtin_amdgcn_raw_buffer_store_b128(acc + (uint32_t)i, ro, (uint32_t)(i << 20) + ocol, 0, 0);
+    if (acc.x == 0x9E3779B9u && threadIdx.x == 999) lds[0] = 1;
+}
+
 // encode pattern with line-aligned input runs (the load side of a DPP-realigned encode): each wave
 // loads 57 consecutive 16-byte input granules per piece — lanes 0..56, lanes 57..63 idle — and lanes
 // 0..55 store 56 blocks (7 whole lines) of each of the 16 coded rows (payload-aligned rows). ALIGN
@@ -284,7 +311,7 @@ int main(int argc, char **argv) {
     for (const void *f : {(const void *)dec_k<1, false>, (const void *)dec_k<1, false, 1u << 20>, (const void *)dec_k<1, false, LB, ST_SPLIT>,
                           (const void *)dec_k<1, false, (1u << 20) + 16>,
                           (const void *)dec_k<1, false, LB, ST_A4>, (const void *)dec_lines_k<true>, (const void *)dec_lines_k<false>,
-                          (const void *)enc_lines_k<true>, (const void *)enc_lines_k<false>, (const void *)dec_tile_lines_k, (const void *)enc_k<4, 1, false>, (const void *)enc_k<4, 0, false>, (const void *)enc_k<4, 2, false>,
+                          (const void *)enc_lines_k<true>, (const void *)enc_lines_k<false>, (const void *)dec_tile_lines_k, (const void *)dec_wg248_k, (const void *)enc_k<4, 1, false>, (const void *)enc_k<4, 0, false>, (const void *)enc_k<4, 2, false>,
                           (const void *)enc_k<2, 0, false>, (const void *)enc_k<1, 0, false>, (const void *)enc_k<8, 2, false>})
         CK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, LDS2));
     for (size_t n : {103, 256, 1024}) {
@@ -319,6 +346,8 @@ int main(int argc, char **argv) {
             run("dec_lines56_aligned_3wg", n, db, [&] { dec_lines_k<true><<<gl, 256, LDS3>>>(coded, rep, n); }, a);
             run("dec_lines56_real_3wg", n, db, [&] { dec_lines_k<false><<<gl, 256, LDS3>>>(coded, rep, n); }, a);
             run("dec_lines56_aligned_2wg", n, db, [&] { dec_lines_k<true><<<gl, 256, LDS2>>>(coded, rep, n); }, a);
+            const unsigned gw = (unsigned)(n * ((BLOCKS + 247) / 248));
+            run("dec_wg248_3wg", n, db, [&] { dec_wg248_k<<<gw, 256, LDS3>>>(coded, rep, n); }, a);
             run("dec_tile_lines_3wg", n, db, [&] { dec_tile_lines_k<<<g1, 256, LDS3>>>(coded, rep, n); }, a);
             run("dec_tile_lines_2wg", n, db, [&] { dec_tile_lines_k<<<g1, 256, LDS2>>>(coded, rep, n); }, a);
             run("dec_u1_2wg", n, db, [&] { dec_k<1, false><<<g1, 256, LDS2>>>(coded, rep, n); }, a);
