@@ -200,6 +200,41 @@ __global__ __launch_bounds__(256) void dec_wg248_k(const uint8_t *__restrict__ i
     if (acc.x == 0x9E3779B9u && threadIdx.x == 999) lds[0] = 1;
 }
 
+// decode pattern of a persistent line-aligned walk: each wave owns R consecutive 1-KiB column runs
+// (64 blocks each) and walks them in order; every store instruction is 64 aligned granules = 8 whole
+// lines (the previous block's bytes come from the previous iteration's lane 63 in a real kernel),
+// except at the start of the wave's walk, where lane 0 stores its block at the real offset, and at its
+// end, where lane 63 adds a store of its block at the real offset. The stores only.
+template <uint32_t R>
+__global__ __launch_bounds__(256) void dec_walk_k(const uint8_t *__restrict__ in, uint8_t *__restrict__ out, size_t n) {
+    extern __shared__ uint8_t lds[];
+    constexpr uint32_t PER_WG = 4 * 64 * R, T2 = (BLOCKS + PER_WG - 1) / PER_WG;
+    const uint32_t cs = blockIdx.x / T2, t = blockIdx.x % T2;
+    if (cs >= n) return;
+    constexpr uint32_t sel[10] = {0, 2, 3, 5, 6, 8, 9, 11, 13, 15};
+    const auto ri = rsrc(in + cs * 16 * PITCH);
+    const auto ro = rsrc(out + cs * CSB);
+    const uint32_t l = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    u32x4 acc = {0, 0, 0, 0};
+    for (uint32_t r = 0; r < R; r++) {
+        const uint32_t g = t * PER_WG + w * 64 * R + r * 64 + l;
+        const uint32_t col = g < BLOCKS ? g * 16 : 0x80000000u;
+        u32x4 x[10];
+#pragma unroll
+        for (int k = 0; k < 10; k++) x[k] = __builtin_amdgcn_raw_buffer_load_b128(ri, 128 + col + sel[k] * (uint32_t)PITCH, 0, 0);
+#pragma unroll
+        for (int k = 0; k < 10; k++) acc ^= x[k];
+        const bool head = r == 0 && l == 0;
+#pragma unroll
+        for (int i = 0; i < 10; i++)
+            __builtin_amdgcn_raw_buffer_store_b128(acc + (uint32_t)i, ro, (head ? (uint32_t)(i * LB) : (uint32_t)(i << 20)) + col, 0, 0);
+        if (r == R - 1 && l == 63)
+#pragma unroll
+            for (int i = 0; i < 10; i++) __builtin_amdgcn_raw_buffer_store_b128(acc + (uint32_t)i, ro, (uint32_t)(i * LB) + col, 0, 0);
+    }
+    if (acc.x == 0x9E3779B9u && threadIdx.x == 999) lds[0] = 1;
+}
+
 // encode pattern with line-aligned input runs (the load side of a DPP-realigned encode): each wave
 // loads 57 consecutive 16-byte input granules per piece — lanes 0..56, lanes 57..63 idle — and lanes
 // 0..55 store 56 blocks (7 whole lines) of each of the 16 coded rows (payload-aligned rows). ALIGN
@@ -311,7 +346,8 @@ int main(int argc, char **argv) {
     for (const void *f : {(const void *)dec_k<1, false>, (const void *)dec_k<1, false, 1u << 20>, (const void *)dec_k<1, false, LB, ST_SPLIT>,
                           (const void *)dec_k<1, false, (1u << 20) + 16>,
                           (const void *)dec_k<1, false, LB, ST_A4>, (const void *)dec_lines_k<true>, (const void *)dec_lines_k<false>,
-                          (const void *)enc_lines_k<true>, (const void *)enc_lines_k<false>, (const void *)dec_tile_lines_k, (const void *)dec_wg248_k, (const void *)enc_k<4, 1, false>, (const void *)enc_k<4, 0, false>, (const void *)enc_k<4, 2, false>,
+                          (const void *)enc_lines_k<true>, (const void *)enc_lines_k<false>, (const void *)dec_tile_lines_k, (const void *)dec_wg248_k, (const void *)dec_walk_k<4>, (const void *)dec_walk_k<8>,
+                          (const void *)dec_walk_k<16>, (const void *)enc_k<4, 1, false>, (const void *)enc_k<4, 0, false>, (const void *)enc_k<4, 2, false>,
                           (const void *)enc_k<2, 0, false>, (const void *)enc_k<1, 0, false>, (const void *)enc_k<8, 2, false>})
         CK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, LDS2));
     for (size_t n : {103, 256, 1024}) {
@@ -348,6 +384,9 @@ int main(int argc, char **argv) {
             run("dec_lines56_aligned_2wg", n, db, [&] { dec_lines_k<true><<<gl, 256, LDS2>>>(coded, rep, n); }, a);
             const unsigned gw = (unsigned)(n * ((BLOCKS + 247) / 248));
             run("dec_wg248_3wg", n, db, [&] { dec_wg248_k<<<gw, 256, LDS3>>>(coded, rep, n); }, a);
+            run("dec_walk4_3wg", n, db, [&] { dec_walk_k<4><<<(unsigned)(n * ((BLOCKS + 1023) / 1024)), 256, LDS3>>>(coded, rep, n); }, a);
+            run("dec_walk8_3wg", n, db, [&] { dec_walk_k<8><<<(unsigned)(n * ((BLOCKS + 2047) / 2048)), 256, LDS3>>>(coded, rep, n); }, a);
+            run("dec_walk16_3wg", n, db, [&] { dec_walk_k<16><<<(unsigned)(n * ((BLOCKS + 4095) / 4096)), 256, LDS3>>>(coded, rep, n); }, a);
             run("dec_tile_lines_3wg", n, db, [&] { dec_tile_lines_k<<<g1, 256, LDS3>>>(coded, rep, n); }, a);
             run("dec_tile_lines_2wg", n, db, [&] { dec_tile_lines_k<<<g1, 256, LDS2>>>(coded, rep, n); }, a);
             run("dec_u1_2wg", n, db, [&] { dec_k<1, false><<<g1, 256, LDS2>>>(coded, rep, n); }, a);
