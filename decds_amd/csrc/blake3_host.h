@@ -3,6 +3,8 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include <functional>
+
 namespace decds {
 namespace b3h {
 constexpr size_t MAX_SIMD_SUBTREE = 1024;  // chunks per simd_subtree call (32 KiB of chaining values)
@@ -11,4 +13,8 @@ bool simd_available();                      // AVX2 on this CPU
 // `first`; nchunks a power of two in [8, MAX_SIMD_SUBTREE]; requires simd_available()
 void simd_subtree(const uint8_t *p, size_t nchunks, uint64_t first, uint32_t cv[8]);
 }  // namespace b3h
+// Chunk::digest of a full 1,048,587-byte coded piece on the host pool, side(0 .. side_tasks - 1) (if
+// any) beside it (commit.cpp); requires b3h::simd_available()
+void full_piece_digest(uint64_t chunkset_id, uint64_t chunk_id, const uint8_t *data, uint8_t out[32],
+                       const std::function<void(size_t)> *side, size_t side_tasks);
 }  // namespace decds

@@ -15,6 +15,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <functional>
 #include <mutex>
 #include <random>
 #include <string>
@@ -22,6 +23,7 @@
 #include <vector>
 
 #include "../../include/decds_rlnc.h"
+#include "blake3_host.h"
 #include "capi_internal.h"
 #include "commit_kernels.h"
 #include "rlnc_kernels.h"
@@ -690,20 +692,34 @@ int decds_repairing_blob_add_chunk(decds_repairing_blob *rb, uint64_t chunkset_i
     // BlobHeader::validate_chunk (blob.rs:211-215): blob-level proof at the global chunk id, the
     // chunkset id in range, then the first 4 hashes against the chunkset root (chunk.rs:88-110)
     bool ok = proof && proof_len >= PROOF_SIZE && (data || len == 0);
+    if ((s = decds_ctx_bind(rb->ctx))) return s;
+    // a full-length row is copied into a staging piece while it is hashed (the copy is only sent to
+    // the device if the chunk is accepted); the caller's buffer is free when this returns
+    int piece = -1;
+    uint8_t *staged = nullptr;
     if (ok) {
         uint8_t leaf[32];
-        decds_chunk_digest(chunkset_id, chunk_id, data, len, leaf);
+        if (len == F && b3h::simd_available()) {
+            hipError_t e = rb->in_ring.stage(&piece, &staged);
+            if (e) return decds_hip_error(e, "staging piece");
+            constexpr size_t HALF = (F + 1) / 2;
+            const std::function<void(size_t)> copy = [&](size_t h) {
+                std::memcpy(staged + h * HALF, data + h * HALF, h ? F - HALF : HALF);
+            };
+            full_piece_digest(chunkset_id, chunk_id, data, leaf, &copy, 2);
+        } else {
+            decds_chunk_digest(chunkset_id, chunk_id, data, len, leaf);
+        }
         ok = decds_merkle_verify(chunk_id, leaf, proof, proof_len, rb->root) == 1 &&
              decds_merkle_verify(chunk_id % N, leaf, proof, PROOF_SIZE, &rb->cs_roots[chunkset_id * 32]) == 1;
     }
     if (!ok)
         return decds_set_error(DECDS_ERR_INVALID_PROOF_IN_CHUNK, "invalid proof in chunk of chunkset %llu",
                                (unsigned long long)chunkset_id);
-    if ((s = decds_ctx_bind(rb->ctx))) return s;
     uint32_t row;
     if ((s = rb->accept(chunkset_id, data, len, &row))) return s;
-    // the row goes to its device slot now (staged: the caller's buffer is free when this returns)
-    hipError_t e = rb->in_ring.h2d(rb->slot_rows(rb->cs[chunkset_id].slot) + row * F, data, F, rb->s);
+    uint8_t *dst = rb->slot_rows(rb->cs[chunkset_id].slot) + row * F;
+    hipError_t e = staged ? rb->in_ring.commit(piece, dst, F, rb->s) : rb->in_ring.h2d(dst, data, F, rb->s);
     return e ? decds_hip_error(e, "H2D (accepted row)") : DECDS_OK;
 }
 

@@ -2,6 +2,7 @@
 // chunkset Merkle roots and proofs) and host helpers for the blob-level tree (blob.rs:266-273),
 // which covers only the 32-byte chunkset roots.
 #include <cstring>
+#include <functional>
 #include <thread>
 #include <vector>
 
@@ -10,6 +11,7 @@
 #include "blake3_impl.h"
 #include "capi_internal.h"
 #include "commit_kernels.h"
+#include "host_mem.h"
 #include "rlnc_kernels.h"
 #include "rlnc_layout.h"
 
@@ -95,6 +97,46 @@ void hash_pair(const uint8_t *l, const uint8_t *r, uint8_t out[32]) {
 
 }  // namespace
 
+namespace decds {
+// Chunk::digest of a full coded piece (chunk.rs:40-46) without copying it: message chunk c >= 8 is
+// data[1024c - 16, 1024c + 1008), so chunks 8..1023 are hashed in place as complete subtrees; chunks
+// 0..7 (the ids' chunk) from an 8 KiB copy; the 27-byte 1025th chunk joins the 1024-chunk left tree
+// under ROOT. Four quarters (0-255, 256-511, 512-767, 768-1023) run on the host pool; side(0 ..
+// side_tasks - 1), if any, run beside them (RepairingBlob::add_chunk stages the piece for its H2D copy).
+void full_piece_digest(uint64_t chunkset_id, uint64_t chunk_id, const uint8_t *data, uint8_t out[32],
+                       const std::function<void(size_t)> *side, size_t side_tasks) {
+    auto at = [&](size_t c) { return data + c * b3::CHUNK - 16; };
+    uint32_t q[4][8];
+    host_parallel(4 + (side ? side_tasks : 0), [&](size_t task) {
+        if (task >= 4) {
+            (*side)(task - 4);
+        } else if (task == 0) {
+            alignas(64) uint8_t head[8 * b3::CHUNK];
+            for (int b = 0; b < 8; b++) {
+                head[b] = (uint8_t)(chunkset_id >> (8 * b));
+                head[8 + b] = (uint8_t)(chunk_id >> (8 * b));
+            }
+            std::memcpy(head + 16, data, sizeof(head) - 16);
+            uint32_t sub[8];
+            b3h::simd_subtree(head, 8, 0, q[0]);
+            for (size_t k = 8; k < 256; k *= 2) {
+                b3h::simd_subtree(at(k), k, k, sub);
+                b3::parent(q[0], sub, 0, q[0]);
+            }
+        } else {
+            b3h::simd_subtree(at(256 * task), 256, 256 * task, q[task]);
+        }
+    });
+    uint32_t lo[8], hi[8], left[8], last[8], root[8];
+    b3::parent(q[0], q[1], 0, lo);
+    b3::parent(q[2], q[3], 0, hi);
+    b3::parent(lo, hi, 0, left);
+    chunk_cv(at(1024), F + 16 - 1024 * b3::CHUNK, 1024, false, last);
+    b3::parent(left, last, b3::ROOT, root);
+    to_bytes(root, out);
+}
+}  // namespace decds
+
 extern "C" {
 
 void decds_blake3(const uint8_t *data, size_t len, uint8_t out[32]) {
@@ -110,6 +152,10 @@ void decds_blake3_parallel(const uint8_t *data, size_t len, uint8_t out[32], int
 }
 
 void decds_chunk_digest(uint64_t chunkset_id, uint64_t chunk_id, const uint8_t *data, size_t len, uint8_t out[32]) {
+    if (len == F && b3h::simd_available()) {
+        full_piece_digest(chunkset_id, chunk_id, data, out, nullptr, 0);
+        return;
+    }
     std::vector<uint8_t> msg(16 + len);
     for (int b = 0; b < 8; b++) {
         msg[b] = (uint8_t)(chunkset_id >> (8 * b));

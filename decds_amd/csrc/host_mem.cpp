@@ -229,6 +229,25 @@ hipError_t BounceRing::h2d(uint8_t *ddst, const uint8_t *hsrc, size_t n, hipStre
     return hipSuccess;
 }
 
+hipError_t BounceRing::stage(int *idx, uint8_t **piece) {
+    hipError_t e;
+    if ((e = init())) return e;
+    const int i = next;
+    next = (next + 1) % R;
+    if ((e = settle(i))) return e;
+    *idx = i;
+    *piece = buf[i];
+    return hipSuccess;
+}
+
+hipError_t BounceRing::commit(int i, uint8_t *ddst, size_t n, hipStream_t s) {
+    hipError_t e;
+    if (n > PIECE) return hipErrorInvalidValue;
+    if ((e = hipMemcpyAsync(ddst, buf[i], n, hipMemcpyHostToDevice, s)) || (e = hipEventRecord(ev[i], s))) return e;
+    used[i] = true;
+    return hipSuccess;
+}
+
 hipError_t BounceRing::d2h(uint8_t *hdst, const uint8_t *dsrc, size_t n, hipStream_t s) {
     hipError_t e;
     if ((e = init())) return e;

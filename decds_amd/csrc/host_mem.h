@@ -67,6 +67,11 @@ struct BounceRing {
     hipError_t d2h(uint8_t *hdst, const uint8_t *dsrc, size_t n, hipStream_t s);
     hipError_t flush();
     void abandon();  // after a failed call: wait for the pieces' copies, drop pending copy-outs
+    // h2d in two steps, so the host fill of a piece can overlap other host work: stage() settles the
+    // next piece and returns it (*idx), commit() queues its copy to the device; an uncommitted piece is
+    // simply reused later
+    hipError_t stage(int *idx, uint8_t **piece);
+    hipError_t commit(int idx, uint8_t *ddst, size_t n, hipStream_t s);
     ~BounceRing();
 
    private:
