@@ -52,18 +52,6 @@ constexpr uint32_t DEC_UNIT = DECDS_DEC_UNIT;
 // non-persistent units of 4 tiles per XCD eighth, r02r; that form is in git history, rlnc_kernels.hip
 // at 227db28); the decode runs non-persistent workgroups of one tile.
 
-// ---- GF(2^8) ----------------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t gf_mul(uint32_t a, uint32_t b, uint32_t poly) {
-    uint32_t acc = 0;
-#pragma unroll
-    for (int i = 0; i < 8; i++) {
-        acc ^= ((b >> i) & 1u) ? a : 0u;
-        a <<= 1;
-        a ^= (a & 0x100u) ? poly : 0u;
-    }
-    return acc & 0xFFu;
-}
-
 // A wave-uniform 64-bit value in SGPRs. __builtin_amdgcn_readfirstlane returns int: each half goes
 // back through uint32_t, or a low half with bit 31 set would sign-extend into the high half (an
 // address above 2 GiB within its 4 GiB window became 0xFFFFFFFF'xxxxxxxx: GPUTEST r02i).
@@ -743,106 +731,113 @@ void rlnc_decode_kernel(const uint8_t *__restrict__ coded, size_t pitch, size_t 
 // all reductions of one step are independent (ILP across the basis instead of a serial chain).
 // At rank 10 the coefficient parts are unit vectors e_piv, so B = E·R = P and R^-1 = Pᵀ·E: row i
 // of the inverse is the combination part of the basis row whose pivot is column i.
-// Products use log / exp tables of the generator `gen` in LDS: x * f = exp[log x + log f] — one
-// table read per product, and the products of one step are independent reads.
+// Products are log-domain: x * f = exp[log x + log f], with log 0 = PLAN_LOG0 and exp zero from
+// index 510 on, so a product with a zero factor reads a zero and no term needs a mask. The basis
+// is kept with its logs and every candidate's log is read up front, so a step is four dependent
+// LDS reads (projection, log of the reduced row, normalised row + basis update, basis logs); the
+// exp table comes from the host as a kernel argument.
+struct GfExpTable {
+    uint32_t w[64];  // byte i = gen^i (i < 255), byte 255 = 0
+};
+constexpr uint32_t PLAN_LOG0 = 512;
+constexpr uint32_t PLAN_EXP_BYTES = 2 * PLAN_LOG0 + 4;  // largest index: log0 + log0
 __global__ __launch_bounds__(64) void rlnc_plan_kernel(const uint8_t *__restrict__ coded, size_t pitch, size_t n,
                                                        const uint8_t *__restrict__ cand,
                                                        RepairPlan *__restrict__ plan,
                                                        int8_t *__restrict__ verdicts,
-                                                       int32_t *__restrict__ status, uint32_t poly,
-                                                       uint32_t gen) {
+                                                       int32_t *__restrict__ status, GfExpTable tab) {
     const size_t cs = blockIdx.x;
     const uint32_t lane = threadIdx.x;
     const bool col = lane < K;
-    // the arrival order, and the 10-byte coding vector of every coded row of the chunkset (lane
-    // c < 10 loads byte c of rows 0..15): both in flight while the tables below are built
+    // the arrival order and the coding vector of every coded row of the chunkset (lane c < 10
+    // loads byte c of rows 0..15): all in flight while the tables below are built
     const uint32_t my_cand = lane < N ? cand[cs * N + lane] : (uint32_t)DECDS_NO_CANDIDATE_U8;
     uint32_t rowcv[N];
 #pragma unroll
     for (int r = 0; r < (int)N; r++) rowcv[r] = col ? coded[(cs * N + r) * pitch + lane] : 0u;
-    // exp[i] = gen^i for i < 510 (doubled: exp[log a + log b] needs no reduction mod 255),
-    // log[gen^i] = i. Lane l starts at gen^(4l) (square-and-multiply) and steps 4 times.
-    __shared__ uint8_t s_exp[512], s_log[256], s_cv[N * 16];
+    __shared__ __attribute__((aligned(16))) uint8_t s_exp[PLAN_EXP_BYTES];
+    __shared__ uint16_t s_log[256];
+    __shared__ uint16_t s_lcv[N * 16];  // log of byte c of row r's coding vector at r * 16 + c
     {
-        uint32_t v = 1, b = gen;
-#pragma unroll
-        for (int k = 0; k < 8; k++) {
-            if ((4 * lane >> k) & 1u) v = gf_mul(v, b, poly);
-            b = gf_mul(b, b, poly);
-        }
+        // exp[i] = gen^i for i < 510 (doubled: a sum of two logs needs no reduction), zeros after
+        const uint32_t e4 = tab.w[lane];  // exp[4 lane .. 4 lane + 3]
 #pragma unroll
         for (uint32_t q = 0; q < 4; q++) {
-            const uint32_t i = 4 * lane + q;
+            const uint32_t i = 4 * lane + q, v = (e4 >> (8 * q)) & 0xFFu;
             if (i < 255) {
                 s_exp[i] = (uint8_t)v;
                 s_exp[i + 255] = (uint8_t)v;
-                s_log[v] = (uint8_t)i;
+                s_log[v] = (uint16_t)i;
             }
-            v = gf_mul(v, gen, poly);
         }
-        if (lane == 0) s_log[0] = 0;  // log 0 is never used unmasked; keep the reads defined
-    }
-    if (col) {
-#pragma unroll
-        for (int r = 0; r < (int)N; r++) s_cv[r * 16 + lane] = (uint8_t)rowcv[r];
+        for (uint32_t w = 512 / 4 + lane; w < PLAN_EXP_BYTES / 4; w += 64) reinterpret_cast<uint32_t *>(s_exp)[w] = 0;
+        if (lane < 2) s_exp[510 + lane] = 0;
+        if (lane == 0) s_log[0] = PLAN_LOG0;
     }
     __syncthreads();
-    // Every term below is computed unconditionally and masked by selects: no branch splits the
-    // ten independent table reads of a step, so they are all in flight together.
-    uint32_t basis[K], lgb[K], piv[K], sel[K];  // lgb[e] = log basis[e] (masked where basis[e] == 0)
+    if (col) {
 #pragma unroll
-    for (int e = 0; e < (int)K; e++) basis[e] = lgb[e] = piv[e] = sel[e] = 0;
-    uint32_t rank = 0;
-    bool ended = false;
-    int32_t my_verdict = -1;  // lane a < 16 keeps candidate a's verdict
+        for (int r = 0; r < (int)N; r++) s_lcv[r * 16 + lane] = s_log[rowcv[r]];
+    }
+    __syncthreads();
+    // Basis slot k is filled by the k-th accepted candidate, so the slot loop is unrolled with k a
+    // constant: step k reduces against k basis rows only, and the pivots stay in SGPRs. Candidates
+    // are taken in arrival order by a uniform inner loop until one raises the rank.
+    uint32_t basis[K], lgb[K], piv[K], sel[K];  // lgb[e] = log basis[e] (PLAN_LOG0 where 0)
+    uint32_t a = 0, rank = 0;                     // next candidate; rank = accepted so far
+    bool stop = false;                            // the arrival list ended (no candidate / id >= 16)
+    int32_t my_verdict = -1;                      // lane a < 16 keeps candidate a's verdict
 #pragma unroll
-    for (uint32_t a = 0; a < N; a++) {
-        const uint32_t r = __builtin_amdgcn_readlane(my_cand, a);
-        int32_t v;
-        if (ended || r >= N) {
-            ended = true;
-            v = -1;
-        } else if (rank == K) {
-            v = 3;  // DECDS_ERR_CHUNKSET_READY_TO_REPAIR
-        } else {
-            const uint32_t cv = col ? s_cv[r * 16 + lane] : 0u;
-            // augmented row [cv | unit(rank)] minus its projection on the basis
-            uint32_t row = col ? cv : (lane == K + rank ? 1u : 0u);
-#pragma unroll
-            for (int e = 0; e < (int)K; e++) {
-                const uint32_t f = e < (int)rank ? __builtin_amdgcn_readlane(cv, piv[e]) : 0u;
-                const uint32_t t = s_exp[lgb[e] + s_log[f]];
-                row ^= (f != 0 && basis[e] != 0) ? t : 0u;
+    for (int k = 0; k < (int)K; k++) {
+        basis[k] = 0;
+        lgb[k] = PLAN_LOG0;
+        piv[k] = sel[k] = 0;
+        if (stop || rank < (uint32_t)k) continue;
+        while (true) {
+            const uint32_t r = a < N ? __builtin_amdgcn_readlane(my_cand, a) : N;
+            if (r >= N) {
+                stop = true;
+                break;
             }
+            const uint32_t lcv = col ? (uint32_t)s_lcv[r * 16 + lane] : PLAN_LOG0;
+            // augmented row [cv | unit(k)] minus its projection on the basis: the factor of basis row
+            // e is the row's entry at pivot e
+            uint32_t row = col ? (uint32_t)s_exp[lcv] : (lane == K + k ? 1u : 0u);
+#pragma unroll
+            for (int e = 0; e < k; e++) row ^= s_exp[lgb[e] + __builtin_amdgcn_readlane(lcv, piv[e])];
             const uint64_t nz = __ballot(col && row != 0);
             if (!nz) {
-                v = 4;  // DECDS_ERR_CHUNK_DECODING_FAILED: piece not useful
-            } else {
-                const uint32_t p = __builtin_ctzll(nz);
-                // row /= row[p]: log of the inverse = 255 - log (exp is doubled, so 255 is fine)
-                const uint32_t linv = 255u - s_log[__builtin_amdgcn_readlane(row, p)];
-                row = row ? s_exp[s_log[row] + linv] : 0u;
-                const uint32_t lrow = s_log[row];
-#pragma unroll
-                for (int e = 0; e < (int)K; e++) {
-                    const uint32_t f = e < (int)rank ? __builtin_amdgcn_readlane(basis[e], p) : 0u;
-                    const uint32_t t = s_exp[lrow + s_log[f]];
-                    basis[e] ^= (f != 0 && row != 0) ? t : 0u;
-                }
-#pragma unroll
-                for (int e = 0; e < (int)K; e++) {
-                    if (e == (int)rank) {
-                        basis[e] = row;
-                        piv[e] = p;
-                        sel[e] = r;
-                    }
-                    lgb[e] = s_log[basis[e]];
-                }
-                rank++;
-                v = 0;
+                if (lane == a) my_verdict = 4;  // DECDS_ERR_CHUNK_DECODING_FAILED: piece not useful
+                a++;
+                continue;
             }
+            const uint32_t p = __builtin_ctzll(nz);
+            // row /= row[p] in logs: lrow = log row - log row[p] (mod 255), log0 kept
+            const uint32_t lrow0 = s_log[row];
+            const uint32_t linv = 255u - __builtin_amdgcn_readlane(lrow0, p);
+            const uint32_t ls = lrow0 + linv;
+            const uint32_t lrow = lrow0 >= PLAN_LOG0 ? PLAN_LOG0 : (ls >= 255u ? ls - 255u : ls);
+            // clear column p from the basis: basis[e] -= basis[e][p] * row
+#pragma unroll
+            for (int e = 0; e < k; e++) basis[e] ^= s_exp[lrow + __builtin_amdgcn_readlane(lgb[e], p)];
+#pragma unroll
+            for (int e = 0; e < k; e++) lgb[e] = s_log[basis[e]];
+            basis[k] = s_exp[lrow];
+            lgb[k] = lrow;
+            piv[k] = p;
+            sel[k] = r;
+            if (lane == a) my_verdict = 0;
+            a++;
+            rank++;
+            break;
         }
-        if (lane == a) my_verdict = v;
+    }
+    // after rank 10 every further candidate is "ready to repair", up to the end of the list
+    if (rank == K) {
+        while (a < N && __builtin_amdgcn_readlane(my_cand, a) < N) {
+            if (lane == a) my_verdict = 3;  // DECDS_ERR_CHUNKSET_READY_TO_REPAIR
+            a++;
+        }
     }
     if (lane < N) verdicts[cs * N + lane] = (int8_t)my_verdict;
     RepairPlan *pl = plan + cs;
@@ -982,8 +977,26 @@ hipError_t launch_encode_commit(const uint8_t *src, size_t n, const uint8_t *coe
 hipError_t launch_repair_plan(const uint8_t *coded, size_t pitch, size_t n, const uint8_t *cand, uint8_t *plan,
                               int8_t *verdicts, int32_t *status, uint32_t poly, uint32_t gen, hipStream_t stream) {
     if (n == 0) return hipSuccess;
+    // exp table of gen, kept for the last (poly, gen) asked for
+    static thread_local uint32_t last_poly = 0, last_gen = 0;
+    static thread_local GfExpTable tab;
+    if (poly != last_poly || gen != last_gen) {
+        uint32_t v = 1;
+        for (uint32_t i = 0; i < 256; i++) {
+            if (i % 4 == 0) tab.w[i / 4] = 0;
+            tab.w[i / 4] |= (i < 255 ? v : 0u) << (8 * (i % 4));
+            uint32_t acc = 0, a = v;  // v *= gen
+            for (int b = 0; b < 8; b++) {
+                acc ^= ((gen >> b) & 1u) ? a : 0u;
+                a = (a << 1) ^ ((a & 0x80u) ? (poly & 0x1FFu) : 0u);
+            }
+            v = acc & 0xFFu;
+        }
+        last_poly = poly;
+        last_gen = gen;
+    }
     hipLaunchKernelGGL(rlnc_plan_kernel, dim3((uint32_t)n), dim3(64), 0, stream, coded, pitch, n, cand,
-                       reinterpret_cast<RepairPlan *>(plan), verdicts, status, poly, gen);
+                       reinterpret_cast<RepairPlan *>(plan), verdicts, status, tab);
     return hipGetLastError();
 }
 

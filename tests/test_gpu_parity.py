@@ -200,6 +200,61 @@ def test_repair_batch_roundtrip_dependent_and_not_ready(ctx):
     assert NOT_USEFUL in list(v[1]) and NOT_USEFUL in list(v[2])
 
 
+def test_repair_plan_fuzz_low_rank_and_repeats(ctx):
+    """The plan kernel alone (chunkset.rs:173-184 replayed per candidate) on 96 chunksets of
+    rank-deficient coding vectors: rows drawn from random subspaces of rank 1..10, zero and repeated
+    rows, candidate lists of every length with repeated ids. Verdicts, rank and status must equal the
+    oracle decoder's; at rank 10 sel must be the accepted rows in order and inv their inverse."""
+    n = 96
+    rng = np.random.default_rng(0x91A7)
+    coded = torch.zeros(n * N * F, dtype=torch.uint8, device="cuda")
+    vecs = np.zeros((n, N, K), np.uint8)
+    cand = np.full((n, N), 0xFF, np.uint8)
+    for c in range(n):
+        r = 10 if c % 4 == 0 else int(rng.integers(1, K + 1))
+        basis = rng.integers(0, 256, (r, K), dtype=np.uint8)
+        for j in range(N):
+            w = rng.integers(0, 256, r)
+            v = np.zeros(K, np.uint8)
+            for i in range(r):
+                v ^= np.array([o.gf_mul(int(w[i]), int(x)) for x in basis[i]], np.uint8)
+            vecs[c, j] = v
+        if c % 7 == 3:
+            vecs[c, 5] = 0
+        length = int(rng.integers(0, N + 1)) if c % 3 else N
+        ids = rng.integers(0, N, length) if c % 2 else rng.permutation(N)[:length]
+        cand[c, :length] = ids
+    host_rows = np.zeros((n * N, 16), np.uint8)
+    host_rows[:, :K] = vecs.reshape(n * N, K)
+    coded.view(n * N, F)[:, :16].copy_(dev(host_rows))
+    plan = torch.empty(n * 128, dtype=torch.uint8, device="cuda")
+    verd = torch.empty(n * N, dtype=torch.int8, device="cuda")
+    status = torch.full((n,), -7, dtype=torch.int32, device="cuda")
+    codec.repair_plan_batch(ctx, coded, n, dev(cand), plan, verd, status)
+    st, v, pl = host(status), host(verd).reshape(n, N), host(plan).reshape(n, 128)
+    ranks = set()
+    for c in range(n):
+        ov, rank = _oracle_verdicts(vecs[c], cand[c])
+        assert list(v[c]) == ov, (c, list(v[c]), ov)
+        assert pl[c, 10] == rank, c
+        ranks.add(rank)
+        if rank < K:
+            assert st[c] == 5, c
+            continue
+        assert st[c] == 0, c
+        acc = [int(cand[c, a]) for a in range(N) if ov[a] == OKV]
+        assert list(pl[c, :K]) == acc, c
+        inv = pl[c, 16:16 + K * K].reshape(K, K)
+        m = vecs[c, acc]
+        for i in range(K):
+            for j in range(K):
+                s = 0
+                for k in range(K):
+                    s ^= o.gf_mul(int(inv[i, k]), int(m[k, j]))
+                assert s == (1 if i == j else 0), (c, i, j)
+    assert len(ranks) >= 8  # the draws cover most ranks
+
+
 def test_decode_tail_corruption_is_repairing_failed(ctx):
     data = o.fill_random(41, CS)
     coeffs = o.fill_random(42, N * K)
