@@ -47,6 +47,10 @@ constexpr uint32_t SWEEP_LDS = 2 * LDS_BYTES + 16;             // two table buff
 #define DECDS_PREFETCH_FIRST 1  // 1: a decode workgroup's first tile loads are issued before its table build
 #endif
 constexpr uint32_t DEC_UNIT = DECDS_DEC_UNIT;
+#ifndef DECDS_DEC_XCD_RUN
+#define DECDS_DEC_XCD_RUN 8  // decode: consecutive tiles per XCD (1 = plain dispatch order)
+#endif
+constexpr uint32_t DEC_XCD_RUN = DECDS_DEC_XCD_RUN;
 // The shipped work splits: the encode is one persistent sweep fed by a tile
 // counter for every batch (0.69-0.73 of 8 TB/s at 103-1639 chunksets against 0.64-0.66 for round 2's
 // non-persistent units of 4 tiles per XCD eighth, r02r; that form is in git history, rlnc_kernels.hip
@@ -670,7 +674,17 @@ void rlnc_decode_kernel(const uint8_t *__restrict__ coded, size_t pitch, size_t 
     constexpr uint32_t T = TILES<DW>;
     static_assert(T % UNIT == 0, "a workgroup's tiles stay in one chunkset");
     constexpr uint32_t phase = 0;  // aligned decode loads measured slower (+3…+5 %)
-    const uint32_t t0 = blockIdx.x * UNIT, cs = t0 / T, tile0 = t0 % T;
+    // Workgroups are dealt round-robin over the 8 XCDs. Piece i's stores start i bytes past a line
+    // boundary, so the line at every tile edge is written partly by each of two workgroups; when those
+    // sit on different XCDs both L2s write back a partial line. Runs of R consecutive tiles go to one
+    // XCD instead (block 8R·g + 8j + x -> tile 8R·g + R·x + j), global order otherwise: only every R-th
+    // tile edge crosses an L2 (-3 % decode time).
+    uint32_t u = blockIdx.x;
+    if constexpr (DEC_XCD_RUN > 1) {
+        constexpr uint32_t R = DEC_XCD_RUN;
+        if (gridDim.x % (8 * R) == 0) u = (u / (8 * R)) * 8 * R + (u % 8) * R + (u / 8) % R;
+    }
+    const uint32_t t0 = u * UNIT, cs = t0 / T, tile0 = t0 % T;
     if (cs >= n) return;
     const uint32_t *pw = reinterpret_cast<const uint32_t *>(plan + cs);
     const uint32_t w0 = __builtin_amdgcn_readfirstlane(pw[0]);

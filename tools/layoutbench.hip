@@ -40,13 +40,20 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void *p) {
 
 // workgroup -> unit: ORDER 0 dispatcher order, 1 each XCD sweeps one contiguous eighth, 2 dispatcher
 // order with a unit's tiles strided (tile r + k * 256/UNIT of its chunkset: the resident workgroups
-// sweep every chunkset's rows together)
+// sweep every chunkset's rows together), ORDER = 100 + R: runs of R consecutive units per XCD in
+// global order (blocks b = 8R·grp + 8j + x -> unit 8R·grp + R·x + j; the grid a multiple of 8R), so a
+// unit's neighbours share its XCD's L2 except at every R-th edge
 template <int ORDER>
 __device__ __forceinline__ uint32_t unit_of() {
     uint32_t u = blockIdx.x;
     if constexpr (ORDER == 1) {
         const uint32_t g = gridDim.x, x = u % 8, q = u / 8, per = g / 8, rem = g % 8;
         u = x * per + (x < rem ? x : rem) + q;
+    }
+    if constexpr (ORDER > 100) {
+        constexpr uint32_t R = ORDER - 100;
+        const uint32_t x = u % 8, q = u / 8;
+        u = (q / R) * 8 * R + x * R + q % R;
     }
     return u;
 }
@@ -116,10 +123,10 @@ __device__ __forceinline__ void piece_store(u32x4 v, __amdgpu_buffer_rsrc_t ro, 
     }
 }
 
-template <int UNIT, bool TM, uint64_t OROW = LB, int ST = ST_PLAIN>
+template <int UNIT, bool TM, uint64_t OROW = LB, int ST = ST_PLAIN, int ORDER = 0>
 __global__ __launch_bounds__(256) void dec_k(const uint8_t *__restrict__ in, uint8_t *__restrict__ out, size_t n) {
     extern __shared__ uint8_t lds[];
-    const uint32_t t0 = blockIdx.x * UNIT, cs = t0 / TILES, tile0 = t0 % TILES;
+    const uint32_t t0 = unit_of<ORDER>() * UNIT, cs = t0 / TILES, tile0 = t0 % TILES;
     if (cs >= n) return;
     constexpr uint32_t sel[10] = {0, 2, 3, 5, 6, 8, 9, 11, 13, 15};
     const auto ri = rsrc(in + cs * (TM ? TM_CS : 16 * PITCH));
@@ -147,9 +154,10 @@ __global__ __launch_bounds__(256) void dec_k(const uint8_t *__restrict__ in, uin
 // exchange in the real kernel). At tile edges the granule reaches into the previous tile, so the
 // tile's first lane stores its block at the real (misaligned) offset instead and the tile's last lane
 // adds a misaligned store of its own block. The stores only, no arithmetic.
+template <int ORDER = 0>
 __global__ __launch_bounds__(256) void dec_tile_lines_k(const uint8_t *__restrict__ in, uint8_t *__restrict__ out, size_t n) {
     extern __shared__ uint8_t lds[];
-    const uint32_t cs = blockIdx.x / TILES, t = blockIdx.x % TILES;
+    const uint32_t u = unit_of<ORDER>(), cs = u / TILES, t = u % TILES;
     if (cs >= n) return;
     constexpr uint32_t sel[10] = {0, 2, 3, 5, 6, 8, 9, 11, 13, 15};
     const auto ri = rsrc(in + cs * 16 * PITCH);
@@ -346,7 +354,9 @@ int main(int argc, char **argv) {
     for (const void *f : {(const void *)dec_k<1, false>, (const void *)dec_k<1, false, 1u << 20>, (const void *)dec_k<1, false, LB, ST_SPLIT>,
                           (const void *)dec_k<1, false, (1u << 20) + 16>,
                           (const void *)dec_k<1, false, LB, ST_A4>, (const void *)dec_lines_k<true>, (const void *)dec_lines_k<false>,
-                          (const void *)enc_lines_k<true>, (const void *)enc_lines_k<false>, (const void *)dec_tile_lines_k, (const void *)dec_wg248_k, (const void *)dec_walk_k<4>, (const void *)dec_walk_k<8>,
+                          (const void *)enc_lines_k<true>, (const void *)enc_lines_k<false>, (const void *)dec_tile_lines_k<0>, (const void *)dec_tile_lines_k<104>, (const void *)dec_tile_lines_k<108>, (const void *)dec_tile_lines_k<116>,
+                          (const void *)dec_k<1, false, LB, ST_PLAIN, 104>, (const void *)dec_k<1, false, LB, ST_PLAIN, 108>, (const void *)dec_k<1, false, LB, ST_PLAIN, 116>, (const void *)dec_k<1, false, 1u << 20, ST_PLAIN, 108>,
+                          (const void *)enc_k<1, 108, false>, (const void *)dec_wg248_k, (const void *)dec_walk_k<4>, (const void *)dec_walk_k<8>,
                           (const void *)dec_walk_k<16>, (const void *)enc_k<4, 1, false>, (const void *)enc_k<4, 0, false>, (const void *)enc_k<4, 2, false>,
                           (const void *)enc_k<2, 0, false>, (const void *)enc_k<1, 0, false>, (const void *)enc_k<8, 2, false>})
         CK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, LDS2));
@@ -374,6 +384,24 @@ int main(int argc, char **argv) {
             }, a);
             continue;
         }
+        if (only == "xcdgrp") {
+            // tile edges on one XCD: do partial lines written from two XCDs' L2s cost the misaligned
+            // decode stores? runs of R consecutive tiles per XCD, global order otherwise
+            constexpr uint32_t LDS3 = 52 * 1024;
+            run("dec_u1_3wg", n, db, [&] { dec_k<1, false><<<g1, 256, LDS3>>>(coded, rep, n); }, a);
+            run("dec_u1_grp4_3wg", n, db, [&] { dec_k<1, false, LB, ST_PLAIN, 104><<<g1, 256, LDS3>>>(coded, rep, n); }, a);
+            run("dec_u1_grp8_3wg", n, db, [&] { dec_k<1, false, LB, ST_PLAIN, 108><<<g1, 256, LDS3>>>(coded, rep, n); }, a);
+            run("dec_u1_grp16_3wg", n, db, [&] { dec_k<1, false, LB, ST_PLAIN, 116><<<g1, 256, LDS3>>>(coded, rep, n); }, a);
+            run("dec_u1_outA_3wg", n, db, [&] { dec_k<1, false, 1u << 20><<<g1, 256, LDS3>>>(coded, rep, n); }, a);
+            run("dec_u1_outA_grp8_3wg", n, db, [&] { dec_k<1, false, 1u << 20, ST_PLAIN, 108><<<g1, 256, LDS3>>>(coded, rep, n); }, a);
+            run("dec_tile_lines_3wg", n, db, [&] { dec_tile_lines_k<0><<<g1, 256, LDS3>>>(coded, rep, n); }, a);
+            run("dec_tile_lines_grp4_3wg", n, db, [&] { dec_tile_lines_k<104><<<g1, 256, LDS3>>>(coded, rep, n); }, a);
+            run("dec_tile_lines_grp8_3wg", n, db, [&] { dec_tile_lines_k<108><<<g1, 256, LDS3>>>(coded, rep, n); }, a);
+            run("dec_tile_lines_grp16_3wg", n, db, [&] { dec_tile_lines_k<116><<<g1, 256, LDS3>>>(coded, rep, n); }, a);
+            run("enc_u1_disp_2wg", n, eb, [&] { enc_k<1, 0, false><<<g1, 256, LDS2>>>(src, coded, n); }, a);
+            run("enc_u1_grp8_2wg", n, eb, [&] { enc_k<1, 108, false><<<g1, 256, LDS2>>>(src, coded, n); }, a);
+            continue;
+        }
         if (only == "declines") {
             constexpr uint32_t LDS3 = 52 * 1024;
             const unsigned gl = (unsigned)(n * ((BLOCKS + 223) / 224));
@@ -387,8 +415,8 @@ int main(int argc, char **argv) {
             run("dec_walk4_3wg", n, db, [&] { dec_walk_k<4><<<(unsigned)(n * ((BLOCKS + 1023) / 1024)), 256, LDS3>>>(coded, rep, n); }, a);
             run("dec_walk8_3wg", n, db, [&] { dec_walk_k<8><<<(unsigned)(n * ((BLOCKS + 2047) / 2048)), 256, LDS3>>>(coded, rep, n); }, a);
             run("dec_walk16_3wg", n, db, [&] { dec_walk_k<16><<<(unsigned)(n * ((BLOCKS + 4095) / 4096)), 256, LDS3>>>(coded, rep, n); }, a);
-            run("dec_tile_lines_3wg", n, db, [&] { dec_tile_lines_k<<<g1, 256, LDS3>>>(coded, rep, n); }, a);
-            run("dec_tile_lines_2wg", n, db, [&] { dec_tile_lines_k<<<g1, 256, LDS2>>>(coded, rep, n); }, a);
+            run("dec_tile_lines_3wg", n, db, [&] { dec_tile_lines_k<0><<<g1, 256, LDS3>>>(coded, rep, n); }, a);
+            run("dec_tile_lines_2wg", n, db, [&] { dec_tile_lines_k<0><<<g1, 256, LDS2>>>(coded, rep, n); }, a);
             run("dec_u1_2wg", n, db, [&] { dec_k<1, false><<<g1, 256, LDS2>>>(coded, rep, n); }, a);
             continue;
         }
