@@ -50,6 +50,9 @@ def parse():
     p.add_argument("--no-sweep", action="store_true", help="skip the encode batch sweep (256..1639 chunksets)")
     p.add_argument("--cpu-sample", type=int, default=0, help="chunksets in the CPU sample (0 = auto)")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
+    p.add_argument("--rehearse-shard", default=None, metavar="R/W",
+                   help="one process, no process group: run only rank R's shard of a W-GPU job on this GPU "
+                        "(cfg5, the 128 GiB blob over 8 GPUs, is --config cfg3 --rehearse-shard R/8)")
     p.add_argument("--packed", action="store_true",
                    help="coded rows packed at pitch 1,048,587 instead of the recommended 128-B-aligned layout")
     return p.parse_args()
@@ -121,13 +124,22 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit("--gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
+    rehearse = None
+    if args.rehearse_shard:
+        if world != 1:
+            raise SystemExit("--rehearse-shard runs in a single process")
+        rank, world = (int(v) for v in args.rehearse_shard.split("/"))
+        if not 0 <= rank < world:
+            raise SystemExit("--rehearse-shard R/W needs 0 <= R < W")
+        rehearse = {"rank": rank, "world": world}
+    dist_on = world > 1 and rehearse is None
     # DECDS_BENCH_BACKEND=gloo is a rehearsal mode for the N > 1 path on a box with fewer GPUs than
     # ranks (ranks share devices round-robin, timing reduced over gloo); the real runs use RCCL.
     backend = os.environ.get("DECDS_BENCH_BACKEND", "nccl")
     if backend == "gloo":
         local = local % torch.cuda.device_count()
     torch.cuda.set_device(local)
-    if world > 1:
+    if dist_on:
         if backend == "gloo":
             dist.init_process_group("gloo")
         else:
@@ -187,7 +199,7 @@ def main():
         settle_steps += 10
         stream.synchronize()
     events = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
-    if world > 1:
+    if dist_on:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -196,7 +208,7 @@ def main():
     stream.synchronize()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    if world > 1:
+    if dist_on:
         dist.barrier()
         t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if backend == "gloo" else dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -305,18 +317,19 @@ def main():
     # value: blob bytes encoded plus blob bytes repaired (only the chunksets that were ready; the
     # decode kernel skips the rest), halved — encode+repair GiB/s of blob, whole job
     rep_len = sum(min(CS, blob_len_rank - c * CS) for c in np.nonzero(st == 0)[0].tolist())
-    if world > 1:
+    if dist_on:
         rt = torch.tensor([float(rep_len)], dtype=torch.float64, device="cpu" if backend == "gloo" else dev)
         dist.all_reduce(rt, op=dist.ReduceOp.SUM)
         rep_total = float(rt.item())
     else:
         rep_total = float(rep_len)
-    if rank == 0:
-        enc_total = float(blob_per_gpu * world)
+    if rank == 0 or rehearse:
+        # whole-job blob bytes (a rehearsal: this shard's bytes only)
+        enc_total = float(blob_len_rank if rehearse else blob_per_gpu * world)
         value = (enc_total + rep_total) / 2 * args.steps / GIB / elapsed
         line = {
             "metric": "RLNC encode+repair GiB/s device-resident, 10MB chunksets; % HBM roofline",
-            "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
+            "value": round(value, 2), "unit": "GiB/s", "n_gpus": 1 if rehearse else world, "steps": args.steps,
             "warmup": args.warmup, "settle_steps": settle_steps, "ms_per_step": round(elapsed * 1e3 / args.steps, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
             "data": "synthetic (SplitMix64 random blob + coding vectors, seeded)",
@@ -339,6 +352,8 @@ def main():
                           "encode_blob_GiBps": round(n * CS / GIB / (enc_ms * 1e-3), 1),
                           "repair_blob_GiBps": round(rep_len / GIB / ((plan_ms + dec_ms) * 1e-3), 1),
                           "ready_chunksets": n_ready, "not_ready_chunksets": n - n_ready},
+            "rehearsal": None if rehearse is None else dict(rehearse, first_chunkset=lo, chunksets=n,
+                                                             blob_bytes=blob_per_gpu * world, shard_bytes=blob_len_rank),
             "commitment": commit,
             "encode_batch_sweep": sweep,
         }
@@ -347,7 +362,7 @@ def main():
         else:
             line["cpu_baseline"] = None
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if dist_on:
         dist.destroy_process_group()
 
 

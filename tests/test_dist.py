@@ -38,6 +38,18 @@ def test_shard_range_partitions():
             assert max(b - a for a, b in spans) - min(b - a for a, b in spans) <= -(-n_total // world)
 
 
+def test_cfg5_shard_plan():
+    # BASELINE cfg5: a 128 GiB blob over 8 GPUs = bench.py --config cfg3 at N = 8 (and the one-GPU
+    # rehearsal --rehearse-shard R/8): 13108 chunksets, 1639 per rank, the last rank 1635 with a final
+    # chunkset of 2 MiB of data
+    blob_per_gpu, world, cs = bench.CONFIGS["cfg3"][0], 8, 10 << 20
+    n_total = -(-(blob_per_gpu * world) // cs)
+    assert n_total == 13108
+    spans = [bench.shard_range(n_total, world, r) for r in range(world)]
+    assert [b - a for a, b in spans] == [1639] * 7 + [1635]
+    assert blob_per_gpu * world - (n_total - 1) * cs == 2 << 20
+
+
 def _worker(rank, world, port, n_total, blob_len, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
