@@ -15,19 +15,20 @@ import oracle as o  # noqa: E402
 pytestmark = pytest.mark.gpu
 
 
-def _broken(ctx, tmp_path, size, seed):
+def _broken(ctx, tmp_path, size, seed, **kw):
     blob = o.fill_random(seed, size)
     coeffs = o.fill_random(seed + 1, -(-size // CS) * N * K)
     src = tmp_path / "blob.data"
     blob.tofile(src)
     d = tmp_path / "shares"
-    header = files.break_blob(ctx, str(src), str(d), batch=2, coeffs=coeffs)
+    header = files.break_blob(ctx, str(src), str(d), batch=2, coeffs=coeffs, **kw)
     return blob, header, d
 
 
-def test_break_layout_header_and_proofs(ctx, tmp_path):
+@pytest.mark.parametrize("device_store", [None, False])  # coded rows kept in HBM / in a page-locked host store
+def test_break_layout_header_and_proofs(ctx, tmp_path, device_store):
     size = 2 * CS + 12345
-    blob, header, d = _broken(ctx, tmp_path, size, 0xF11E)
+    blob, header, d = _broken(ctx, tmp_path, size, 0xF11E, device_store=device_store)
     n = 3
     h2 = files.read_blob_metadata(str(d))
     assert h2 == header and h2.get_blob_size() == size and h2.get_num_chunksets() == n

@@ -18,12 +18,16 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gib", type=float, default=1.0)
     ap.add_argument("--dir", default="/dev/shm" if os.path.isdir("/dev/shm") else tempfile.gettempdir())
-    ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--batch", type=int, default=0, help="chunksets per device batch (0: the flow's default)")
+    ap.add_argument("--module", default="files", help="decds_amd module holding the flow (A/B of versions)")
     a = ap.parse_args()
     import numpy as np
     import torch  # noqa: F401  (torch's HIP runtime must initialise before the library creates its context)
     import decds_amd
-    from decds_amd import codec, files
+    import importlib
+    from decds_amd import codec
+    files = importlib.import_module("decds_amd." + a.module)
+    kw = {"batch": a.batch} if a.batch else {}
     from decds_amd._capi import N
     ctx = decds_amd.Context(0)
     size = int(a.gib * (1 << 30))
@@ -34,7 +38,7 @@ def main():
         blob.tofile(src)
         tb = {}
         t0 = time.perf_counter()
-        header = files.break_blob(ctx, src, os.path.join(work, "shares"), batch=a.batch, timings=tb)
+        header = files.break_blob(ctx, src, os.path.join(work, "shares"), timings=tb, **kw)
         t_break = time.perf_counter() - t0
         rng = np.random.default_rng(6)
         for c in range(header.get_num_chunksets()):
@@ -42,12 +46,12 @@ def main():
                 os.remove(os.path.join(work, "shares", "chunkset.%d" % c, "share%02d.data" % j))
         tr = {}
         t0 = time.perf_counter()
-        out = files.repair_blob(ctx, os.path.join(work, "shares"), os.path.join(work, "repaired"), batch=a.batch,
-                                timings=tr)
+        out = files.repair_blob(ctx, os.path.join(work, "shares"), os.path.join(work, "repaired"), timings=tr,
+                                **kw)
         t_repair = time.perf_counter() - t0
         same = bool(np.array_equal(np.fromfile(out, dtype=np.uint8), blob))
         gib = size / (1 << 30)
-        print(json.dumps({"blob_GiB": gib, "chunksets": header.get_num_chunksets(), "batch": a.batch,
+        print(json.dumps({"blob_GiB": gib, "chunksets": header.get_num_chunksets(), "batch": a.batch or "default", "module": a.module,
                           "workdir_fs": a.dir, "break_s": round(t_break, 3), "break_GiBps": round(gib / t_break, 3),
                           "break_phases_s": {k: round(v, 3) for k, v in tb.items()},
                           "repair_s": round(t_repair, 3), "repair_GiBps": round(gib / t_repair, 3),
