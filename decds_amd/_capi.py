@@ -125,6 +125,7 @@ def _declare(L):
         "decds_host_unregister": (c.c_int, [VP]),
         "decds_host_alloc": (c.c_int, [SZ, c.POINTER(c.c_void_p)]),
         "decds_host_free": (c.c_int, [VP]),
+        "decds_host_cache_trim": (SZ, []),
         "decds_host_is_registered": (c.c_int, [VP, SZ]),
         "decds_device_status": (c.c_int, [P]),
         "decds_blob_encode_host_multi": (c.c_int, [VP, SZ, VP, SZ, VP, VP, SZ]),
@@ -176,7 +177,7 @@ EXPORTED = [
     "decds_repairing_blob_is_chunkset_ready_to_repair", "decds_repairing_blob_is_chunkset_already_repaired",
     "decds_repairing_blob_get_repaired_chunkset", "decds_repairing_blob_free",
     "decds_encode_commit_workspace_bytes", "decds_encode_commit_batch", "decds_encode_kernel_name",
-    "decds_decode_kernel_name",
+    "decds_decode_kernel_name", "decds_host_cache_trim",
 ]
 
 

@@ -92,11 +92,15 @@ class Blob:
         return [Chunk(c, c * N + share_id, data[c].tobytes(),
                       [proofs[c, 32 * k:32 * (k + 1)].tobytes() for k in range(plen)]) for c in range(n)]
 
+    def free(self):
+        """releases the Blob (its coded store goes to the library's page-locked block cache)"""
+        if self._h:
+            lib().decds_blob_free(self._h)
+            self._h = None
+
     def __del__(self):
         try:
-            if self._h:
-                lib().decds_blob_free(self._h)
-                self._h = None
+            self.free()
         except Exception:
             pass
 

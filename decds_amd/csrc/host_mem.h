@@ -26,7 +26,8 @@ namespace decds {
 // memory + hipHostRegister was measured against hipHostMalloc here and moved data at the same rate
 // (blob host paths 28.7 / 35 GiB/s either way, r02zd-ze), so these stay hipHostMalloc memory.
 hipError_t host_pinned_alloc(size_t n, void **out);
-void host_pinned_free(void *p, size_t n);
+void host_pinned_free(void *p, size_t n);  // blocks >= 64 MiB are cached for reuse (host_mem.cpp)
+size_t host_cache_trim();                   // frees the cached blocks; returns their bytes
 
 // A use of [p, p+n) by one call: pinned() is true iff the whole range lies in one registered
 // range, which then stays locked until the use ends (an unregister meanwhile is deferred).

@@ -344,9 +344,14 @@ void decds_blake3_parallel(const uint8_t *data, size_t len, uint8_t out[32], int
  * range takes effect when that call returns. Pair with decds_host_unregister before freeing. */
 int decds_host_register(const void *ptr, size_t len);
 int decds_host_unregister(const void *ptr);
-/* page-locked host memory the host paths DMA directly (hipHostMalloc + the same registry) */
+/* page-locked host memory the host paths DMA directly (hipHostMalloc + the same registry). Blocks
+ * of 64 MiB and more (the library's own, e.g. a Blob's coded store, and these) go to a cache when
+ * freed — up to DECDS_PINNED_CACHE_MB (default 16384) — and serve later requests of 80-100 % of
+ * their size without page-locking again (~0.25 s per GiB); decds_host_cache_trim releases them and
+ * returns the bytes released. Memory from the cache is not zeroed. */
 int decds_host_alloc(size_t len, void **out);
 int decds_host_free(void *ptr);
+size_t decds_host_cache_trim(void);
 /* 1 if [ptr, ptr+len) lies inside one registered or allocated range, else 0 */
 int decds_host_is_registered(const void *ptr, size_t len);
 

@@ -152,3 +152,44 @@ def test_chunkset_mirror_concurrent_callers(ctx):
         ref = o.chunkset_encode(data, o.fill_random(0xD100 + t, N * K), nthreads=8)
         cs = results[t][0]
         assert all(cs.get_chunk(j).erasure_coded_data == ref[j].tobytes() for j in range(N))
+
+
+def test_pinned_block_cache_reuse_and_trim(ctx):
+    # blocks >= 64 MiB go back to the library's page-locked cache on free and serve the next request
+    # of 80-100 % of their size (a Blob's coded store: page-locking costs ~0.25 s per GiB); trim frees them
+    import ctypes
+    L = lib()
+    L.decds_host_cache_trim()
+    big = 96 << 20
+    p1 = ctypes.c_void_p()
+    check(L.decds_host_alloc(big, ctypes.byref(p1)))
+    assert L.decds_host_is_registered(p1, big) == 1
+    ctypes.memset(p1, 0x5A, big)
+    check(L.decds_host_free(p1))
+    assert L.decds_host_is_registered(p1, big) == 0
+    p2 = ctypes.c_void_p()
+    check(L.decds_host_alloc(big - (8 << 20), ctypes.byref(p2)))      # 92 % of the cached block
+    assert p2.value == p1.value and L.decds_host_is_registered(p2, big - (8 << 20)) == 1
+    check(L.decds_host_free(p2))
+    p3 = ctypes.c_void_p()
+    check(L.decds_host_alloc(64 << 20, ctypes.byref(p3)))             # 67 %: too small a request for it
+    assert p3.value != p1.value
+    check(L.decds_host_free(p3))                                       # 64 MiB: cached too
+    assert L.decds_host_cache_trim() == big + (64 << 20)
+    assert L.decds_host_cache_trim() == 0
+    # the blob path into a cached block (holding the previous call's bytes) is still bit-exact
+    n = 5
+    blob = o.fill_random(0xCAC4E, n * CS - 99)
+    coeffs = o.fill_random(0xCAC4F, n * N * K)
+    want = o.blob_encode(blob, coeffs, nthreads=8)
+    ptrs = []
+    for fill in (0xA5, None):
+        hb = decds_amd.HostBuffer(n * N * F)                            # 84 MiB: cached when freed
+        ptrs.append(hb.array.ctypes.data)
+        if fill is not None:
+            hb.array[:] = fill
+        coded = codec.blob_encode_host(ctx, blob, coeffs, batch=2, out=hb.array.reshape(n * N, F))
+        assert np.array_equal(coded, want)
+        hb.free()
+    assert ptrs[0] == ptrs[1]
+    L.decds_host_cache_trim()
