@@ -101,15 +101,21 @@ namespace decds {
 // Chunk::digest of a full coded piece (chunk.rs:40-46) without copying it: message chunk c >= 8 is
 // data[1024c - 16, 1024c + 1008), so chunks 8..1023 are hashed in place as complete subtrees; chunks
 // 0..7 (the ids' chunk) from an 8 KiB copy; the 27-byte 1025th chunk joins the 1024-chunk left tree
-// under ROOT. Four quarters (0-255, 256-511, 512-767, 768-1023) run on the host pool; side(0 ..
+// under ROOT. PIECE_PARTS aligned parts of 1024 / PIECE_PARTS chunks run on the host pool (per
+// RepairingBlob::add_chunk, r04p: 4 parts 75-76 us, 8 parts 72-75, 16 parts 89-119); side(0 ..
 // side_tasks - 1), if any, run beside them (RepairingBlob::add_chunk stages the piece for its H2D copy).
+#ifndef DECDS_PIECE_PARTS
+#define DECDS_PIECE_PARTS 4
+#endif
+constexpr size_t PIECE_PARTS = DECDS_PIECE_PARTS, PART_CHUNKS = 1024 / PIECE_PARTS;
+static_assert(PART_CHUNKS >= 16 && (PART_CHUNKS & (PART_CHUNKS - 1)) == 0, "parts are power-of-two subtrees");
 void full_piece_digest(uint64_t chunkset_id, uint64_t chunk_id, const uint8_t *data, uint8_t out[32],
                        const std::function<void(size_t)> *side, size_t side_tasks) {
     auto at = [&](size_t c) { return data + c * b3::CHUNK - 16; };
-    uint32_t q[4][8];
-    host_parallel(4 + (side ? side_tasks : 0), [&](size_t task) {
-        if (task >= 4) {
-            (*side)(task - 4);
+    uint32_t q[PIECE_PARTS][8];
+    host_parallel(PIECE_PARTS + (side ? side_tasks : 0), [&](size_t task) {
+        if (task >= PIECE_PARTS) {
+            (*side)(task - PIECE_PARTS);
         } else if (task == 0) {
             alignas(64) uint8_t head[8 * b3::CHUNK];
             for (int b = 0; b < 8; b++) {
@@ -119,20 +125,19 @@ void full_piece_digest(uint64_t chunkset_id, uint64_t chunk_id, const uint8_t *d
             std::memcpy(head + 16, data, sizeof(head) - 16);
             uint32_t sub[8];
             b3h::simd_subtree(head, 8, 0, q[0]);
-            for (size_t k = 8; k < 256; k *= 2) {
+            for (size_t k = 8; k < PART_CHUNKS; k *= 2) {
                 b3h::simd_subtree(at(k), k, k, sub);
                 b3::parent(q[0], sub, 0, q[0]);
             }
         } else {
-            b3h::simd_subtree(at(256 * task), 256, 256 * task, q[task]);
+            b3h::simd_subtree(at(PART_CHUNKS * task), PART_CHUNKS, PART_CHUNKS * task, q[task]);
         }
     });
-    uint32_t lo[8], hi[8], left[8], last[8], root[8];
-    b3::parent(q[0], q[1], 0, lo);
-    b3::parent(q[2], q[3], 0, hi);
-    b3::parent(lo, hi, 0, left);
+    for (size_t w = PIECE_PARTS; w > 1; w /= 2)  // fold the parts pairwise up to the 1024-chunk left tree
+        for (size_t i = 0; i < w / 2; i++) b3::parent(q[2 * i], q[2 * i + 1], 0, q[i]);
+    uint32_t last[8], root[8];
     chunk_cv(at(1024), F + 16 - 1024 * b3::CHUNK, 1024, false, last);
-    b3::parent(left, last, b3::ROOT, root);
+    b3::parent(q[0], last, b3::ROOT, root);
     to_bytes(root, out);
 }
 }  // namespace decds
