@@ -282,18 +282,23 @@ def main():
             obig, bpitch = codec.coded_buffer(nmax, aligned=not args.packed, device=dev)
         sweep = []
         for ns in SWEEP:
-            reps = 3 if ns >= 1024 else 5 if ns >= 256 else 20
-            codec.encode_batch(ctx, big, ns, cbig, obig, bpitch, stream=stream)
-            sev = [torch.cuda.Event(enable_timing=True) for _ in range(reps + 1)]
-            sev[0].record(stream)
+            # warm, then the median of >= 10 launches, each bracketed by its own events
+            reps = 10 if ns >= 256 else 20
+            t_w = time.perf_counter()
+            while time.perf_counter() - t_w < 0.2:
+                for _ in range(4):
+                    codec.encode_batch(ctx, big, ns, cbig, obig, bpitch, stream=stream)
+                stream.synchronize()
+            sev = [[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(reps)]
             for r in range(reps):
+                sev[r][0].record(stream)
                 codec.encode_batch(ctx, big, ns, cbig, obig, bpitch, stream=stream)
-                sev[r + 1].record(stream)
+                sev[r][1].record(stream)
             stream.synchronize()
-            ms = sev[0].elapsed_time(sev[-1]) / reps
+            ms = float(np.median([a.elapsed_time(b) for a, b in sev]))
             gbs = ns * (CS + N * F) / (ms * 1e-3) / 1e9
             sweep.append({"chunksets": ns, "kernel": _lib().decds_encode_kernel_name(ns).decode(),
-                          "encode_ms": round(ms, 3), "encode_GBps": round(gbs, 1),
+                          "encode_ms": round(ms, 4), "launches": reps, "encode_GBps": round(gbs, 1),
                           "frac": round(gbs / HBM_PEAK_GBS, 4), "blob_GiBps": round(ns * CS / GIB / (ms * 1e-3), 1)})
         del big, cbig, obig
 
