@@ -126,6 +126,10 @@ def _declare(L):
         "decds_host_alloc": (c.c_int, [SZ, c.POINTER(c.c_void_p)]),
         "decds_host_free": (c.c_int, [VP]),
         "decds_host_cache_trim": (SZ, []),
+        "decds_blake3_stream_new": (c.c_void_p, []),
+        "decds_blake3_stream_update": (None, [VP, VP, SZ, c.c_int]),
+        "decds_blake3_stream_finalize": (None, [VP, VP]),
+        "decds_blake3_stream_free": (None, [VP]),
         "decds_host_is_registered": (c.c_int, [VP, SZ]),
         "decds_device_status": (c.c_int, [P]),
         "decds_blob_encode_host_multi": (c.c_int, [VP, SZ, VP, SZ, VP, VP, SZ]),
@@ -177,7 +181,8 @@ EXPORTED = [
     "decds_repairing_blob_is_chunkset_ready_to_repair", "decds_repairing_blob_is_chunkset_already_repaired",
     "decds_repairing_blob_get_repaired_chunkset", "decds_repairing_blob_free",
     "decds_encode_commit_workspace_bytes", "decds_encode_commit_batch", "decds_encode_kernel_name",
-    "decds_decode_kernel_name", "decds_host_cache_trim",
+    "decds_decode_kernel_name", "decds_host_cache_trim", "decds_blake3_stream_new", "decds_blake3_stream_update",
+    "decds_blake3_stream_finalize", "decds_blake3_stream_free",
 ]
 
 

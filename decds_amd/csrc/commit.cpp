@@ -1,6 +1,8 @@
 // commit.cpp — C-ABI of the commitment layer: the batched device path (ChunkSet::new's digests,
 // chunkset Merkle roots and proofs) and host helpers for the blob-level tree (blob.rs:266-273),
 // which covers only the 32-byte chunkset roots.
+#include <algorithm>
+#include <array>
 #include <cstring>
 #include <functional>
 #include <thread>
@@ -155,6 +157,98 @@ void decds_blake3_parallel(const uint8_t *data, size_t len, uint8_t out[32], int
     subtree_cv_par(data, len, 0, true, cv, nthreads < 1 ? 1 : nthreads);
     to_bytes(cv, out);
 }
+
+}  // extern "C"
+
+// Incremental BLAKE3 over consecutive pieces of one message (the repaired blob's digest from the
+// file flow's output slots, handle_repair.rs:129-151): the hasher of the blake3 crate — a stack of
+// chaining values merged lazily, complete power-of-two subtrees aligned to the chunks hashed so far
+// taken from each piece (split over host threads), at most one chunk held back for finalize.
+struct decds_blake3_stream {
+    std::vector<std::array<uint32_t, 8>> stack;
+    uint64_t chunks = 0;  // chunks pushed (the counter of the held-back chunk)
+    uint8_t part[b3::CHUNK];
+    size_t part_len = 0;
+    void merge(uint64_t total) {  // post-merge stack depth = popcount(total)
+        while (stack.size() > (size_t)__builtin_popcountll(total)) {
+            std::array<uint32_t, 8> r = stack.back(), l;
+            stack.pop_back();
+            l = stack.back();
+            stack.pop_back();
+            b3::parent(l.data(), r.data(), 0, l.data());
+            stack.push_back(l);
+        }
+    }
+    void push(const uint32_t cv[8], uint64_t counter) {
+        merge(counter);
+        std::array<uint32_t, 8> a;
+        std::memcpy(a.data(), cv, 32);
+        stack.push_back(a);
+    }
+};
+
+extern "C" {
+
+decds_blake3_stream *decds_blake3_stream_new(void) { return new decds_blake3_stream; }
+
+void decds_blake3_stream_update(decds_blake3_stream *s, const uint8_t *p, size_t len, int nthreads) {
+    if (!s || (!p && len)) return;
+    constexpr size_t C = b3::CHUNK;
+    uint32_t cv[8];
+    if (s->part_len > 0) {  // fill the held-back chunk; finalise it only when more input follows
+        const size_t take = std::min(C - s->part_len, len);
+        std::memcpy(s->part + s->part_len, p, take);
+        s->part_len += take, p += take, len -= take;
+        if (len == 0) return;
+        chunk_cv(s->part, C, s->chunks, false, cv);
+        s->push(cv, s->chunks);
+        s->chunks++;
+        s->part_len = 0;
+    }
+    while (len > C) {  // the largest power-of-two subtree that fits and divides the chunks so far
+        size_t sub = (size_t)1 << (63 - __builtin_clzll((unsigned long long)len));
+        while (((sub - 1) & (s->chunks * C)) != 0) sub /= 2;
+        if (sub <= C) {
+            chunk_cv(p, C, s->chunks, false, cv);
+            s->push(cv, s->chunks);
+            s->chunks++;
+        } else {  // its two halves pushed separately: the lazy merge never merges a would-be root
+            const size_t half = sub / 2;
+            uint32_t l[8], r[8];
+            subtree_cv_par(p, half, s->chunks, false, l, nthreads < 1 ? 1 : nthreads);
+            subtree_cv_par(p + half, half, s->chunks + half / C, false, r, nthreads < 1 ? 1 : nthreads);
+            s->push(l, s->chunks);
+            s->push(r, s->chunks + half / C);
+            s->chunks += sub / C;
+        }
+        p += sub, len -= sub;
+    }
+    if (len > 0) {
+        std::memcpy(s->part, p, len);
+        s->part_len = len;
+        s->merge(s->chunks);
+    }
+}
+
+void decds_blake3_stream_finalize(const decds_blake3_stream *s, uint8_t out[32]) {
+    uint32_t cur[8];
+    size_t n = s->stack.size();
+    if (n == 0) {  // one chunk or less: the chunk is the root
+        chunk_cv(s->part, s->part_len, s->chunks, true, cur);
+        to_bytes(cur, out);
+        return;
+    }
+    if (s->part_len > 0) {
+        chunk_cv(s->part, s->part_len, s->chunks, false, cur);
+    } else {  // no held-back chunk: the top two entries are the last subtree's halves (n >= 2)
+        b3::parent(s->stack[n - 2].data(), s->stack[n - 1].data(), n == 2 ? b3::ROOT : 0u, cur);
+        n -= 2;
+    }
+    for (; n > 0; n--) b3::parent(s->stack[n - 1].data(), cur, n == 1 ? b3::ROOT : 0u, cur);
+    to_bytes(cur, out);
+}
+
+void decds_blake3_stream_free(decds_blake3_stream *s) { delete s; }
 
 void decds_chunk_digest(uint64_t chunkset_id, uint64_t chunk_id, const uint8_t *data, size_t len, uint8_t out[32]) {
     if (len == F && b3h::simd_available()) {

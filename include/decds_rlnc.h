@@ -337,6 +337,15 @@ int decds_blob_header_from_bytes(const uint8_t *bytes, size_t len, uint64_t *byt
 /* blake3::hash of a whole blob (Blob::new's header digest, blob.rs:249) with BLAKE3's subtrees
  * split over up to nthreads host threads (same result as decds_blake3) */
 void decds_blake3_parallel(const uint8_t *data, size_t len, uint8_t out[32], int nthreads);
+/* the same hash over consecutive pieces of one message (blake3::Hasher update / finalize): complete
+ * power-of-two subtrees of each piece are hashed on up to nthreads host threads as they arrive,
+ * at most one chunk is held back; finalize does not consume the stream (free it separately). Any
+ * split of the message gives decds_blake3's result. */
+typedef struct decds_blake3_stream decds_blake3_stream;
+decds_blake3_stream *decds_blake3_stream_new(void);
+void decds_blake3_stream_update(decds_blake3_stream *s, const uint8_t *data, size_t len, int nthreads);
+void decds_blake3_stream_finalize(const decds_blake3_stream *s, uint8_t out[32]);
+void decds_blake3_stream_free(decds_blake3_stream *s);
 
 /* Page-lock a caller buffer once for many host calls (unregistered memory is staged through the
  * context's page-locked buffers instead). Registrations are refcounted per exact range; a range

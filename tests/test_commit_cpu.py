@@ -137,3 +137,45 @@ def test_merkle_three_leaves_by_hand():
     l1 = [ab, o.blake3(c + a), o.blake3(b + z)]
     l2 = [o.blake3(l1[0] + l1[1]), o.blake3(l1[2] + z1)]
     assert root5 == o.blake3(l2[0] + l2[1])
+
+
+def _stream_blake3(data, cuts, threads=4):
+    L = _capi.lib()
+    s = L.decds_blake3_stream_new()
+    try:
+        lo = 0
+        for hi in list(cuts) + [data.size]:
+            L.decds_blake3_stream_update(s, data[lo:hi].ctypes.data if hi > lo else None, hi - lo, threads)
+            lo = hi
+        out = np.empty(32, np.uint8)
+        L.decds_blake3_stream_finalize(s, out.ctypes.data)
+        return out.tobytes()
+    finally:
+        L.decds_blake3_stream_free(s)
+
+
+def test_blake3_stream_matches_one_shot_for_any_split():
+    # blake3::Hasher semantics (lazy CV-stack merges, aligned power-of-two subtrees, one chunk held
+    # back): every split of the message gives the one-shot hash; KAT lengths pinned as well
+    for n, h in KAT_MOD251.items():
+        d = np.frombuffer(mod251(n), np.uint8).copy()
+        assert _stream_blake3(d, []).hex() == h
+        assert _stream_blake3(d, [1, 1024 % max(1, n)] if n > 1024 else [n // 2]).hex() == h
+    rng = np.random.default_rng(0xB3)
+    for n in (0, 1, 64, 1024, 1025, 2048, 2049, 3 * 1024 + 5, 8192, (1 << 20) + 17, 5 * (1 << 20) + 3,
+              10 * (1 << 20) * 3 - 99):
+        d = rng.integers(0, 256, n, dtype=np.uint8)
+        want = host_blake3(d.tobytes()) if n < (1 << 20) else None
+        if want is None:
+            out = np.empty(32, np.uint8)
+            _capi.lib().decds_blake3_parallel(d.ctypes.data, n, out.ctypes.data, 4)
+            want = out.tobytes()
+        assert _stream_blake3(d, []) == want, n
+        for _ in range(4):
+            k = int(rng.integers(1, 6))
+            cuts = sorted(int(c) for c in rng.integers(0, n + 1, k)) if n else []
+            assert _stream_blake3(d, cuts) == want, (n, cuts)
+        if n >= 3 * 1024:  # pieces ending exactly on chunk / power-of-two boundaries
+            cuts = [c for c in (1024, 2048, 4096, 10 << 20, 20 << 20) if c < n]
+            assert _stream_blake3(d, cuts) == want, (n, cuts)
+    assert _stream_blake3(np.zeros(0, np.uint8), [0, 0]) == bytes.fromhex(KAT[b""])
