@@ -181,6 +181,42 @@ __global__ __launch_bounds__(256) void dec_tile_lines_k(const uint8_t *__restric
     if (acc.x == 0x9E3779B9u && threadIdx.x == 999) lds[0] = 1;
 }
 
+// decode pattern of a line-aligned walk over T consecutive tiles per workgroup: every lane stores its
+// block's aligned granule (the previous block's bytes from the neighbour lane / previous wave / previous
+// tile in a real kernel), so every wave store is 8 whole lines; only the walk's first tile's first lane
+// stores its block at the real (misaligned) offset and the walk's last lane adds a store at the real
+// offset. Workgroup -> walk through unit_of<ORDER> (100 + R: runs of R walks per XCD). The stores only.
+template <uint32_t T, int ORDER = 0>
+__global__ __launch_bounds__(256) void dec_walk_lines_k(const uint8_t *__restrict__ in, uint8_t *__restrict__ out, size_t n) {
+    extern __shared__ uint8_t lds[];
+    constexpr uint32_t WPC = TILES / T;  // walks per chunkset
+    const uint32_t u = unit_of<ORDER>(), cs = u / WPC, t0 = (u % WPC) * T;
+    if (cs >= n) return;
+    constexpr uint32_t sel[10] = {0, 2, 3, 5, 6, 8, 9, 11, 13, 15};
+    const auto ri = rsrc(in + cs * 16 * PITCH);
+    const auto ro = rsrc(out + cs * CSB);
+    u32x4 acc = {0, 0, 0, 0};
+    for (uint32_t t = t0; t < t0 + T; t++) {
+        const uint32_t g = t * 256 + threadIdx.x;
+        const uint32_t col = g < BLOCKS ? g * 16 : 0x80000000u;
+        u32x4 x[10];
+#pragma unroll
+        for (int k = 0; k < 10; k++) x[k] = __builtin_amdgcn_raw_buffer_load_b128(ri, 128 + col + sel[k] * (uint32_t)PITCH, 0, 0);
+#pragma unroll
+        for (int k = 0; k < 10; k++) acc ^= x[k];
+        const bool first = t == t0 && threadIdx.x == 0, last = (t == t0 + T - 1 && threadIdx.x == 255) || g == BLOCKS - 1;
+#pragma unroll
+        for (int i = 0; i < 10; i++) {
+            const uint32_t off = first ? (uint32_t)(i * LB) + col : (uint32_t)(i << 20) + col;
+            __builtin_amdgcn_raw_buffer_store_b128(acc + (uint32_t)i, ro, off, 0, 0);
+        }
+        if (last)
+#pragma unroll
+            for (int i = 0; i < 10; i++) __builtin_amdgcn_raw_buffer_store_b128(acc + (uint32_t)i, ro, (uint32_t)(i * LB) + col, 0, 0);
+    }
+    if (acc.x == 0x9E3779B9u && threadIdx.x == 999) lds[0] = 1;
+}
+
 // decode pattern: a workgroup's 256 lanes compute 256 consecutive blocks, lane 0 the block before the
 // tile (recomputed), and lanes 1..248 store 248 aligned granules = 31 whole lines per piece (lanes
 // 249..255 idle): no straggler crosses a workgroup; wave runs (63 / 64 / 64 / 57 granules) meet inside
@@ -356,7 +392,8 @@ int main(int argc, char **argv) {
                           (const void *)dec_k<1, false, LB, ST_A4>, (const void *)dec_lines_k<true>, (const void *)dec_lines_k<false>,
                           (const void *)enc_lines_k<true>, (const void *)enc_lines_k<false>, (const void *)dec_tile_lines_k<0>, (const void *)dec_tile_lines_k<104>, (const void *)dec_tile_lines_k<108>, (const void *)dec_tile_lines_k<116>,
                           (const void *)dec_k<1, false, LB, ST_PLAIN, 104>, (const void *)dec_k<1, false, LB, ST_PLAIN, 108>, (const void *)dec_k<1, false, LB, ST_PLAIN, 116>, (const void *)dec_k<1, false, 1u << 20, ST_PLAIN, 108>,
-                          (const void *)enc_k<1, 108, false>, (const void *)dec_wg248_k, (const void *)dec_walk_k<4>, (const void *)dec_walk_k<8>,
+                          (const void *)enc_k<1, 108, false>, (const void *)dec_walk_lines_k<4>, (const void *)dec_walk_lines_k<4, 102>,
+                          (const void *)dec_walk_lines_k<8>, (const void *)dec_walk_lines_k<2, 104>, (const void *)dec_walk_lines_k<1, 108>, (const void *)dec_wg248_k, (const void *)dec_walk_k<4>, (const void *)dec_walk_k<8>,
                           (const void *)dec_walk_k<16>, (const void *)enc_k<4, 1, false>, (const void *)enc_k<4, 0, false>, (const void *)enc_k<4, 2, false>,
                           (const void *)enc_k<2, 0, false>, (const void *)enc_k<1, 0, false>, (const void *)enc_k<8, 2, false>})
         CK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, LDS2));
@@ -382,6 +419,18 @@ int main(int argc, char **argv) {
                 const size_t n16 = (size_t)n * CSB / 16;
                 copy_flat<<<(unsigned)((n16 + 255) / 256), 256>>>((const u32x4 *)src, (u32x4 *)rep, n16);
             }, a);
+            continue;
+        }
+        if (only == "walklines") {
+            // line-aligned walks of T tiles (stragglers only at walk ends) against the plain decode
+            constexpr uint32_t LDS3 = 52 * 1024;
+            run("dec_u1_grp8_3wg", n, db, [&] { dec_k<1, false, LB, ST_PLAIN, 108><<<g1, 256, LDS3>>>(coded, rep, n); }, a);
+            run("dec_u1_outA_3wg", n, db, [&] { dec_k<1, false, 1u << 20><<<g1, 256, LDS3>>>(coded, rep, n); }, a);
+            run("dec_walklines1_grp8_3wg", n, db, [&] { dec_walk_lines_k<1, 108><<<g1, 256, LDS3>>>(coded, rep, n); }, a);
+            run("dec_walklines2_grp4_3wg", n, db, [&] { dec_walk_lines_k<2, 104><<<g1 / 2, 256, LDS3>>>(coded, rep, n); }, a);
+            run("dec_walklines4_3wg", n, db, [&] { dec_walk_lines_k<4><<<g1 / 4, 256, LDS3>>>(coded, rep, n); }, a);
+            run("dec_walklines4_grp2_3wg", n, db, [&] { dec_walk_lines_k<4, 102><<<g1 / 4, 256, LDS3>>>(coded, rep, n); }, a);
+            run("dec_walklines8_3wg", n, db, [&] { dec_walk_lines_k<8><<<g1 / 8, 256, LDS3>>>(coded, rep, n); }, a);
             continue;
         }
         if (only == "xcdgrp") {
