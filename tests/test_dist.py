@@ -98,3 +98,12 @@ def test_two_rank_sharded_encode_matches_single_process():
     coeffs = o.fill_random(0xC0EF0002, n_total * o.N * o.K)
     coded = o.blob_encode(blob, coeffs, nthreads=4)
     assert flat == [hashlib.sha256(coded[j].tobytes()).hexdigest() for j in range(coded.shape[0])]
+
+
+def test_rehearse_shard_argument_checked_before_any_device_work():
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for bad in ("8/8", "-1/8"):
+        r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--rehearse-shard=" + bad],
+                           capture_output=True, text=True, timeout=120, env=dict(os.environ, WORLD_SIZE="1"))
+        assert r.returncode != 0 and "--rehearse-shard R/W needs 0 <= R < W" in r.stderr
