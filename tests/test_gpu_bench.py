@@ -32,3 +32,18 @@ def test_bench_line_roofline_is_the_dominant_kernels():
     assert abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-3
     assert enc["achieved"] == bd["encode_GBps"] and dec["achieved"] == bd["decode_GBps"]
     assert enc["kernel"].startswith("rlnc_encode")
+
+
+@pytest.mark.gpu
+def test_bench_rehearsal_runs_one_shard_of_a_larger_job():
+    # --rehearse-shard R/W (the one-GPU run of cfg5's shards): rank 1 of a 2-GPU cfg2 job = chunksets
+    # [103, 205) of a 2 GiB blob, the last one partial, every repaired chunkset checked inside bench.py
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "2", "--warmup", "1", "--settle-s", "0.1",
+                        "--no-cpu-baseline", "--no-commit", "--rehearse-shard", "1/2"], capture_output=True, text=True,
+                       timeout=110, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    reh = d["rehearsal"]
+    assert reh["rank"] == 1 and reh["world"] == 2 and reh["first_chunkset"] == 103 and reh["chunksets"] == 102
+    assert reh["shard_bytes"] == (2 << 30) - 103 * (10 << 20) and d["n_gpus"] == 1
+    assert d["encode_batch_sweep"] is None and d["value"] > 0
