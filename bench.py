@@ -2,9 +2,11 @@
 
 Step = one pass of the hot path over one batch: encode the rank's chunksets (10 -> 16,
 chunkset.rs:43-52) and repair every chunkset from exactly 10 random surviving coded chunks
-(plan + decode, chunkset.rs:173-208), all resident in HBM. Default workload = BASELINE config 2:
-a 1 GiB random blob = 103 chunksets per GPU, all in one batch. For N > 1 each rank owns its own
-1 GiB slice of an N GiB blob (contiguous chunkset-index shard, no collective on the data path);
+(plan + decode, chunkset.rs:173-208), all resident in HBM. Default workload = BASELINE configs 3 + 4,
+the largest single-GPU configuration: a 16 GiB random blob = 1639 chunksets per GPU, all in one
+batch, encoded and repaired from exactly 10 random survivors per chunkset (--config cfg2: the 1 GiB
+blob of config 2). For N > 1 each rank owns its own 16 GiB slice of a 16N GiB blob (contiguous
+chunkset-index shard, no collective on the data path; N = 8 is config 5, the 128 GiB blob);
 value = blob bytes of all ranks / max-over-ranks time ("scaling": "weak").
 
 Launched with torchrun for N > 1 (RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* from the environment).
@@ -37,75 +39,112 @@ def shard_range(n_total, world, rank):
     return lo, min(lo + per, n_total)
 
 
-def parse():
+def shard_arg(v):
+    """--rehearse-shard R/W: integers with 0 <= R < W (checked before anything touches the device)"""
+    try:
+        r, w = (int(x) for x in v.split("/"))
+    except ValueError:
+        raise argparse.ArgumentTypeError("expected R/W, e.g. 7/8, got %r" % v)
+    if not 0 <= r < w:
+        raise argparse.ArgumentTypeError("--rehearse-shard R/W needs 0 <= R < W, got %r" % v)
+    return r, w
+
+
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--settle-s", type=float, default=0.5,
                    help="after the W warmup steps, keep running untimed steps until this many seconds passed")
-    p.add_argument("--config", default="cfg2", choices=sorted(CONFIGS))
+    p.add_argument("--config", default="cfg3", choices=sorted(CONFIGS),
+                   help="cfg3 (default): BASELINE's largest single-GPU configuration, 16 GiB per GPU "
+                        "(configs 3 + 4; at N = 8 the whole job is config 5, the 128 GiB blob)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-commit", action="store_true", help="skip timing the commitment kernels (row f1)")
     p.add_argument("--no-sweep", action="store_true", help="skip the encode batch sweep (256..1639 chunksets)")
     p.add_argument("--cpu-sample", type=int, default=0, help="chunksets in the CPU sample (0 = auto)")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
-    p.add_argument("--rehearse-shard", default=None, metavar="R/W",
+    p.add_argument("--rehearse-shard", default=None, metavar="R/W", type=shard_arg,
                    help="one process, no process group: run only rank R's shard of a W-GPU job on this GPU "
                         "(cfg5, the 128 GiB blob over 8 GPUs, is --config cfg3 --rehearse-shard R/8)")
+    p.add_argument("--spot-out", default=None, metavar="PATH.npz",
+                   help="after the timed region, save the source bytes, coding vectors and coded rows of the "
+                        "shard's first, middle and last chunkset (the GPU tests check them against the oracle)")
     p.add_argument("--packed", action="store_true",
                    help="coded rows packed at pitch 1,048,587 instead of the recommended 128-B-aligned layout")
-    return p.parse_args()
+    return p.parse_args(argv)
 
 
-def cpu_baseline(n_sample, seed):
-    """The CPU restatement (oracle/, "port") on the host cores: rayon-style chunkset-parallel encode
-    (blob.rs:256-264) + per-chunkset incremental decode (chunkset.rs:173-208)."""
+def cpu_threads():
+    """the host threads the CPU baseline uses: the CPUs this process may run on, at most 16 (the GPU
+    box's CPU share; os.cpu_count() reports the whole machine there)"""
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        avail = os.cpu_count() or 1
+    return max(1, min(16, avail))
+
+
+def cpu_baseline(n_sample, seed, repeats=3):
+    """The CPU restatement (oracle/, "port") on the host cores: chunkset-parallel encode
+    (blob.rs:256-264) + per-chunkset repair from 10 survivors (chunkset.rs:173-208).
+
+    Headline = the strongest restatement: column-blocked GFNI affine multiplies on AVX-512
+    (oracle/rlnc_cpu_fast.c; coefficient-only rank + inverse, then one blocked pass for the repair),
+    the median of `repeats` runs with their spread. Beside it, one run each of the row-pass forms:
+    AVX2 nibble tables, and the scalar table-driven loop rlnc 0.4.0 is recalled to use. All produce
+    the same bytes (tests/test_oracle.py)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import numpy as np
     import oracle as o
-    # the GPU box's CPU share is 16 threads (os.cpu_count() reports the whole machine)
-    threads = max(1, min(16, os.cpu_count() or 1))
+    threads = cpu_threads()
     if n_sample <= 0:
-        n_sample = 8 * threads  # ~10-20 s of CPU work
+        n_sample = 16 * threads
     blob = o.fill_random(seed, n_sample * o.CS)
     coeffs = o.fill_random(seed + 1, n_sample * o.N * o.K)
     rng = np.random.default_rng(seed)
     cand = np.full((n_sample, o.N), 0xFF, np.uint8)
     for c in range(n_sample):
         cand[c, :o.K] = rng.permutation(o.N)[:o.K]
-    def run():
+    gib = n_sample * o.CS / GIB
+
+    def run(enc, rep):
         t0 = time.perf_counter()
-        coded = o.blob_encode(blob, coeffs, nthreads=threads)
+        coded = enc(blob, coeffs, nthreads=threads)
         t1 = time.perf_counter()
-        out, status = o.blob_repair(coded, cand, blob.size, nthreads=threads)
+        out, status = rep(coded, cand, blob.size, nthreads=threads)
         t2 = time.perf_counter()
         ok = status == 0
         assert np.array_equal(out.reshape(n_sample, o.CS)[ok], blob.reshape(n_sample, o.CS)[ok])
-        return t0, t1, t2
+        del coded, out
+        # encode + repair GiB/s as the GPU's value: (blob bytes encoded + repaired) / 2 per second
+        return {"value": gib / (t2 - t0), "encode_gib_s": gib / (t1 - t0), "repair_gib_s": gib / (t2 - t1)}
 
-    gib = n_sample * o.CS / GIB
-
-    def point(t0, t1, t2):
-        return {"value": gib / (t2 - t0), "encode_gib_s": gib / (t1 - t0), "repair_gib_s": gib / (t2 - t1),
-                "encode_s": round(t1 - t0, 3), "repair_s": round(t2 - t1, 3)}
-
-    # headline: the restatement with AVX2 nibble-table row kernels (same bytes as the scalar,
-    # tests/test_oracle.py) — the stronger of the two CPU points; the scalar table-driven row loop
-    # rlnc 0.4.0 is recalled to use is reported beside it
+    rows = {}
     o.set_simd(0)
-    scalar = point(*run())
-    simd = None
+    rows["scalar tables, row passes"] = run(o.blob_encode, o.blob_repair)
     if o.set_simd(1):
-        simd = point(*run())
-        o.set_simd(0)
-    head = simd or scalar
-    line = {"value": head["value"], "unit": "GiB/s", "cores": threads, "kind": "port",
-            "variant": "avx2 nibble tables" if simd else "scalar tables",
+        rows["avx2 nibble tables, row passes"] = run(o.blob_encode, o.blob_repair)
+    o.set_simd(0)
+    head_name, head = None, None
+    if o.fast_supported():
+        head_name = "avx512 gfni affine, column-blocked"
+        runs = [run(o.fast_blob_encode, o.fast_blob_repair) for _ in range(max(1, repeats))]
+        med = lambda k: float(np.median([r[k] for r in runs]))
+        head = {"value": med("value"), "encode_gib_s": med("encode_gib_s"), "repair_gib_s": med("repair_gib_s"),
+                "runs": len(runs), "spread": [round(min(r["value"] for r in runs), 2),
+                                              round(max(r["value"] for r in runs), 2)]}
+    else:
+        head_name = max(rows, key=lambda k: rows[k]["value"])
+        head = dict(rows[head_name], runs=1, spread=None)
+    rnd = lambda d: {k: (round(v, 2) if isinstance(v, float) else v) for k, v in d.items()}
+    return {"value": round(head["value"], 2), "unit": "GiB/s", "cores": threads, "kind": "port",
+            "variant": head_name, "median_of": head["runs"], "spread": head["spread"],
             "sample": "%d chunksets (%.0f MiB) encode + repair from 10 survivors, %d threads (chunkset-parallel)"
                       % (n_sample, n_sample * o.CS / 2 ** 20, threads),
-            "encode_gib_s": head["encode_gib_s"], "repair_gib_s": head["repair_gib_s"], "scalar": scalar}
-    return line
+            "encode_gib_s": round(head["encode_gib_s"], 2), "repair_gib_s": round(head["repair_gib_s"], 2),
+            "other_variants": {k: rnd(v) for k, v in rows.items()}}
 
 
 def main():
@@ -128,9 +167,7 @@ def main():
     if args.rehearse_shard:
         if world != 1:
             raise SystemExit("--rehearse-shard runs in a single process")
-        rank, world = (int(v) for v in args.rehearse_shard.split("/"))
-        if not 0 <= rank < world:
-            raise SystemExit("--rehearse-shard R/W needs 0 <= R < W")
+        rank, world = args.rehearse_shard
         rehearse = {"rank": rank, "world": world}
     dist_on = world > 1 and rehearse is None
     # DECDS_BENCH_BACKEND=gloo is a rehearsal mode for the N > 1 path on a box with fewer GPUs than
@@ -224,6 +261,14 @@ def main():
     for c in np.nonzero(st == 0)[0].tolist():
         assert torch.equal(out[c * CS:(c + 1) * CS], src[c * CS:(c + 1) * CS]), "repaired chunkset %d differs" % c
     n_ready = int((st == 0).sum())
+    if args.spot_out:
+        spots = sorted({0, n // 2, n - 1})
+        rows = coded.as_strided((n * N, F), (pitch, 1))
+        np.savez(args.spot_out, chunksets=np.array([lo + c for c in spots], np.int64),
+                 src=np.stack([src[c * CS:(c + 1) * CS].cpu().numpy() for c in spots]),
+                 coeffs=np.stack([coeffs_h[c * N * K:(c + 1) * N * K] for c in spots]),
+                 coded=np.stack([rows[c * N:(c + 1) * N].cpu().numpy() for c in spots]),
+                 shard_bytes=np.int64(blob_len_rank), pitch=np.int64(pitch))
 
     # the next row, timed beside the headline step, never inside it: ChunkSet::new's
     # commitment (BLAKE3 of every coded row + 16-leaf Merkle trees/proofs) over the same coded rows
@@ -275,11 +320,14 @@ def main():
     if world == 1 and not args.no_sweep:
         del out, plan, verd, status
         nmax = max(SWEEP)
-        with torch.cuda.stream(stream):
-            big = torch.empty(nmax * CS, dtype=torch.uint8, device=dev)
-            codec.fill_random_device(ctx, 0xDEC05003, big, stream=stream)
-            cbig = torch.from_numpy(codec.fill_random_host(0xC0EF0003, nmax * N * K)).to(dev)
-            obig, bpitch = codec.coded_buffer(nmax, aligned=not args.packed, device=dev)
+        if n >= nmax:  # cfg3: the headline's own 16 GiB blob and coded rows
+            big, cbig, obig, bpitch = src, coeffs, coded, pitch
+        else:
+            with torch.cuda.stream(stream):
+                big = torch.empty(nmax * CS, dtype=torch.uint8, device=dev)
+                codec.fill_random_device(ctx, 0xDEC05003, big, stream=stream)
+                cbig = torch.from_numpy(codec.fill_random_host(0xC0EF0003, nmax * N * K)).to(dev)
+                obig, bpitch = codec.coded_buffer(nmax, aligned=not args.packed, device=dev)
         sweep = []
         for ns in SWEEP:
             # warm, then the median of >= 10 launches, each bracketed by its own events

@@ -59,6 +59,10 @@ def lib():
             ("orc_matrix_inverse", c.c_int, [vp, vp, sz, u32]),
             ("orc_blob_encode", c.c_int, [vp, sz, vp, vp, u32, u8, c.c_int]),
             ("orc_blob_repair", c.c_int, [vp, sz, vp, sz, vp, vp, u32, u8, c.c_int]),
+            ("orc_fast_supported", c.c_int, []),
+            ("orc_gf_affine_matrix", u64, [u8, u32]),
+            ("orc_fast_blob_encode", c.c_int, [vp, sz, vp, vp, u32, u8, c.c_int]),
+            ("orc_fast_blob_repair", c.c_int, [vp, sz, vp, sz, vp, vp, u32, u8, c.c_int]),
             ("orc_blake3", None, [vp, sz, vp]),
             ("orc_chunk_digest", None, [u64, u64, vp, sz, vp]),
             ("orc_merkle", c.c_int, [vp, sz, vp, vp]),
@@ -187,6 +191,36 @@ def blob_repair(coded, cand, blob_len, poly=POLY, marker=MARKER, nthreads=1):
     out = np.zeros(blob_len, dtype=np.uint8)
     status = np.empty(n, dtype=np.int32)
     lib().orc_blob_repair(_p(coded), n, _p(cand), blob_len, _p(out), _p(status), poly, marker, nthreads)
+    return out, status
+
+
+def fast_supported():
+    """the blocked GFNI / AVX-512 codec (rlnc_cpu_fast.c) runs on this CPU"""
+    return bool(lib().orc_fast_supported())
+
+
+def fast_blob_encode(blob, coeffs, poly=POLY, marker=MARKER, nthreads=1):
+    """blob_encode's bytes from the column-blocked GFNI codec (cpu_baseline's headline variant)"""
+    blob = np.ascontiguousarray(blob, dtype=np.uint8)
+    n = -(-blob.size // CS)
+    coeffs = np.ascontiguousarray(coeffs, dtype=np.uint8)
+    out = np.empty((n * N, F), dtype=np.uint8)
+    st = lib().orc_fast_blob_encode(_p(blob), blob.size, _p(coeffs), _p(out), poly, marker, nthreads)
+    if st != OK:
+        raise RuntimeError("orc_fast_blob_encode status %d" % st)
+    return out
+
+
+def fast_blob_repair(coded, cand, blob_len, poly=POLY, marker=MARKER, nthreads=1):
+    """blob_repair's output and statuses from coefficient-only rank + inverse + one blocked GFNI pass"""
+    coded = np.ascontiguousarray(coded, dtype=np.uint8)
+    n = coded.shape[0] // N
+    cand = np.ascontiguousarray(cand, dtype=np.uint8)
+    out = np.zeros(blob_len, dtype=np.uint8)
+    status = np.empty(n, dtype=np.int32)
+    st = lib().orc_fast_blob_repair(_p(coded), n, _p(cand), blob_len, _p(out), _p(status), poly, marker, nthreads)
+    if st != OK:
+        raise RuntimeError("orc_fast_blob_repair status %d" % st)
     return out, status
 
 

@@ -103,7 +103,11 @@ def test_two_rank_sharded_encode_matches_single_process():
 def test_rehearse_shard_argument_checked_before_any_device_work():
     import subprocess
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    for bad in ("8/8", "-1/8"):
+    # argparse refuses a malformed or out-of-range R/W with a usage error, before torch is imported
+    for bad, msg in (("8/8", "needs 0 <= R < W"), ("-1/8", "needs 0 <= R < W"), ("3", "expected R/W"),
+                     ("x/8", "expected R/W"), ("1/2/3", "expected R/W")):
         r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--rehearse-shard=" + bad],
                            capture_output=True, text=True, timeout=120, env=dict(os.environ, WORLD_SIZE="1"))
-        assert r.returncode != 0 and "--rehearse-shard R/W needs 0 <= R < W" in r.stderr
+        assert r.returncode == 2 and msg in r.stderr and "Traceback" not in r.stderr, (bad, r.stderr[-500:])
+    assert bench.parse(["--rehearse-shard", "7/8"]).rehearse_shard == (7, 8)
+    assert bench.parse([]).config == "cfg3"     # BASELINE's largest single-GPU configuration

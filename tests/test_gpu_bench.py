@@ -14,7 +14,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 @pytest.mark.gpu
 def test_bench_line_roofline_is_the_dominant_kernels():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "3", "--warmup", "1", "--settle-s", "0.1",
-                        "--no-cpu-baseline", "--no-commit", "--no-sweep"], capture_output=True, text=True, timeout=110,
+                        "--config", "cfg2", "--no-cpu-baseline", "--no-commit", "--no-sweep"], capture_output=True,
+                       text=True, timeout=110,
                        cwd=ROOT)
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
@@ -39,7 +40,8 @@ def test_bench_rehearsal_runs_one_shard_of_a_larger_job():
     # --rehearse-shard R/W (the one-GPU run of cfg5's shards): rank 1 of a 2-GPU cfg2 job = chunksets
     # [103, 205) of a 2 GiB blob, the last one partial, every repaired chunkset checked inside bench.py
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "2", "--warmup", "1", "--settle-s", "0.1",
-                        "--no-cpu-baseline", "--no-commit", "--rehearse-shard", "1/2"], capture_output=True, text=True,
+                        "--config", "cfg2", "--no-cpu-baseline", "--no-commit", "--rehearse-shard", "1/2"],
+                       capture_output=True, text=True,
                        timeout=110, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-2000:]
     d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
@@ -47,3 +49,36 @@ def test_bench_rehearsal_runs_one_shard_of_a_larger_job():
     assert reh["rank"] == 1 and reh["world"] == 2 and reh["first_chunkset"] == 103 and reh["chunksets"] == 102
     assert reh["shard_bytes"] == (2 << 30) - 103 * (10 << 20) and d["n_gpus"] == 1
     assert d["encode_batch_sweep"] is None and d["value"] > 0
+
+
+@pytest.mark.gpu
+def test_bench_cfg5_last_shard_rehearsal_spot_checked(tmp_path):
+    # cfg5's shard geometry on one GPU: rank 7 of the 128 GiB blob over 8 GPUs = chunksets
+    # [11473, 13108), 1635 of them, the last holding 2 MiB of data (blob.rs:252-254 zero-pads it).
+    # bench.py repairs every chunkset and compares it with its source itself; here its first, middle
+    # and last chunkset's coded rows (payload-aligned layout) are checked against the oracle, and
+    # their source bytes against the global synthetic blob at the shard's offset.
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as o
+    spot = str(tmp_path / "spot.npz")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--config", "cfg3", "--rehearse-shard", "7/8",
+                        "--steps", "1", "--warmup", "1", "--settle-s", "0", "--no-cpu-baseline", "--no-commit",
+                        "--spot-out", spot], capture_output=True, text=True, timeout=110, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    reh = d["rehearsal"]
+    assert reh["first_chunkset"] == 11473 and reh["chunksets"] == 1635 and reh["world"] == 8
+    assert reh["shard_bytes"] == (128 << 30) - 11473 * o.CS
+    assert d["config"]["chunksets_per_gpu"] == 1635 and d["breakdown"]["ready_chunksets"] >= 1600
+    z = np.load(spot)
+    assert z["chunksets"].tolist() == [11473, 11473 + 817, 13107]
+    for k, c in enumerate(z["chunksets"].tolist()):
+        have = min(o.CS, (128 << 30) - c * o.CS)
+        expect = np.zeros(o.CS, np.uint8)
+        expect[:have] = o.fill_random(0xDEC05002, have, c * o.CS)
+        assert np.array_equal(z["src"][k], expect), c
+        assert np.array_equal(z["coeffs"][k], o.fill_random(0xC0EF0002, o.N * o.K, c * o.N * o.K)), c
+        ref = o.chunkset_encode(expect, z["coeffs"][k], nthreads=8)
+        assert np.array_equal(z["coded"][k], ref), c
+    assert (128 << 30) - 13107 * o.CS == 2 << 20

@@ -108,3 +108,41 @@ def test_cfg3_16gib_encode_repair_commit_validate(ctx):
     codec.validate_batch(ctx, coded, n * N, ids, fp, 4 + depth, roots, n, vdig, valid, blob_root=broot)
     v = valid.cpu().numpy()
     assert int(v.sum()) == n * N - 1 and v[777] == 0
+
+
+def test_payload_aligned_layout_at_the_bench_batches(ctx):
+    # the layout bench.py and the encode sweep time (pitch 1,048,704, payloads 128-byte aligned) at the
+    # north-star batches: launches of 256 and of all 1639 chunksets of a 16 GiB blob, first / middle /
+    # last chunkset of each bit-exact against the oracle; then every chunkset of the 1639 repaired
+    # from 10 survivors equals its source
+    blob_len = 16 << 30
+    n = -(-blob_len // CS)
+    src = torch.zeros(n * CS, dtype=torch.uint8, device="cuda")
+    codec.fill_random_device(ctx, 0xDEC05004, src, nbytes=blob_len)
+    coeffs = o.fill_random(0xC0EF0004, n * N * K)
+    dco = torch.from_numpy(coeffs).cuda()
+    coded, pitch = codec.coded_buffer(n)
+    assert pitch == codec.CODED_PITCH_ALIGNED and (coded.data_ptr() + K) % 128 == 0
+    rows = coded.as_strided((n * N, F), (pitch, 1))
+    for nb in (256, n):
+        coded.fill_(0xA5)
+        codec.encode_batch(ctx, src, nb, dco, coded, pitch)
+        torch.cuda.synchronize()
+        for c in sorted({0, nb // 2, nb - 1}):
+            ref = o.chunkset_encode(src[c * CS:(c + 1) * CS].cpu().numpy(), coeffs[c * 160:(c + 1) * 160], nthreads=8)
+            assert np.array_equal(rows[c * N:(c + 1) * N].cpu().numpy(), ref), (nb, c)
+        if nb < n:  # nothing past the batch was written
+            assert int(rows[nb * N].cpu()[0]) == 0xA5 and int(rows[n * N - 1].cpu()[-1]) == 0xA5
+    rng = np.random.default_rng(0x5EED0004)
+    cand = np.full((n, N), 0xFF, np.uint8)
+    for c in range(n):
+        cand[c, :K] = rng.permutation(N)[:K]
+    plan = torch.empty(n * 128, dtype=torch.uint8, device="cuda")
+    verd = torch.empty(n * N, dtype=torch.int8, device="cuda")
+    status = torch.empty(n, dtype=torch.int32, device="cuda")
+    out = torch.empty(n * CS, dtype=torch.uint8, device="cuda")
+    codec.repair_batch(ctx, coded, n, torch.from_numpy(cand).cuda(), plan, verd, out, status, pitch=pitch)
+    st = status.cpu().numpy()
+    assert set(np.unique(st).tolist()) <= {0, 5} and int((st == 0).sum()) > n - 30
+    for c in np.nonzero(st == 0)[0].tolist():
+        assert torch.equal(out[c * CS:(c + 1) * CS], src[c * CS:(c + 1) * CS]), c
