@@ -46,6 +46,7 @@ STATUS_NAMES = {
     -1: "HipError",
     -2: "InvalidArgument",
     -3: "NoDevice",
+    -4: "OutOfDeviceMemory",
 }
 STATUS = {v: k for k, v in STATUS_NAMES.items()}
 
@@ -142,6 +143,9 @@ def _declare(L):
         "decds_blob_get_share": (c.c_int, [P, SZ, VP, SZ, VP, SZ]),
         "decds_blob_free": (None, [P]),
         "decds_repairing_blob_new": (c.c_int, [P, c.c_uint64, c.c_uint64, VP, VP, c.POINTER(c.c_void_p)]),
+        "decds_repairing_blob_new_multi": (c.c_int, [VP, SZ, c.c_uint64, c.c_uint64, VP, VP, c.POINTER(c.c_void_p)]),
+        "decds_repairing_blob_set_device_budget": (c.c_int, [P, c.c_uint64]),
+        "decds_repairing_blob_memory": (c.c_int, [P, c.POINTER(c.c_uint64), SZ]),
         "decds_repairing_blob_add_chunk": (c.c_int, [P, c.c_uint64, c.c_uint64, VP, SZ, VP, SZ]),
         "decds_repairing_blob_add_chunks": (c.c_int, [P, SZ, VP, VP, VP, SZ, VP]),
         "decds_repairing_blob_is_chunkset_ready_to_repair": (c.c_int, [P, SZ, c.POINTER(c.c_int)]),
@@ -179,7 +183,8 @@ EXPORTED = [
     "decds_blob_proof_len", "decds_blob_get_chunk", "decds_blob_get_share", "decds_blob_free",
     "decds_repairing_blob_new", "decds_repairing_blob_add_chunk", "decds_repairing_blob_add_chunks",
     "decds_repairing_blob_is_chunkset_ready_to_repair", "decds_repairing_blob_is_chunkset_already_repaired",
-    "decds_repairing_blob_get_repaired_chunkset", "decds_repairing_blob_free",
+    "decds_repairing_blob_get_repaired_chunkset", "decds_repairing_blob_free", "decds_repairing_blob_new_multi",
+    "decds_repairing_blob_set_device_budget", "decds_repairing_blob_memory",
     "decds_encode_commit_workspace_bytes", "decds_encode_commit_batch", "decds_encode_kernel_name",
     "decds_decode_kernel_name", "decds_host_cache_trim", "decds_blake3_stream_new", "decds_blake3_stream_update",
     "decds_blake3_stream_finalize", "decds_blake3_stream_free",

@@ -17,27 +17,52 @@ def _ctx_array(ctxs):
     return arr, len(ctxs)
 
 
+class _PinnedBlock:
+    """owns one decds_host_alloc block; frees it when the last reference (a HostBuffer or any numpy
+    view of its array) is gone, or on release()"""
+
+    def __init__(self, p):
+        self.p = p
+
+    def release(self):
+        if self.p:
+            lib().decds_host_free(self.p)
+            self.p = None
+
+    def __del__(self):
+        try:
+            self.release()
+        except Exception:
+            pass
+
+
 class HostBuffer:
-    """Page-locked host bytes from decds_host_alloc, viewed as a numpy uint8 array (`.array`)."""
+    """Page-locked host bytes from decds_host_alloc, viewed as a numpy uint8 array (`.array`).
+
+    Every numpy view of `.array` keeps the block alive (view -> array -> ctypes block -> owner), so the
+    memory is released only when neither the HostBuffer nor any view remains. free() releases it early
+    and returns True only when no view is alive; with views alive it refuses (returns False) and the
+    block goes when the last view does."""
 
     def __init__(self, nbytes):
         p = ctypes.c_void_p()
         check(lib().decds_host_alloc(max(1, int(nbytes)), ctypes.byref(p)))
-        self._p = p
+        self._block = _PinnedBlock(p)
         self.nbytes = int(nbytes)
-        self.array = np.ctypeslib.as_array((ctypes.c_uint8 * max(1, self.nbytes)).from_address(p.value))[:self.nbytes]
+        blk = (ctypes.c_uint8 * max(1, self.nbytes)).from_address(p.value)
+        blk._owner = self._block
+        self.array = np.frombuffer(blk, np.uint8, count=self.nbytes)
 
     def free(self):
-        if self._p:
-            self.array = None
-            lib().decds_host_free(self._p)
-            self._p = None
-
-    def __del__(self):
-        try:
-            self.free()
-        except Exception:
-            pass
+        import sys
+        if self.array is None:
+            return True
+        # references to the array: the attribute, getrefcount's argument; anything more is a view
+        if sys.getrefcount(self.array) > 2:
+            return False
+        self.array = None
+        self._block.release()
+        return True
 
 
 class Blob:
@@ -108,14 +133,27 @@ class Blob:
 class RepairingBlob:
     """RepairingBlob (blob.rs:321-473)."""
 
-    def __init__(self, ctx, header):
-        """RepairingBlob::new(header) (blob.rs:341-353)"""
+    def __init__(self, ctxs, header, device_budget=None):
+        """RepairingBlob::new(header) (blob.rs:341-353) on one Context or a list of them (chunksets
+        sharded by contiguous index range, as Blob). device_budget: bytes of device memory per context
+        for accepted rows and decoding; rows past it spill to page-locked host memory."""
         roots = b"".join(header.chunkset_root_commitments)
+        arr, n_ctx = _ctx_array(ctxs)
         h = ctypes.c_void_p()
-        check(lib().decds_repairing_blob_new(ctx.handle, header.get_blob_size(), header.get_num_chunksets(),
-                                             header.get_root_commitment(), roots, ctypes.byref(h)))
+        check(lib().decds_repairing_blob_new_multi(arr, n_ctx, header.get_blob_size(), header.get_num_chunksets(),
+                                                   header.get_root_commitment(), roots, ctypes.byref(h)))
         self._h = h
         self.header = header
+        if device_budget is not None:
+            check(lib().decds_repairing_blob_set_device_budget(h, int(device_budget)))
+
+    def memory(self):
+        """device bytes, chunksets with rows on the device / spilled to host, spill bytes, decode
+        areas, contexts (decds_repairing_blob_memory)"""
+        st = (ctypes.c_uint64 * 6)()
+        check(lib().decds_repairing_blob_memory(self._h, st, 6))
+        keys = ("device_bytes", "device_chunksets", "spilled_chunksets", "spill_bytes", "decode_areas", "contexts")
+        return dict(zip(keys, [int(v) for v in st]))
 
     def add_chunk(self, chunk):
         """RepairingBlob::add_chunk (blob.rs:373-394): raises DecdsError(InvalidChunksetId |
@@ -147,7 +185,13 @@ class RepairingBlob:
 
     def add_rows(self, rows, ids, proofs, proof_len):
         """decds_repairing_blob_add_chunks on arrays: rows (m, F) uint8, ids (m, 2) uint64, proofs (m, proof_len*32)"""
-        m = ids.shape[0]
+        ids = np.ascontiguousarray(ids, dtype=np.uint64)
+        rows = np.ascontiguousarray(rows, dtype=np.uint8)
+        proofs = np.ascontiguousarray(proofs, dtype=np.uint8)
+        m = ids.shape[0] if ids.ndim == 2 else -1
+        if ids.shape != (m, 2) or rows.shape != (m, CODED_PIECE_BYTES) or proofs.shape != (m, proof_len * 32):
+            raise ValueError("add_rows needs rows (m, %d), ids (m, 2), proofs (m, %d); got %s, %s, %s"
+                             % (CODED_PIECE_BYTES, proof_len * 32, rows.shape, ids.shape, proofs.shape))
         status = np.empty(m, np.int32)
         vp = ctypes.c_void_p
         check(lib().decds_repairing_blob_add_chunks(self._h, m, vp(ids.ctypes.data), vp(rows.ctypes.data),

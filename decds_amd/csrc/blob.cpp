@@ -356,76 +356,242 @@ struct decds_blob {
 };
 
 // ---------------------------------------------------------------------------- RepairingBlob ----
+// Sharded over n contexts by contiguous chunkset index (shard_range, as decds_blob_new); each shard
+// owns its stream, bounce rings and memory. Accepted rows (10 x F per chunkset) go to a device row
+// slot while the shard is under its device budget, else to a page-locked host spill slot (the
+// reference keeps them in host RAM, chunkset.rs:129-135). Decoding uses a small pool of device
+// decode areas (a spilled chunkset's rows are staged there, and every decoded chunkset's 10 MiB
+// output waits there until get_repaired_chunkset copies it out); an area holding a decoded but not
+// yet fetched chunkset is reclaimed when needed (that chunkset is decoded again later).
 namespace {
 struct RbChunkset {
     uint8_t basis[K * K], piv[K];
     uint8_t cv[K][K];  // coding vectors of the accepted rows, acceptance order
     uint32_t rank = 0;
     bool repaired = false;  // get_repaired_chunkset took it (blob.rs:458-462: even if repair fails)
-    bool decoded = false;   // decoded on the device into its slot's result area
+    bool decoded = false;   // decoded on the device into decode area `area`
     int32_t dec_status = DECDS_OK;
-    int32_t slot = -1;
+    int32_t slot = -1;   // device row slot
+    int32_t hslot = -1;  // page-locked host spill slot
+    int32_t area = -1;   // decode area holding its decoded bytes
 };
 constexpr size_t RB_SLAB_SLOTS = 8;
-constexpr size_t RB_MAX_DECODE = 64;   // chunksets decoded per device batch
+constexpr size_t RB_MAX_DECODE = 64;   // chunksets decoded per device batch (and decode areas per shard)
 constexpr size_t RB_MAX_ROWS = 256;    // rows validated per device batch (decds_repairing_blob_add_chunks)
 constexpr size_t RB_ROWS_BYTES = (K * F + 255) & ~(size_t)255;
-constexpr size_t RB_SLOT_BYTES = RB_ROWS_BYTES + ((CS + 255) & ~(size_t)255);
+constexpr size_t RB_OUT_BYTES = (CS + 255) & ~(size_t)255;
+constexpr size_t RB_AREA_BYTES = RB_ROWS_BYTES + RB_OUT_BYTES;
+constexpr size_t RB_SLAB_BYTES = RB_SLAB_SLOTS * RB_ROWS_BYTES;
 // small device / pinned areas: plans, bases, statuses, valid flags
 constexpr size_t RB_SM_PLAN = 0, RB_SM_INB = RB_SM_PLAN + RB_MAX_DECODE * 128, RB_SM_OUTB = RB_SM_INB + RB_MAX_DECODE * 8,
                  RB_SM_STAT = RB_SM_OUTB + RB_MAX_DECODE * 8, RB_SM_VALID = RB_SM_STAT + RB_MAX_DECODE * 4,
                  RB_SM_BYTES = RB_SM_VALID + RB_MAX_ROWS;
-}  // namespace
 
-struct decds_repairing_blob {
+struct RbShard {
     decds_ctx *ctx = nullptr;
-    uint64_t byte_length = 0, n = 0;
-    uint8_t root[32];
-    std::vector<uint8_t> cs_roots;
-    std::vector<RbChunkset> cs;
+    size_t lo = 0, hi = 0;  // chunksets [lo, hi)
     hipStream_t s = nullptr;
     BounceRing in_ring, out_ring;
-    std::vector<uint8_t *> slabs;
-    std::vector<int32_t> free_slots;
+    std::vector<uint8_t *> slabs, hslabs, areas;
+    std::vector<int32_t> free_slots, free_hslots, free_areas;
+    std::vector<int64_t> area_owner;  // chunkset whose decoded bytes area a holds, -1 = free
+    size_t max_slabs = 0, max_areas = 1;  // from the device budget
+    uint64_t budget = 0;
     uint8_t *d_small = nullptr, *h_small = nullptr;
-    uint8_t *d_hdr = nullptr;     // chunkset roots (n x 32) + blob root (32), for decds_validate_batch
-    uint8_t *d_batch = nullptr;   // RB_MAX_ROWS rows + ids + proofs + digests of one validation batch
+    uint8_t *d_hdr = nullptr;    // chunkset roots (n x 32) + blob root (32), for decds_validate_batch
+    uint8_t *d_batch = nullptr;  // RB_MAX_ROWS rows + ids + proofs + digests of one validation batch
     size_t batch_plen = 0;
-    ~decds_repairing_blob() {
+    uint64_t batch_bytes = 0;
+
+    ~RbShard() {
         if (ctx) (void)hipSetDevice(ctx->device);
         if (s) (void)hipStreamSynchronize(s);
         in_ring.abandon();
         out_ring.abandon();
         for (uint8_t *p : slabs) (void)hipFree(p);
+        for (uint8_t *p : areas) (void)hipFree(p);
+        for (uint8_t *p : hslabs) host_pinned_free(p, RB_SLAB_BYTES);
         for (uint8_t *p : {d_small, d_hdr, d_batch})
             if (p) (void)hipFree(p);
         if (h_small) (void)hipHostFree(h_small);
         if (s) (void)hipStreamDestroy(s);
     }
-    uint8_t *slot_rows(int32_t slot) const {
-        return slabs[slot / RB_SLAB_SLOTS] + (slot % RB_SLAB_SLOTS) * RB_SLOT_BYTES;
+    // device budget per context: a quarter for decode areas (at least one), the rest for row slots
+    void set_budget(uint64_t bytes) {
+        budget = bytes;
+        max_areas = std::max<size_t>(1, std::min<size_t>(RB_MAX_DECODE, (size_t)(bytes / 4 / RB_AREA_BYTES)));
+        const uint64_t rest = bytes > max_areas * RB_AREA_BYTES ? bytes - max_areas * RB_AREA_BYTES : 0;
+        max_slabs = (size_t)(rest / RB_SLAB_BYTES);
     }
-    uint8_t *slot_out(int32_t slot) const { return slot_rows(slot) + RB_ROWS_BYTES; }
-    size_t chunkset_size(size_t c) const {  // BlobHeader::get_chunkset_size (blob.rs:84-94)
-        const uint64_t from = c * CS;
-        return (size_t)(std::min<uint64_t>(from + CS, byte_length) - from);
+    uint64_t device_bytes() const {
+        return slabs.size() * RB_SLAB_BYTES + areas.size() * RB_AREA_BYTES + batch_bytes + RB_SM_BYTES;
     }
+    uint8_t *slot_rows(int32_t slot) const { return slabs[slot / RB_SLAB_SLOTS] + (slot % RB_SLAB_SLOTS) * RB_ROWS_BYTES; }
+    uint8_t *hslot_rows(int32_t h) const { return hslabs[h / RB_SLAB_SLOTS] + (h % RB_SLAB_SLOTS) * RB_ROWS_BYTES; }
+    uint8_t *area_rows(int32_t a) const { return areas[a]; }
+    uint8_t *area_out(int32_t a) const { return areas[a] + RB_ROWS_BYTES; }
+
+    // a device row slot while under budget, else a host spill slot
     int take_slot(RbChunkset &c) {
-        if (c.slot >= 0) return DECDS_OK;
-        if (free_slots.empty()) {
+        if (c.slot >= 0 || c.hslot >= 0) return DECDS_OK;
+        if (free_slots.empty() && slabs.size() < max_slabs) {
             uint8_t *p = nullptr;
-            hipError_t e = hipMalloc(reinterpret_cast<void **>(&p), RB_SLAB_SLOTS * RB_SLOT_BYTES);
-            if (e) return decds_hip_error(e, "hipMalloc (repair slots)");
-            slabs.push_back(p);
-            for (size_t i = RB_SLAB_SLOTS; i-- > 0;) free_slots.push_back((int32_t)((slabs.size() - 1) * RB_SLAB_SLOTS + i));
+            if (hipMalloc(reinterpret_cast<void **>(&p), RB_SLAB_BYTES) == hipSuccess) {
+                slabs.push_back(p);
+                for (size_t i = RB_SLAB_SLOTS; i-- > 0;) free_slots.push_back((int32_t)((slabs.size() - 1) * RB_SLAB_SLOTS + i));
+            } else {
+                (void)hipGetLastError();  // device memory ran out below the budget: spill from here on
+                max_slabs = slabs.size();
+            }
         }
-        c.slot = free_slots.back();
-        free_slots.pop_back();
+        if (!free_slots.empty()) {
+            c.slot = free_slots.back();
+            free_slots.pop_back();
+            return DECDS_OK;
+        }
+        if (free_hslots.empty()) {
+            void *p = nullptr;
+            hipError_t e = host_pinned_alloc(RB_SLAB_BYTES, &p);
+            if (e) return decds_hip_error(e, "page-locked host memory for spilled rows");
+            hslabs.push_back(static_cast<uint8_t *>(p));
+            for (size_t i = RB_SLAB_SLOTS; i-- > 0;) free_hslots.push_back((int32_t)((hslabs.size() - 1) * RB_SLAB_SLOTS + i));
+        }
+        c.hslot = free_hslots.back();
+        free_hslots.pop_back();
         return DECDS_OK;
     }
     void drop_slot(RbChunkset &c) {
         if (c.slot >= 0) free_slots.push_back(c.slot);
-        c.slot = -1;
+        if (c.hslot >= 0) free_hslots.push_back(c.hslot);
+        c.slot = c.hslot = -1;
+    }
+    void drop_area(RbChunkset &c) {
+        if (c.area >= 0) {
+            area_owner[c.area] = -1;
+            free_areas.push_back(c.area);
+        }
+        c.area = -1;
+        c.decoded = false;
+    }
+    // a decode area: a free one, a new one within the budget, or (evict) one whose decoded chunkset
+    // has not been fetched yet; -1 when none (*err set only when not even one area can be allocated)
+    int32_t take_area(std::vector<RbChunkset> &cs, bool evict, int *err) {
+        if (!free_areas.empty()) {
+            const int32_t a = free_areas.back();
+            free_areas.pop_back();
+            return a;
+        }
+        if (areas.size() < max_areas) {
+            uint8_t *p = nullptr;
+            if (hipMalloc(reinterpret_cast<void **>(&p), RB_AREA_BYTES) == hipSuccess) {
+                areas.push_back(p);
+                area_owner.push_back(-1);
+                return (int32_t)(areas.size() - 1);
+            }
+            (void)hipGetLastError();
+            max_areas = std::max<size_t>(1, areas.size());
+            if (areas.empty()) {
+                *err = decds_set_error(DECDS_ERR_OUT_OF_DEVICE_MEMORY,
+                                       "device %d has no memory left for a %zu-byte decode area", ctx->device, RB_AREA_BYTES);
+                return -1;
+            }
+        }
+        if (!evict) return -1;
+        for (size_t a = 0; a < areas.size(); a++) {
+            const int64_t o = area_owner[a];
+            if (o >= 0) {
+                cs[o].area = -1;
+                cs[o].decoded = false;  // decoded again when asked for
+                area_owner[a] = -1;
+                return (int32_t)a;
+            }
+        }
+        return -1;
+    }
+    // decode `first` and further ready, undecoded chunksets of this shard for which a decode area is
+    // free, in one launch (the decode kernel's gather form)
+    int decode_ready(std::vector<RbChunkset> &cs, size_t first) {
+        int err = DECDS_OK;
+        std::vector<size_t> todo;
+        std::vector<int32_t> area;
+        const int32_t a0 = take_area(cs, true, &err);
+        if (a0 < 0) return err ? err : decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "no decode area");
+        todo.push_back(first);
+        area.push_back(a0);
+        for (size_t c = lo; c < hi && todo.size() < RB_MAX_DECODE; c++) {
+            if (c == first || cs[c].rank != K || cs[c].decoded || cs[c].repaired) continue;
+            int e2 = DECDS_OK;
+            const int32_t a = take_area(cs, false, &e2);
+            if (a < 0) break;
+            todo.push_back(c);
+            area.push_back(a);
+        }
+        const size_t m = todo.size();
+        RepairPlan *plans = reinterpret_cast<RepairPlan *>(h_small + RB_SM_PLAN);
+        uint64_t *inb = reinterpret_cast<uint64_t *>(h_small + RB_SM_INB), *outb = reinterpret_cast<uint64_t *>(h_small + RB_SM_OUTB);
+        hipError_t e;
+        int st = DECDS_OK;
+        for (size_t i = 0; i < m && st == DECDS_OK; i++) {
+            RbChunkset &c = cs[todo[i]];
+            c.area = area[i];
+            area_owner[area[i]] = (int64_t)todo[i];
+            std::memset(&plans[i], 0, sizeof(RepairPlan));
+            for (uint32_t k = 0; k < K; k++) plans[i].sel[k] = (uint8_t)k;
+            plans[i].rank = K;
+            if (!host_gf_invert(&c.cv[0][0], plans[i].inv, ctx->poly)) {
+                st = decds_set_error(DECDS_ERR_CHUNKSET_REPAIRING_FAILED, "accepted coding vectors are singular");
+                break;
+            }
+            if (c.slot >= 0) {
+                inb[i] = reinterpret_cast<uint64_t>(slot_rows(c.slot));
+            } else {  // spilled: stage its rows into the area (page-locked host memory: direct DMA)
+                if ((e = hipMemcpyAsync(area_rows(area[i]), hslot_rows(c.hslot), K * F, hipMemcpyHostToDevice, s)))
+                    st = decds_hip_error(e, "H2D (spilled rows)");
+                inb[i] = reinterpret_cast<uint64_t>(area_rows(area[i]));
+            }
+            outb[i] = reinterpret_cast<uint64_t>(area_out(area[i]));
+        }
+        if (st == DECDS_OK) {
+            if ((e = hipMemcpyAsync(d_small, h_small, RB_SM_STAT, hipMemcpyHostToDevice, s)) ||
+                (e = hipMemsetAsync(d_small + RB_SM_STAT, 0, m * 4, s)))
+                st = decds_hip_error(e, "H2D (plans)");
+        }
+        if (st == DECDS_OK &&
+            (e = launch_decode(ctx->geom, nullptr, F, m, d_small + RB_SM_PLAN, nullptr,
+                               reinterpret_cast<int32_t *>(d_small + RB_SM_STAT), reinterpret_cast<const uint64_t *>(d_small + RB_SM_INB),
+                               reinterpret_cast<const uint64_t *>(d_small + RB_SM_OUTB), ctx->poly, ctx->marker, s)))
+            st = decds_hip_error(e, "rlnc_decode_kernel launch");
+        if (st == DECDS_OK &&
+            ((e = hipMemcpyAsync(h_small + RB_SM_STAT, d_small + RB_SM_STAT, m * 4, hipMemcpyDeviceToHost, s)) ||
+             (e = hipStreamSynchronize(s))))
+            st = decds_hip_error(e, "D2H (statuses)");
+        if (st != DECDS_OK) {
+            for (size_t i = 0; i < m; i++) drop_area(cs[todo[i]]);
+            return st;
+        }
+        const int32_t *stat = reinterpret_cast<const int32_t *>(h_small + RB_SM_STAT);
+        for (size_t i = 0; i < m; i++) {
+            cs[todo[i]].decoded = true;
+            cs[todo[i]].dec_status = stat[i];
+        }
+        return DECDS_OK;
+    }
+};
+}  // namespace
+
+struct decds_repairing_blob {
+    uint64_t byte_length = 0, n = 0, per = 1;
+    uint8_t root[32];
+    std::vector<uint8_t> cs_roots;
+    std::vector<RbChunkset> cs;
+    std::vector<RbShard *> shards;
+    ~decds_repairing_blob() {
+        for (RbShard *sh : shards) delete sh;
+    }
+    RbShard &shard_of(uint64_t c) { return *shards[c / per]; }
+    size_t chunkset_size(size_t c) const {  // BlobHeader::get_chunkset_size (blob.rs:84-94)
+        const uint64_t from = c * CS;
+        return (size_t)(std::min<uint64_t>(from + CS, byte_length) - from);
     }
     // the routing checks of RepairingBlob::add_chunk that precede validation (blob.rs:374-381)
     int route_check(uint64_t cs_id) {
@@ -439,7 +605,7 @@ struct decds_repairing_blob {
     }
     // after validation (blob.rs:383-388): ready check, then add_chunk_unvalidated's rank step
     // (chunkset.rs:177-183). On success the row's coding vector is recorded and its slot row index
-    // (rank - 1) returned through *row.
+    // (rank - 1) returned through *row; the caller then stores the row (store_row).
     int accept(uint64_t cs_id, const uint8_t *cv, size_t len, uint32_t *row) {
         RbChunkset &c = cs[cs_id];
         if (c.rank == K)
@@ -449,50 +615,24 @@ struct decds_repairing_blob {
             return decds_set_error(DECDS_ERR_CHUNK_DECODING_FAILED,
                                    "decoding chunk for chunkset %llu failed: invalid piece length %zu",
                                    (unsigned long long)cs_id, len);
-        int s = take_slot(c);
-        if (s) return s;
-        if (!decds_rank_push(c.basis, c.piv, &c.rank, cv, ctx->poly))
+        RbShard &sh = shard_of(cs_id);
+        // the rank step on a copy: a slot is taken only for a useful piece, and a failed slot
+        // allocation leaves the chunkset as it was
+        uint8_t basis[K * K], piv[K];
+        uint32_t rank = c.rank;
+        std::memcpy(basis, c.basis, sizeof(basis));
+        std::memcpy(piv, c.piv, sizeof(piv));
+        if (!decds_rank_push(basis, piv, &rank, cv, sh.ctx->poly))
             return decds_set_error(DECDS_ERR_CHUNK_DECODING_FAILED,
                                    "decoding chunk for chunkset %llu failed: received piece is not useful",
                                    (unsigned long long)cs_id);
+        int s = sh.take_slot(c);
+        if (s) return s;
+        std::memcpy(c.basis, basis, sizeof(basis));
+        std::memcpy(c.piv, piv, sizeof(piv));
+        c.rank = rank;
         std::memcpy(c.cv[c.rank - 1], cv, K);
         *row = c.rank - 1;
-        return DECDS_OK;
-    }
-    // decode `first` and up to RB_MAX_DECODE - 1 further ready, undecoded chunksets in one launch
-    int decode_ready(size_t first) {
-        std::vector<size_t> todo{first};
-        for (size_t c = 0; c < n && todo.size() < RB_MAX_DECODE; c++)
-            if (c != first && cs[c].rank == K && !cs[c].decoded && !cs[c].repaired) todo.push_back(c);
-        const size_t m = todo.size();
-        RepairPlan *plans = reinterpret_cast<RepairPlan *>(h_small + RB_SM_PLAN);
-        uint64_t *inb = reinterpret_cast<uint64_t *>(h_small + RB_SM_INB), *outb = reinterpret_cast<uint64_t *>(h_small + RB_SM_OUTB);
-        for (size_t i = 0; i < m; i++) {
-            RbChunkset &c = cs[todo[i]];
-            std::memset(&plans[i], 0, sizeof(RepairPlan));
-            for (uint32_t k = 0; k < K; k++) plans[i].sel[k] = (uint8_t)k;
-            plans[i].rank = K;
-            if (!host_gf_invert(&c.cv[0][0], plans[i].inv, ctx->poly))
-                return decds_set_error(DECDS_ERR_CHUNKSET_REPAIRING_FAILED, "accepted coding vectors are singular");
-            inb[i] = reinterpret_cast<uint64_t>(slot_rows(c.slot));
-            outb[i] = reinterpret_cast<uint64_t>(slot_out(c.slot));
-        }
-        hipError_t e;
-        if ((e = hipMemcpyAsync(d_small, h_small, RB_SM_STAT, hipMemcpyHostToDevice, s)) ||
-            (e = hipMemsetAsync(d_small + RB_SM_STAT, 0, m * 4, s)))
-            return decds_hip_error(e, "H2D (plans)");
-        e = launch_decode(ctx->geom, nullptr, F, m, d_small + RB_SM_PLAN, nullptr,
-                          reinterpret_cast<int32_t *>(d_small + RB_SM_STAT), reinterpret_cast<const uint64_t *>(d_small + RB_SM_INB),
-                          reinterpret_cast<const uint64_t *>(d_small + RB_SM_OUTB), ctx->poly, ctx->marker, s);
-        if (e) return decds_hip_error(e, "rlnc_decode_kernel launch");
-        if ((e = hipMemcpyAsync(h_small + RB_SM_STAT, d_small + RB_SM_STAT, m * 4, hipMemcpyDeviceToHost, s)) ||
-            (e = hipStreamSynchronize(s)))
-            return decds_hip_error(e, "D2H (statuses)");
-        const int32_t *st = reinterpret_cast<const int32_t *>(h_small + RB_SM_STAT);
-        for (size_t i = 0; i < m; i++) {
-            cs[todo[i]].decoded = true;
-            cs[todo[i]].dec_status = st[i];
-        }
         return DECDS_OK;
     }
 };
@@ -651,36 +791,92 @@ int decds_blob_get_share(const decds_blob *b, size_t share_id, uint8_t *data, si
 void decds_blob_free(decds_blob *b) { delete b; }
 
 // ---- RepairingBlob ----------------------------------------------------------------------------
-int decds_repairing_blob_new(decds_ctx *ctx, uint64_t byte_length, uint64_t num_chunksets, const uint8_t *root,
-                             const uint8_t *chunkset_roots, decds_repairing_blob **out) {
+static uint64_t rb_default_budget(decds_ctx *const *ctxs, size_t n_ctx, size_t g) {
+    // DECDS_RB_DEVICE_MB, else half the device's free memory shared by the shards on that device
+    if (const char *env = getenv("DECDS_RB_DEVICE_MB")) return (uint64_t)strtoull(env, nullptr, 10) << 20;
+    size_t fr = 0, total = 0;
+    if (hipMemGetInfo(&fr, &total) != hipSuccess) {
+        (void)hipGetLastError();
+        return (uint64_t)4 << 30;
+    }
+    size_t same = 0;
+    for (size_t k = 0; k < n_ctx; k++) same += ctxs[k]->device == ctxs[g]->device;
+    return (uint64_t)fr / 2 / std::max<size_t>(1, same);
+}
+
+int decds_repairing_blob_new_multi(decds_ctx *const *ctxs, size_t n_ctx, uint64_t byte_length, uint64_t num_chunksets,
+                                   const uint8_t *root, const uint8_t *chunkset_roots, decds_repairing_blob **out) {
     if (!out) return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "null out pointer");
     *out = nullptr;
+    if (!ctxs || n_ctx == 0) return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "no contexts");
+    for (size_t g = 0; g < n_ctx; g++)
+        if (!ctxs[g]) return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "null context %zu", g);
     if (!root || (num_chunksets && !chunkset_roots) || num_chunksets == 0)
         return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "null header field or no chunksets");
     if (byte_length > num_chunksets * CS || byte_length <= (num_chunksets - 1) * CS)
         return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "blob length %llu inconsistent with %llu chunksets",
                                (unsigned long long)byte_length, (unsigned long long)num_chunksets);
-    int s = decds_ctx_bind(ctx);
-    if (s) return s;
     auto *rb = new decds_repairing_blob;
-    rb->ctx = ctx;
     rb->byte_length = byte_length;
     rb->n = num_chunksets;
+    // the contiguous chunkset-index plan of decds_blob_new / run_shards
+    rb->per = (num_chunksets + n_ctx - 1) / n_ctx;
     std::memcpy(rb->root, root, 32);
     rb->cs_roots.assign(chunkset_roots, chunkset_roots + num_chunksets * 32);
     rb->cs.resize(num_chunksets);
-    hipError_t e;
-    if ((e = hipStreamCreateWithFlags(&rb->s, hipStreamNonBlocking)) ||
-        (e = hipMalloc(reinterpret_cast<void **>(&rb->d_small), RB_SM_BYTES)) ||
-        (e = hipHostMalloc(reinterpret_cast<void **>(&rb->h_small), RB_SM_BYTES, DECDS_HOST_MALLOC_FLAGS)) ||
-        (e = hipMalloc(reinterpret_cast<void **>(&rb->d_hdr), (num_chunksets + 1) * 32)) ||
-        (e = hipMemcpyAsync(rb->d_hdr, chunkset_roots, num_chunksets * 32, hipMemcpyHostToDevice, rb->s)) ||
-        (e = hipMemcpyAsync(rb->d_hdr + num_chunksets * 32, root, 32, hipMemcpyHostToDevice, rb->s)) ||
-        (e = hipStreamSynchronize(rb->s))) {
-        delete rb;
-        return decds_hip_error(e, "RepairingBlob setup");
+    for (size_t g = 0; g * rb->per < num_chunksets; g++) {
+        auto *sh = new RbShard;
+        rb->shards.push_back(sh);
+        sh->ctx = ctxs[g];
+        sh->lo = g * rb->per;
+        sh->hi = std::min<uint64_t>(sh->lo + rb->per, num_chunksets);
+        int st = decds_ctx_bind(sh->ctx);
+        if (st) {
+            delete rb;
+            return st;
+        }
+        sh->set_budget(rb_default_budget(ctxs, n_ctx, g));
+        hipError_t e;
+        if ((e = hipStreamCreateWithFlags(&sh->s, hipStreamNonBlocking)) ||
+            (e = hipMalloc(reinterpret_cast<void **>(&sh->d_small), RB_SM_BYTES)) ||
+            (e = hipHostMalloc(reinterpret_cast<void **>(&sh->h_small), RB_SM_BYTES, DECDS_HOST_MALLOC_FLAGS)) ||
+            (e = hipMalloc(reinterpret_cast<void **>(&sh->d_hdr), (num_chunksets + 1) * 32)) ||
+            (e = hipMemcpyAsync(sh->d_hdr, chunkset_roots, num_chunksets * 32, hipMemcpyHostToDevice, sh->s)) ||
+            (e = hipMemcpyAsync(sh->d_hdr + num_chunksets * 32, root, 32, hipMemcpyHostToDevice, sh->s)) ||
+            (e = hipStreamSynchronize(sh->s))) {
+            delete rb;
+            return decds_hip_error(e, "RepairingBlob setup");
+        }
     }
     *out = rb;
+    return DECDS_OK;
+}
+
+int decds_repairing_blob_new(decds_ctx *ctx, uint64_t byte_length, uint64_t num_chunksets, const uint8_t *root,
+                             const uint8_t *chunkset_roots, decds_repairing_blob **out) {
+    decds_ctx *const ctxs[1] = {ctx};
+    return decds_repairing_blob_new_multi(ctxs, 1, byte_length, num_chunksets, root, chunkset_roots, out);
+}
+
+int decds_repairing_blob_set_device_budget(decds_repairing_blob *rb, uint64_t bytes_per_context) {
+    if (!rb) return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "null repairing blob");
+    for (RbShard *sh : rb->shards) sh->set_budget(bytes_per_context);
+    return DECDS_OK;
+}
+
+int decds_repairing_blob_memory(const decds_repairing_blob *rb, uint64_t *stats, size_t n_stats) {
+    if (!rb || !stats) return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "null argument");
+    uint64_t v[6] = {0, 0, 0, 0, 0, (uint64_t)rb->shards.size()};
+    for (const RbShard *sh : rb->shards) {
+        v[0] += sh->device_bytes();
+        v[3] += sh->hslabs.size() * RB_SLAB_BYTES;
+        v[4] += sh->areas.size();
+    }
+    for (const RbChunkset &c : rb->cs) {
+        v[1] += c.slot >= 0;
+        v[2] += c.hslot >= 0;
+    }
+    for (size_t i = 0; i < n_stats && i < 6; i++) stats[i] = v[i];
     return DECDS_OK;
 }
 
@@ -689,18 +885,19 @@ int decds_repairing_blob_add_chunk(decds_repairing_blob *rb, uint64_t chunkset_i
     if (!rb) return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "null repairing blob");
     int s = rb->route_check(chunkset_id);
     if (s) return s;
+    RbShard &sh = rb->shard_of(chunkset_id);
     // BlobHeader::validate_chunk (blob.rs:211-215): blob-level proof at the global chunk id, the
     // chunkset id in range, then the first 4 hashes against the chunkset root (chunk.rs:88-110)
     bool ok = proof && proof_len >= PROOF_SIZE && (data || len == 0);
-    if ((s = decds_ctx_bind(rb->ctx))) return s;
+    if ((s = decds_ctx_bind(sh.ctx))) return s;
     // a full-length row is copied into a staging piece while it is hashed (the copy is only sent to
-    // the device if the chunk is accepted); the caller's buffer is free when this returns
+    // the device if the chunk is accepted into a device slot); the caller's buffer is free on return
     int piece = -1;
     uint8_t *staged = nullptr;
     if (ok) {
         uint8_t leaf[32];
         if (len == F && b3h::simd_available()) {
-            hipError_t e = rb->in_ring.stage(&piece, &staged);
+            hipError_t e = sh.in_ring.stage(&piece, &staged);
             if (e) return decds_hip_error(e, "staging piece");
             constexpr size_t HALF = (F + 1) / 2;
             const std::function<void(size_t)> copy = [&](size_t h) {
@@ -718,66 +915,123 @@ int decds_repairing_blob_add_chunk(decds_repairing_blob *rb, uint64_t chunkset_i
                                (unsigned long long)chunkset_id);
     uint32_t row;
     if ((s = rb->accept(chunkset_id, data, len, &row))) return s;
-    uint8_t *dst = rb->slot_rows(rb->cs[chunkset_id].slot) + row * F;
-    hipError_t e = staged ? rb->in_ring.commit(piece, dst, F, rb->s) : rb->in_ring.h2d(dst, data, F, rb->s);
+    const RbChunkset &c = rb->cs[chunkset_id];
+    if (c.hslot >= 0) {  // spilled: the row stays in page-locked host memory until its decode
+        std::memcpy(sh.hslot_rows(c.hslot) + row * F, staged ? staged : data, F);
+        return DECDS_OK;
+    }
+    uint8_t *dst = sh.slot_rows(c.slot) + row * F;
+    hipError_t e = staged ? sh.in_ring.commit(piece, dst, F, sh.s) : sh.in_ring.h2d(dst, data, F, sh.s);
     return e ? decds_hip_error(e, "H2D (accepted row)") : DECDS_OK;
+}
+
+// decds_repairing_blob_add_chunks for the rows `idx` (arrival order) of one shard
+static int rb_add_rows_shard(decds_repairing_blob *rb, RbShard &sh, const std::vector<size_t> &idx, const uint64_t *ids,
+                             const uint8_t *rows, const uint8_t *proofs, size_t proof_len, int32_t *status) {
+    int s = decds_ctx_bind(sh.ctx);
+    if (s) return s;
+    const size_t P = proof_len * 32;
+    // device batch area: RB_MAX_ROWS rows | ids | proofs (sized for the longest proof seen) | digests
+    hipError_t e;
+    if (!sh.d_batch || sh.batch_plen < proof_len) {
+        if (sh.d_batch) {
+            (void)hipStreamSynchronize(sh.s);
+            (void)hipFree(sh.d_batch);
+            sh.d_batch = nullptr;
+            sh.batch_bytes = 0;
+        }
+        const size_t total = RB_MAX_ROWS * (F + 16 + P + 32);
+        if ((e = hipMalloc(reinterpret_cast<void **>(&sh.d_batch), total))) {
+            (void)hipGetLastError();
+            return decds_set_error(DECDS_ERR_OUT_OF_DEVICE_MEMORY, "device %d has no memory left for a %zu-byte "
+                                   "validation batch", sh.ctx->device, total);
+        }
+        sh.batch_plen = proof_len;
+        sh.batch_bytes = total;
+    }
+    const size_t a_ids = RB_MAX_ROWS * F, a_prf = a_ids + RB_MAX_ROWS * 16, a_dig = a_prf + RB_MAX_ROWS * sh.batch_plen * 32;
+    const size_t n_rows = idx.empty() ? 0 : idx.back() + 1;
+    HostUse urows(rows, n_rows * F), uids(ids, n_rows * 16), uprf(proofs, n_rows * P);
+    for (size_t r0 = 0; r0 < idx.size(); r0 += RB_MAX_ROWS) {
+        const size_t m = std::min(RB_MAX_ROWS, idx.size() - r0);
+        // the batch's rows, ids and proofs, copied in runs of consecutive arrival indices
+        for (size_t i = 0; i < m;) {
+            size_t j = i + 1;
+            while (j < m && idx[r0 + j] == idx[r0 + j - 1] + 1) j++;
+            const size_t a = idx[r0 + i], len = j - i;
+            if ((e = copy_h2d(sh.d_batch + i * F, rows + a * F, len * F, urows.pinned(), sh.in_ring, sh.s)) ||
+                (e = copy_h2d(sh.d_batch + a_ids + i * 16, reinterpret_cast<const uint8_t *>(ids + 2 * a), len * 16,
+                              uids.pinned(), sh.in_ring, sh.s)) ||
+                (P && (e = copy_h2d(sh.d_batch + a_prf + i * P, proofs + a * P, len * P, uprf.pinned(), sh.in_ring, sh.s))))
+                return decds_hip_error(e, "H2D (rows)");
+            i = j;
+        }
+        // BlobHeader::validate_chunk for the whole batch on the device (one digest per row, both proofs)
+        if ((s = decds_validate_batch(sh.ctx, sh.d_batch, F, m, reinterpret_cast<const uint64_t *>(sh.d_batch + a_ids),
+                                      sh.d_batch + a_prf, proof_len, sh.d_hdr, rb->n, sh.d_hdr + rb->n * 32,
+                                      sh.d_batch + a_dig, sh.d_small + RB_SM_VALID, sh.s)))
+            return s;
+        if ((e = hipMemcpyAsync(sh.h_small + RB_SM_VALID, sh.d_small + RB_SM_VALID, m, hipMemcpyDeviceToHost, sh.s)) ||
+            (e = hipStreamSynchronize(sh.s)))
+            return decds_hip_error(e, "D2H (verdicts)");
+        // RepairingBlob::add_chunk's checks in arrival order (blob.rs:373-394)
+        for (size_t i = 0; i < m; i++) {
+            const size_t a = idx[r0 + i];
+            const uint64_t cid = ids[2 * a];
+            int st = rb->route_check(cid);
+            if (st == DECDS_OK && !sh.h_small[RB_SM_VALID + i])
+                st = decds_set_error(DECDS_ERR_INVALID_PROOF_IN_CHUNK, "invalid proof in chunk of chunkset %llu",
+                                     (unsigned long long)cid);
+            uint32_t row = 0;
+            if (st == DECDS_OK) st = rb->accept(cid, rows + a * F, F, &row);
+            if (st == DECDS_OK) {
+                const RbChunkset &c = rb->cs[cid];
+                if (c.hslot >= 0)
+                    std::memcpy(sh.hslot_rows(c.hslot) + row * F, rows + a * F, F);
+                else if ((e = hipMemcpyAsync(sh.slot_rows(c.slot) + row * F, sh.d_batch + i * F, F, hipMemcpyDeviceToDevice,
+                                             sh.s)))
+                    return decds_hip_error(e, "D2D (accepted row)");
+            }
+            status[a] = st;
+        }
+    }
+    if ((e = hipStreamSynchronize(sh.s))) return decds_hip_error(e, "hipStreamSynchronize");
+    return DECDS_OK;
 }
 
 int decds_repairing_blob_add_chunks(decds_repairing_blob *rb, size_t n_rows, const uint64_t *ids, const uint8_t *rows,
                                     const uint8_t *proofs, size_t proof_len, int32_t *status) {
     if (!rb || (n_rows && (!ids || !rows || !status))) return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "null argument");
     if (n_rows && proof_len && !proofs) return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "null proofs");
-    int s = decds_ctx_bind(rb->ctx);
-    if (s) return s;
-    decds_ctx *ctx = rb->ctx;
-    const size_t P = proof_len * 32;
-    // device batch area: RB_MAX_ROWS rows | ids | proofs (sized for the longest proof seen) | digests
-    hipError_t e;
-    if (!rb->d_batch || rb->batch_plen < proof_len) {
-        if (rb->d_batch) {
-            (void)hipStreamSynchronize(rb->s);
-            (void)hipFree(rb->d_batch);
-            rb->d_batch = nullptr;
-        }
-        const size_t total = RB_MAX_ROWS * (F + 16 + P + 32);
-        if ((e = hipMalloc(reinterpret_cast<void **>(&rb->d_batch), total))) return decds_hip_error(e, "hipMalloc");
-        rb->batch_plen = proof_len;
+    // rows go to the shard of their claimed chunkset (the reference routes by the chunk's own id,
+    // blob.rs:376); an id out of range is refused here, before validation, as blob.rs:374-377
+    std::vector<std::vector<size_t>> part(rb->shards.size());
+    for (size_t a = 0; a < n_rows; a++) {
+        const uint64_t cid = ids[2 * a];
+        if (cid >= rb->n)
+            status[a] = rb->route_check(cid);
+        else
+            part[cid / rb->per].push_back(a);
     }
-    const size_t a_ids = RB_MAX_ROWS * F, a_prf = a_ids + RB_MAX_ROWS * 16,
-                 a_dig = a_prf + RB_MAX_ROWS * rb->batch_plen * 32;
-    HostUse urows(rows, n_rows * F), uids(ids, n_rows * 16), uprf(proofs, n_rows * P);
-    for (size_t r0 = 0; r0 < n_rows; r0 += RB_MAX_ROWS) {
-        const size_t m = std::min(RB_MAX_ROWS, n_rows - r0);
-        // BlobHeader::validate_chunk for the whole batch on the device (one digest per row, both proofs)
-        if ((e = copy_h2d(rb->d_batch, rows + r0 * F, m * F, urows.pinned(), rb->in_ring, rb->s)) ||
-            (e = copy_h2d(rb->d_batch + a_ids, reinterpret_cast<const uint8_t *>(ids + 2 * r0), m * 16, uids.pinned(),
-                          rb->in_ring, rb->s)) ||
-            (P && (e = copy_h2d(rb->d_batch + a_prf, proofs + r0 * P, m * P, uprf.pinned(), rb->in_ring, rb->s))))
-            return decds_hip_error(e, "H2D (rows)");
-        if ((s = decds_validate_batch(ctx, rb->d_batch, F, m, reinterpret_cast<const uint64_t *>(rb->d_batch + a_ids),
-                                      rb->d_batch + a_prf, proof_len, rb->d_hdr, rb->n, rb->d_hdr + rb->n * 32,
-                                      rb->d_batch + a_dig, rb->d_small + RB_SM_VALID, rb->s)))
-            return s;
-        if ((e = hipMemcpyAsync(rb->h_small + RB_SM_VALID, rb->d_small + RB_SM_VALID, m, hipMemcpyDeviceToHost, rb->s)) ||
-            (e = hipStreamSynchronize(rb->s)))
-            return decds_hip_error(e, "D2H (verdicts)");
-        // RepairingBlob::add_chunk's checks in arrival order (blob.rs:373-394)
-        for (size_t i = 0; i < m; i++) {
-            const uint64_t cid = ids[2 * (r0 + i)];
-            int st = rb->route_check(cid);
-            if (st == DECDS_OK && !rb->h_small[RB_SM_VALID + i])
-                st = decds_set_error(DECDS_ERR_INVALID_PROOF_IN_CHUNK, "invalid proof in chunk of chunkset %llu",
-                                     (unsigned long long)cid);
-            uint32_t row = 0;
-            if (st == DECDS_OK) st = rb->accept(cid, rows + (r0 + i) * F, F, &row);
-            if (st == DECDS_OK &&
-                (e = hipMemcpyAsync(rb->slot_rows(rb->cs[cid].slot) + row * F, rb->d_batch + i * F, F,
-                                    hipMemcpyDeviceToDevice, rb->s)))
-                return decds_hip_error(e, "D2D (accepted row)");
-            status[r0 + i] = st;
-        }
+    std::vector<int> st(rb->shards.size(), DECDS_OK);
+    std::vector<std::string> msg(rb->shards.size());
+    std::vector<std::thread> th;
+    size_t busy = 0;
+    for (size_t g = 0; g < part.size(); g++) busy += !part[g].empty();
+    for (size_t g = 0; g < part.size(); g++) {
+        if (part[g].empty()) continue;
+        auto run = [&, g] {
+            st[g] = rb_add_rows_shard(rb, *rb->shards[g], part[g], ids, rows, proofs, proof_len, status);
+            if (st[g] != DECDS_OK) msg[g] = decds_last_error();
+        };
+        if (busy == 1)
+            run();
+        else
+            th.emplace_back(run);
     }
-    if ((e = hipStreamSynchronize(rb->s))) return decds_hip_error(e, "hipStreamSynchronize");
+    for (auto &t : th) t.join();
+    for (size_t g = 0; g < part.size(); g++)
+        if (st[g] != DECDS_OK) return busy == 1 ? st[g] : decds_set_error(st[g], "shard %zu: %s", g, msg[g].c_str());
     return DECDS_OK;
 }
 
@@ -811,23 +1065,26 @@ int decds_repairing_blob_get_repaired_chunkset(decds_repairing_blob *rb, size_t 
     if (c.rank != K) return decds_set_error(DECDS_ERR_CHUNKSET_NOT_YET_READY, "chunkset %zu is not ready to repair", chunkset_id);
     const size_t size = rb->chunkset_size(chunkset_id);
     if (!out || out_cap < size) return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "out buffer < %zu", size);
-    int s = decds_ctx_bind(rb->ctx);
+    RbShard &sh = rb->shard_of(chunkset_id);
+    int s = decds_ctx_bind(sh.ctx);
     if (s) return s;
-    if (!c.decoded && (s = rb->decode_ready(chunkset_id))) return s;
+    if (!c.decoded && (s = sh.decode_ready(rb->cs, chunkset_id))) return s;
     c.repaired = true;  // blob.rs:458-462 takes the decoder out before repairing
     if (c.dec_status != DECDS_OK) {
-        rb->drop_slot(c);
+        sh.drop_area(c);
+        sh.drop_slot(c);
         return decds_set_error(DECDS_ERR_CHUNKSET_REPAIRING_FAILED, "chunkset %zu repairing failed: RLNC Decoding error: %s",
                                chunkset_id, "invalid decoded data format");
     }
     HostUse uo(out, size);
     hipError_t e;
-    if ((e = copy_d2h(out, rb->slot_out(c.slot), size, uo.pinned(), rb->out_ring, rb->s)) ||
-        (e = rb->out_ring.flush()) || (e = hipStreamSynchronize(rb->s))) {
-        rb->out_ring.abandon();
+    if ((e = copy_d2h(out, sh.area_out(c.area), size, uo.pinned(), sh.out_ring, sh.s)) || (e = sh.out_ring.flush()) ||
+        (e = hipStreamSynchronize(sh.s))) {
+        sh.out_ring.abandon();
         return decds_hip_error(e, "D2H (repaired chunkset)");
     }
-    rb->drop_slot(c);
+    sh.drop_area(c);
+    sh.drop_slot(c);
     if (out_len) *out_len = size;  // blob.rs:464 truncate to the chunkset's real size
     return DECDS_OK;
 }

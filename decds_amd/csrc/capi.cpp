@@ -3,6 +3,8 @@
 // launchers. Every compute entry point runs the gfx950 kernels; there is no host fallback.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+
 #include <cstdlib>
 
 #include <cstdarg>
@@ -18,6 +20,7 @@
 using namespace decds;
 
 static thread_local std::string g_last_error;
+static std::atomic<int> g_live_ctx{0};  // contexts created and not yet destroyed
 
 int decds_set_error(int code, const char *fmt, ...) {
     char buf[512];
@@ -79,6 +82,7 @@ const char *decds_status_string(int s) {
         case DECDS_ERR_HIP: return "HIP runtime error";
         case DECDS_ERR_INVALID_ARGUMENT: return "invalid argument";
         case DECDS_ERR_NO_DEVICE: return "no gfx950 device";
+        case DECDS_ERR_OUT_OF_DEVICE_MEMORY: return "out of device memory";
         default: return "unknown status";
     }
 }
@@ -123,6 +127,7 @@ int decds_ctx_create(int device, decds_ctx **out) {
         delete c;
         return decds_hip_error(e, "hipMemset (tile counters)");
     }
+    g_live_ctx.fetch_add(1);
     *out = c;
     return DECDS_OK;
 }
@@ -132,6 +137,8 @@ int decds_ctx_destroy(decds_ctx *ctx) {
     (void)hipSetDevice(ctx->device);
     decds_lanes_destroy(ctx);
     if (ctx->host_scratch) (void)hipFree(ctx->host_scratch);
+    // the last context out returns the cached page-locked blocks (no idle pinned memory)
+    if (g_live_ctx.fetch_sub(1) == 1) (void)host_cache_trim();
     if (ctx->geom.counters) {
         (void)hipDeviceSynchronize();  // no launch may still count on them
         (void)hipFree(ctx->geom.counters);

@@ -11,7 +11,8 @@
 #include "rlnc_kernels.h"
 
 namespace decds {
-struct Lane;  // chunkset.cpp: the buffers and stream of one in-flight chunkset-mirror call
+struct Lane;       // chunkset.cpp: the buffers and stream of one in-flight chunkset-mirror call
+struct Coalescer;  // chunkset.cpp: concurrent ChunkSet::new calls gathered into shared launches
 }
 
 struct decds_ctx {
@@ -32,6 +33,7 @@ struct decds_ctx {
     std::mutex lane_mu;
     std::condition_variable lane_cv;
     std::vector<decds::Lane *> lanes_all, lanes_free;
+    decds::Coalescer *coalescer = nullptr;  // created by the first decds_chunkset_new (under lane_mu)
 };
 
 // at least `bytes` of the context's host-path scratch (caller holds ctx->host_mu)
@@ -41,6 +43,10 @@ void decds_lanes_destroy(decds_ctx *ctx);  // chunkset.cpp
 int decds_set_error(int code, const char *fmt, ...);
 int decds_hip_error(hipError_t e, const char *what);
 int decds_ctx_bind(const decds_ctx *ctx);  // hipSetDevice(ctx->device)
+// decds_encode_commit_batch with per-chunkset ids (commit.cpp)
+int encode_commit_ids(decds_ctx *ctx, const uint8_t *src, size_t n, const uint8_t *coeffs, uint8_t *dst, size_t pitch,
+                      uint64_t first_chunkset_id, const uint64_t *ids, uint8_t *digests, uint8_t *roots, uint8_t *proofs,
+                      void *workspace, void *stream);
 
 namespace decds {
 // host-side GF(2^8) helpers for the 10-byte coding vectors (control path, not the hot path)

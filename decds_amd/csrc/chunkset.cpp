@@ -15,10 +15,14 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
+#include <memory>
 #include <mutex>
 #include <random>
+#include <string>
 #include <vector>
 
 #include "../../include/decds_rlnc.h"
@@ -130,22 +134,232 @@ std::mt19937_64 &rng() {
 }
 
 }  // namespace
+
+// ---- coalesced ChunkSet::new ---------------------------------------------------------------------
+// The reference calls ChunkSet::new from rayon workers (blob.rs:256-264): one chunkset per call, many
+// calls at once. Each call copies its chunkset into a page-locked block of its own and queues a
+// request; whichever caller finds one of the context's two batch slots free takes every queued
+// request (up to CO_MAX) and runs them as ONE batch on that slot's stream — H2D of every chunkset,
+// one fused encode + chunk-hashing launch (rlnc_encode_hash_kernel, per-request chunkset ids) + fold
+// + Merkle, D2H of each request's rows and proofs into its own page-locked block — then wakes the
+// callers, who copy their rows out. Two slots: one batch's D2H overlaps the next batch's H2D.
+// A lone caller runs a batch of one. DECDS_CHUNKSET_COALESCE=0 keeps the per-call lane path.
+constexpr size_t CO_MAX = 16;
+constexpr size_t CO_P = DECDS_CODED_PITCH_ALIGNED;  // rows 16 bytes past a 128-byte boundary: the fused form
+
+struct PinnedPool {  // page-locked blocks of one size, kept for reuse
+    size_t bytes, keep;
+    std::mutex mu;
+    std::vector<uint8_t *> free;
+    hipError_t get(uint8_t **out) {
+        {
+            std::lock_guard<std::mutex> g(mu);
+            if (!free.empty()) {
+                *out = free.back();
+                free.pop_back();
+                return hipSuccess;
+            }
+        }
+        return host_pinned_alloc(bytes, reinterpret_cast<void **>(out));
+    }
+    void put(uint8_t *p) {
+        if (!p) return;
+        {
+            std::lock_guard<std::mutex> g(mu);
+            if (free.size() < keep) {
+                free.push_back(p);
+                return;
+            }
+        }
+        host_pinned_free(p, bytes);
+    }
+    void clear() {
+        std::lock_guard<std::mutex> g(mu);
+        for (uint8_t *p : free) host_pinned_free(p, bytes);
+        free.clear();
+    }
+};
+
+struct EncReq {
+    size_t id;
+    uint8_t cv[N * K];
+    uint8_t *in = nullptr;   // page-locked copy of the chunkset (CS)
+    uint8_t *out = nullptr;  // page-locked: 16 x F rows, then root (32) and proofs (16 x 4 x 32)
+    int status = DECDS_OK;
+    std::string err;
+    bool done = false;
+};
+constexpr size_t CO_OUT = N * F + 32 + N * PROOF_SIZE * 32;
+
+struct CoSlot {
+    hipStream_t s = nullptr;
+    uint8_t *d_src = nullptr, *d_rows = nullptr, *d_small = nullptr, *d_ws = nullptr, *h_small = nullptr;
+    uint8_t *rows = nullptr;  // message-aligned: row 0 16 bytes past a 128-byte boundary
+    bool busy = false;
+    // d_small / h_small: cv (CO_MAX x 160) | ids (CO_MAX x 8) | digests | roots | proofs
+    static constexpr size_t O_CV = 0, O_IDS = CO_MAX * N * K, O_DIG = O_IDS + CO_MAX * 8, O_ROOT = O_DIG + CO_MAX * N * 32,
+                            O_PRF = O_ROOT + CO_MAX * 32, BYTES = O_PRF + CO_MAX * N * PROOF_SIZE * 32;
+    hipError_t init() {
+        hipError_t e;
+        if ((e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking)) ||
+            (e = hipMalloc(reinterpret_cast<void **>(&d_src), CO_MAX * CS)) ||
+            (e = hipMalloc(reinterpret_cast<void **>(&d_rows), CO_MAX * N * CO_P + 256)) ||
+            (e = hipMalloc(reinterpret_cast<void **>(&d_small), BYTES)) ||
+            (e = hipMalloc(reinterpret_cast<void **>(&d_ws), decds_encode_commit_workspace_bytes(CO_MAX))) ||
+            (e = hipHostMalloc(reinterpret_cast<void **>(&h_small), BYTES, DECDS_HOST_MALLOC_FLAGS)))
+            return e;
+        rows = d_rows + (16 - reinterpret_cast<uintptr_t>(d_rows)) % 128;
+        return hipSuccess;
+    }
+    ~CoSlot() {
+        if (s) (void)hipStreamSynchronize(s);
+        for (uint8_t *p : {d_src, d_rows, d_small, d_ws})
+            if (p) (void)hipFree(p);
+        if (h_small) (void)hipHostFree(h_small);
+        if (s) (void)hipStreamDestroy(s);
+    }
+};
+
+struct Coalescer {
+    std::mutex mu;
+    std::condition_variable cv;
+    std::deque<EncReq *> pending;
+    CoSlot slot[2];
+    PinnedPool in_pool{CS, 2 * CO_MAX}, out_pool{CO_OUT, 2 * CO_MAX};
+    std::atomic<int> callers{0};
+    ~Coalescer() {
+        in_pool.clear();
+        out_pool.clear();
+    }
+};
+
+bool coalesce_enabled() {
+    static const bool on = [] {
+        const char *e = std::getenv("DECDS_CHUNKSET_COALESCE");
+        return !e || std::atoi(e) != 0;
+    }();
+    return on;
+}
+
+// one batch of m requests on slot sl (the caller holds sl.busy); returns the batch status
+int co_run(decds_ctx *ctx, CoSlot &sl, EncReq *const *req, size_t m) {
+    hipError_t e;
+    if (!sl.s && (e = sl.init())) return decds_hip_error(e, "coalesced ChunkSet::new slot setup");
+    for (size_t i = 0; i < m; i++) {
+        std::memcpy(sl.h_small + CoSlot::O_CV + i * N * K, req[i]->cv, N * K);
+        const uint64_t id = req[i]->id;
+        std::memcpy(sl.h_small + CoSlot::O_IDS + i * 8, &id, 8);
+        if ((e = hipMemcpyAsync(sl.d_src + i * CS, req[i]->in, CS, hipMemcpyHostToDevice, sl.s)))
+            return decds_hip_error(e, "H2D (chunkset)");
+    }
+    if ((e = hipMemcpyAsync(sl.d_small, sl.h_small, CoSlot::O_DIG, hipMemcpyHostToDevice, sl.s)))
+        return decds_hip_error(e, "H2D (coding vectors)");
+    int s = encode_commit_ids(ctx, sl.d_src, m, sl.d_small + CoSlot::O_CV, sl.rows, CO_P, 0,
+                              reinterpret_cast<const uint64_t *>(sl.d_small + CoSlot::O_IDS), sl.d_small + CoSlot::O_DIG,
+                              sl.d_small + CoSlot::O_ROOT, sl.d_small + CoSlot::O_PRF, sl.d_ws, sl.s);
+    if (s) return s;
+    for (size_t i = 0; i < m; i++) {
+        uint8_t *o = req[i]->out;
+        if ((e = hipMemcpy2DAsync(o, F, sl.rows + i * N * CO_P, CO_P, F, N, hipMemcpyDeviceToHost, sl.s)) ||
+            (e = hipMemcpyAsync(o + N * F, sl.d_small + CoSlot::O_ROOT + i * 32, 32, hipMemcpyDeviceToHost, sl.s)) ||
+            (e = hipMemcpyAsync(o + N * F + 32, sl.d_small + CoSlot::O_PRF + i * N * PROOF_SIZE * 32, N * PROOF_SIZE * 32,
+                                hipMemcpyDeviceToHost, sl.s)))
+            return decds_hip_error(e, "D2H (coded rows)");
+    }
+    if ((e = hipStreamSynchronize(sl.s))) return decds_hip_error(e, "hipStreamSynchronize");
+    return DECDS_OK;
+}
+
+// ChunkSet::new through the coalescer: data already checked (len == CS), cv drawn
+int co_chunkset_new(decds_ctx *ctx, size_t chunkset_id, const uint8_t *data, const uint8_t *cv, decds_chunkset **out);
+
 }  // namespace decds
 
 void decds_lanes_destroy(decds_ctx *ctx) {
-    std::lock_guard<std::mutex> g(ctx->lane_mu);
-    for (Lane *l : ctx->lanes_all) delete l;
-    ctx->lanes_all.clear();
-    ctx->lanes_free.clear();
+    {
+        std::lock_guard<std::mutex> g(ctx->lane_mu);
+        for (Lane *l : ctx->lanes_all) delete l;
+        ctx->lanes_all.clear();
+        ctx->lanes_free.clear();
+    }
+    delete ctx->coalescer;
+    ctx->coalescer = nullptr;
 }
 
 struct decds_chunkset {
     size_t id;
-    std::vector<uint8_t> coded;   // 16 x F, rlnc full coded pieces
+    std::unique_ptr<uint8_t[]> coded;  // 16 x F, rlnc full coded pieces (not zero-filled first)
     uint8_t root[32];             // MerkleTree root of the 16 chunk digests (chunkset.rs:57)
     uint8_t proofs[N][PROOF_SIZE][32];
     std::vector<uint8_t> blob_proof;  // appended to every chunk's proof (chunkset.rs:98-102)
 };
+
+int decds::co_chunkset_new(decds_ctx *ctx, size_t chunkset_id, const uint8_t *data, const uint8_t *cv,
+                           decds_chunkset **out) {
+    Coalescer *co;
+    {
+        std::lock_guard<std::mutex> g(ctx->lane_mu);
+        if (!ctx->coalescer) ctx->coalescer = new Coalescer;
+        co = ctx->coalescer;
+    }
+    EncReq r;
+    r.id = chunkset_id;
+    std::memcpy(r.cv, cv, N * K);
+    hipError_t e;
+    if ((e = co->in_pool.get(&r.in)) || (e = co->out_pool.get(&r.out))) {
+        co->in_pool.put(r.in);
+        return decds_hip_error(e, "page-locked staging");
+    }
+    // the copy into page-locked memory runs on the caller's own thread when other callers are copying
+    // too (they are the parallelism), else on the host pool
+    if (co->callers.fetch_add(1) > 0)
+        std::memcpy(r.in, data, CS);
+    else
+        par_memcpy(r.in, data, CS);
+    co->callers.fetch_sub(1);
+    {
+        std::unique_lock<std::mutex> g(co->mu);
+        co->pending.push_back(&r);
+        while (!r.done) {
+            int k = !co->slot[0].busy ? 0 : !co->slot[1].busy ? 1 : -1;
+            if (k < 0 || co->pending.empty()) {
+                co->cv.wait(g);
+                continue;
+            }
+            CoSlot &sl = co->slot[k];
+            sl.busy = true;
+            EncReq *batch[CO_MAX];
+            size_t m = 0;
+            while (m < CO_MAX && !co->pending.empty()) {
+                batch[m++] = co->pending.front();
+                co->pending.pop_front();
+            }
+            g.unlock();
+            int st = co_run(ctx, sl, batch, m);
+            const std::string msg = st ? decds_last_error() : std::string();
+            g.lock();
+            for (size_t i = 0; i < m; i++) {
+                batch[i]->status = st;
+                batch[i]->err = msg;
+                batch[i]->done = true;
+            }
+            sl.busy = false;
+            co->cv.notify_all();
+        }
+    }
+    co->in_pool.put(r.in);
+    if (r.status != DECDS_OK) {
+        co->out_pool.put(r.out);
+        return decds_set_error(r.status, "%s", r.err.c_str());
+    }
+    auto *c = new decds_chunkset{chunkset_id, std::unique_ptr<uint8_t[]>(new uint8_t[N * F]), {}, {}, {}};
+    std::memcpy(c->coded.get(), r.out, N * F);
+    std::memcpy(c->root, r.out + N * F, 32);
+    std::memcpy(c->proofs, r.out + N * F + 32, sizeof c->proofs);
+    co->out_pool.put(r.out);
+    *out = c;
+    return DECDS_OK;
+}
 
 struct decds_repairing_chunkset {
     decds_ctx *ctx;
@@ -170,6 +384,16 @@ int decds_chunkset_new(decds_ctx *ctx, size_t chunkset_id, const uint8_t *data, 
     if (!data) return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "null data");
     int s = decds_ctx_bind(ctx);
     if (s) return s;
+    if (coalesce_enabled()) {
+        uint8_t cvb[N * K];
+        if (coeffs) {
+            std::memcpy(cvb, coeffs, N * K);
+        } else {
+            std::lock_guard<std::mutex> g(g_rng_mu);
+            for (size_t i = 0; i < N * K; i++) cvb[i] = (uint8_t)rng()();
+        }
+        return co_chunkset_new(ctx, chunkset_id, data, cvb, out);
+    }
     LaneGuard lg{ctx};
     if ((s = lane_acquire(ctx, &lg.l))) return s;
     Lane &L = *lg.l;
@@ -194,8 +418,8 @@ int decds_chunkset_new(decds_ctx *ctx, size_t chunkset_id, const uint8_t *data, 
         (e = hipMemcpyAsync(L.h_small + SM_ROOT, L.d_small + SM_ROOT, SM_BYTES - SM_ROOT, hipMemcpyDeviceToHost, L.s)) ||
         (e = hipStreamSynchronize(L.s)))
         return decds_hip_error(e, "D2H");
-    auto *c = new decds_chunkset{chunkset_id, std::vector<uint8_t>(N * F), {}, {}, {}};
-    par_memcpy(c->coded.data(), L.h_big, N * F);
+    auto *c = new decds_chunkset{chunkset_id, std::unique_ptr<uint8_t[]>(new uint8_t[N * F]), {}, {}, {}};
+    par_memcpy(c->coded.get(), L.h_big, N * F);
     std::memcpy(c->root, L.h_small + SM_ROOT, 32);
     std::memcpy(c->proofs, L.h_small + SM_PRF, sizeof c->proofs);
     *out = c;
@@ -209,7 +433,7 @@ int decds_chunkset_get_chunk(const decds_chunkset *cs, size_t chunk_id, uint8_t 
                                               chunk_id, N);
     if (out) {
         if (out_len < F) return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "out buffer < %llu", (unsigned long long)F);
-        std::memcpy(out, cs->coded.data() + chunk_id * F, F);
+        std::memcpy(out, cs->coded.get() + chunk_id * F, F);
     }
     if (global_chunk_id) *global_chunk_id = cs->id * N + chunk_id;  // chunkset.rs:47
     return DECDS_OK;

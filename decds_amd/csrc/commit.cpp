@@ -324,7 +324,19 @@ size_t decds_encode_commit_workspace_bytes(size_t n) { return n * N * encode_com
 int decds_encode_commit_batch(decds_ctx *ctx, const uint8_t *src, size_t n, const uint8_t *coeffs, uint8_t *dst,
                               size_t pitch, uint64_t first_chunkset_id, uint8_t *digests, uint8_t *roots,
                               uint8_t *proofs, void *workspace, void *stream) {
+    return encode_commit_ids(ctx, src, n, coeffs, dst, pitch, first_chunkset_id, nullptr, digests, roots, proofs,
+                             workspace, stream);
+}
+
+}  // extern "C"
+
+// decds_encode_commit_batch with per-chunkset ids (device, n x u64; NULL: first_chunkset_id + c) on
+// message-aligned rows: the coalesced ChunkSet::new batches of callers' unrelated chunkset ids
+int encode_commit_ids(decds_ctx *ctx, const uint8_t *src, size_t n, const uint8_t *coeffs, uint8_t *dst, size_t pitch,
+                      uint64_t first_chunkset_id, const uint64_t *ids, uint8_t *digests, uint8_t *roots, uint8_t *proofs,
+                      void *workspace, void *stream) {
     if (!encode_commit_fusable(dst, pitch) || !n) {  // unaligned rows: encode, then the commitment kernels
+        if (ids) return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "per-chunkset ids need message-aligned rows");
         int s = decds_encode_batch(ctx, src, n, coeffs, dst, pitch, stream);
         return s ? s : decds_commit_batch(ctx, dst, pitch, n, first_chunkset_id, digests, roots, proofs, stream);
     }
@@ -337,12 +349,14 @@ int decds_encode_commit_batch(decds_ctx *ctx, const uint8_t *src, size_t n, cons
         return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "coded pitch %zu outside [%llu, 2 GiB / 16)", pitch,
                                (unsigned long long)F);
     auto *sub = static_cast<uint32_t *>(workspace);
-    hipError_t e = launch_encode_commit(src, n, coeffs, dst, pitch, ctx->poly, ctx->marker, first_chunkset_id, sub,
+    hipError_t e = launch_encode_commit(src, n, coeffs, dst, pitch, ctx->poly, ctx->marker, first_chunkset_id, ids, sub,
                                         (hipStream_t)stream);
     if (e) return decds_hip_error(e, "fused encode + chunk hashing launch");
     e = launch_commit_fold(dst, pitch, n, sub, encode_commit_subtrees(), digests, roots, proofs, (hipStream_t)stream);
     return e == hipSuccess ? DECDS_OK : decds_hip_error(e, "commit_fold_kernel launch");
 }
+
+extern "C" {
 
 int decds_validate_batch(decds_ctx *ctx, const uint8_t *coded, size_t pitch, size_t n_rows, const uint64_t *ids,
                          const uint8_t *proofs, size_t proof_len, const uint8_t *chunkset_roots,

@@ -28,7 +28,8 @@ hipError_t launch_encode(const LaunchGeom &g, const uint8_t *src, size_t n, cons
 bool encode_commit_fusable(const uint8_t *dst, size_t pitch);
 uint32_t encode_commit_subtrees();
 hipError_t launch_encode_commit(const uint8_t *src, size_t n, const uint8_t *coeffs, uint8_t *dst, size_t pitch,
-                                uint32_t poly, uint32_t marker, uint64_t first_id, uint32_t *sub, hipStream_t stream);
+                                uint32_t poly, uint32_t marker, uint64_t first_id, const uint64_t *ids, uint32_t *sub,
+                                hipStream_t stream);
 hipError_t launch_repair_plan(const uint8_t *coded, size_t pitch, size_t n, const uint8_t *cand,
                               uint8_t *plan, int8_t *verdicts, int32_t *status, uint32_t poly,
                               uint32_t gen, hipStream_t stream);

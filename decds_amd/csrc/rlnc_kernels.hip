@@ -40,6 +40,12 @@ constexpr uint32_t TABLE_BYTES = 16 * ROW_BYTES;              // 16 nibble rows 
 constexpr uint32_t LDS_BYTES = K * 2 * TABLE_BYTES;           // 5 KiB
 constexpr uint32_t SWEEP_LDS = 2 * LDS_BYTES + 16;             // two table buffers + the next-tile slot
 
+#ifndef DECDS_BUILD_XOR
+#define DECDS_BUILD_XOR 0  // table builds in a bank-conflict-free row order (build_tables)
+#endif
+#ifndef DECDS_ENC_DBUF
+#define DECDS_ENC_DBUF 0  // sweep encode: double-buffered tables, one barrier per tile
+#endif
 #ifndef DECDS_DEC_UNIT
 #define DECDS_DEC_UNIT 1  // decode tiles per workgroup (+3...+11 % against 8 once the tables stopped being replicated, r02e)
 #endif
@@ -132,8 +138,20 @@ __device__ __forceinline__ void build_tables(uint8_t *lds, uint32_t cw, uint32_t
 #pragma unroll
         for (int nib = 1; nib < 16; nib++) w[nib] = w[nib & (nib - 1)] ^ bw[__builtin_ctz(nib)];
         uint8_t *base = lds + (i * 2 + h) * TABLE_BYTES + 4 * q;
+#if DECDS_BUILD_XOR
+        // conflict-free order: table s = (2i + h) mod 16 writes row nib ^ s at step nib. The 8 tables of
+        // a ds_write_b32 lane group (32 lanes) then hit 8 distinct rows mod 8 = 32 distinct banks instead
+        // of one row's 4 banks (8-way). Rows are linear in the nibble: w[nib ^ s] = w[nib] ^ w[s].
+        const uint32_t s = (i * 2 + h) & 15u;
+        const uint32_t ws = ((s & 1u) ? bw[0] : 0u) ^ ((s & 2u) ? bw[1] : 0u) ^ ((s & 4u) ? bw[2] : 0u) ^
+                            ((s & 8u) ? bw[3] : 0u);
+#pragma unroll
+        for (uint32_t nib = 0; nib < 16; nib++)
+            *reinterpret_cast<uint32_t *>(base + ((nib ^ s) * ROW_BYTES)) = w[nib] ^ ws;
+#else
 #pragma unroll
         for (int nib = 0; nib < 16; nib++) *reinterpret_cast<uint32_t *>(base + nib * ROW_BYTES) = w[nib];
+#endif
     }
 }
 
@@ -437,7 +455,7 @@ template <int DW, int WAVES>
 __global__ __launch_bounds__(WG, WAVES) __attribute__((amdgpu_waves_per_eu(WAVES, WAVES)))
 void rlnc_encode_hash_kernel(const uint8_t *__restrict__ src, size_t n, const uint8_t *__restrict__ coeffs,
                              uint8_t *__restrict__ dst, size_t pitch, uint32_t poly, uint32_t marker,
-                             uint64_t first_id, uint32_t *__restrict__ sub) {
+                             uint64_t first_id, const uint64_t *__restrict__ ids, uint32_t *__restrict__ sub) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     constexpr uint32_t STEP = FH_STEP<DW>, STEPS = b3::CHUNK / STEP, BPS = STEP / b3::BLOCK;  // blocks per step
     const uint32_t cs = blockIdx.x / FH_WG_UNITS, gu = blockIdx.x % FH_WG_UNITS;
@@ -503,7 +521,8 @@ void rlnc_encode_hash_kernel(const uint8_t *__restrict__ src, size_t n, const ui
     uint32_t cv[8];
 #pragma unroll
     for (int i = 0; i < 8; i++) cv[i] = b3::K3.iv[i];
-    const uint64_t cs_id = first_id + cs, chunk_id = cs_id * N + j;  // chunkset.rs:47
+    // chunkset.rs:47; ids (coalesced ChunkSet::new callers): one chunkset id per batch entry
+    const uint64_t cs_id = ids ? uniform_u64(ids[cs]) : first_id + cs, chunk_id = cs_id * N + j;
     uint32_t st = 0;
 #pragma unroll 1
     do {
@@ -566,7 +585,6 @@ void rlnc_encode_sweep_kernel(const uint8_t *__restrict__ src, size_t n, const u
     // no static __shared__ here: the lookups' inline-asm ds_reads address the tables from LDS byte 0,
     // so everything lives in the dynamic allocation (2 table buffers, then the next-tile slot)
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    uint32_t &s_next = *reinterpret_cast<uint32_t *>(lds + 2 * LDS_BYTES);
     constexpr uint32_t T = TILES<DW>;
     uint32_t ioff[K], ooff[N];
 #pragma unroll
@@ -627,6 +645,44 @@ void rlnc_encode_sweep_kernel(const uint8_t *__restrict__ src, size_t n, const u
     // the next tile's coefficient bytes, then the lookups with the rolling prefetch of the next tile's
     // inputs and this tile's stores, and a barrier before the tables are rebuilt.
     lds_barrier();  // the edge pass's table readers are done
+#if DECDS_ENC_DBUF
+    // Double-buffered tables, one barrier per tile: tile t's lookups read buffer b while the same
+    // iteration builds the next tile's tables into buffer 1 - b (from coefficient bytes loaded at the
+    // top of the iteration); the barrier at the end both publishes the new tables and retires the old
+    // ones. The counter result travels through two alternating LDS slots (a slot is rewritten only
+    // after every wave has passed the barrier that follows its read).
+    uint32_t *slot = reinterpret_cast<uint32_t *>(lds + 2 * LDS_BYTES);
+    build_tables<K, N>(lds, cw, poly);
+    if constexpr (QUEUE) {
+        asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+        if (threadIdx.x == 0) slot[0] = G + grab;
+    }
+    lds_barrier();
+    auto step = [&](auto tbc) -> bool {
+        constexpr uint32_t B = decltype(tbc)::value;  // this tile's table buffer
+        const uint32_t tn = QUEUE ? slot[B] : t + G;
+        grab = grab_next();
+        const bool nx = tn < total;
+        const uint32_t csn = nx ? tn / T : cs;
+        const uint32_t cwn = table_coeffs_all<K, N>(coeffs + (size_t)csn * N * K, K);
+        combine_block<K, N, DW, B * LDS_BYTES>(x, dst + (size_t)cs * N * pitch, ooff, col_of(t),
+                                               src + (size_t)csn * CS, ioff, nx ? col_of(tn) : OOB_COL);
+        build_tables<K, N>(lds + (1 - B) * LDS_BYTES, cwn, poly);
+        if constexpr (QUEUE) {
+            asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+            if (threadIdx.x == 0) slot[1 - B] = G + grab;
+        }
+        lds_barrier();
+        t = tn;
+        cs = csn;
+        return nx;
+    };
+#pragma unroll 1
+    while (step(std::integral_constant<uint32_t, 0>{}) && step(std::integral_constant<uint32_t, 1>{})) {
+    }
+    (void)cw;
+#else
+    uint32_t &s_next = *reinterpret_cast<uint32_t *>(lds + 2 * LDS_BYTES);
     uint32_t more;
 #pragma unroll 1
     do {
@@ -647,6 +703,7 @@ void rlnc_encode_sweep_kernel(const uint8_t *__restrict__ src, size_t n, const u
         t = tn;
         cs = csn;
     } while (more);
+#endif
     // the last workgroup out resets the counter pair (tile counter, exit count) for the next launch
     // that takes this slot: no reset launch on the stream (a hipMemsetAsync was ~5 µs per encode)
     if (QUEUE && counter && threadIdx.x == 0) {
@@ -980,11 +1037,12 @@ static_assert(MSG_PHASE < COLS<2>, "16-byte-aligned rows have the message phase 
 uint32_t encode_commit_subtrees() { return FH_WAVE_UNITS; }
 
 hipError_t launch_encode_commit(const uint8_t *src, size_t n, const uint8_t *coeffs, uint8_t *dst, size_t pitch,
-                                uint32_t poly, uint32_t marker, uint64_t first_id, uint32_t *sub, hipStream_t stream) {
+                                uint32_t poly, uint32_t marker, uint64_t first_id, const uint64_t *ids, uint32_t *sub,
+                                hipStream_t stream) {
     if (n == 0) return hipSuccess;
     if (!encode_commit_fusable(dst, pitch)) return hipErrorInvalidValue;
     hipLaunchKernelGGL((ENC_HASH), dim3((uint32_t)(n * FH_WG_UNITS)), dim3(WG), FH_LDS<DECDS_FH_DW>, stream, src, n,
-                       coeffs, dst, pitch, poly, marker, first_id, sub);
+                       coeffs, dst, pitch, poly, marker, first_id, ids, sub);
     return hipGetLastError();
 }
 

@@ -68,6 +68,7 @@ extern "C" {
 #define DECDS_ERR_HIP (-1)                         /* HIP runtime failure (text: decds_last_error) */
 #define DECDS_ERR_INVALID_ARGUMENT (-2)
 #define DECDS_ERR_NO_DEVICE (-3)
+#define DECDS_ERR_OUT_OF_DEVICE_MEMORY (-4)        /* a device allocation the call cannot do without failed */
 
 typedef struct decds_ctx decds_ctx;
 
@@ -243,14 +244,32 @@ void decds_blob_free(decds_blob *blob);
 
 /* ---- RepairingBlob (blob.rs:321-473) ---------------------------------------------------------- */
 typedef struct decds_repairing_blob decds_repairing_blob;
-/* RepairingBlob::new(header) (blob.rs:341-353) from the BlobHeader fields it uses */
+/* RepairingBlob::new(header) (blob.rs:341-353) from the BlobHeader fields it uses, on one context */
 int decds_repairing_blob_new(decds_ctx *ctx, uint64_t byte_length, uint64_t num_chunksets, const uint8_t *root,
                              const uint8_t *chunkset_roots, decds_repairing_blob **out);
+/* the same over n_ctx contexts (devices): chunkset c belongs to context c / ceil(num_chunksets / n_ctx),
+ * the contiguous chunkset-index shards of decds_blob_new; every call below routes to the chunkset's
+ * context, and decds_repairing_blob_add_chunks validates each context's rows on its own device (one
+ * host thread per context). Statuses and repaired bytes are identical to the one-context object.
+ * Memory: accepted rows (10 x 1,048,587 B per chunkset, as the reference's decoder keeps them,
+ * chunkset.rs:129-135) stay on the device while the context is under its device budget and spill to
+ * page-locked host memory past it; a device allocation the call cannot do without fails with
+ * DECDS_ERR_OUT_OF_DEVICE_MEMORY instead of a HIP error. Default budget per context: env
+ * DECDS_RB_DEVICE_MB, else half the device's free memory at creation, split over the contexts that
+ * share the device. */
+int decds_repairing_blob_new_multi(decds_ctx *const *ctxs, size_t n_ctx, uint64_t byte_length, uint64_t num_chunksets,
+                                   const uint8_t *root, const uint8_t *chunkset_roots, decds_repairing_blob **out);
+/* device budget per context from now on (a quarter of it, at least one 20.5 MiB decode area, for
+ * decoding; the rest for row slots); memory already held is kept */
+int decds_repairing_blob_set_device_budget(decds_repairing_blob *rb, uint64_t bytes_per_context);
+/* stats[0..n_stats) of: device bytes held, chunksets with rows on the device, chunksets with rows
+ * spilled to host memory, host spill bytes held, decode areas, contexts */
+int decds_repairing_blob_memory(const decds_repairing_blob *rb, uint64_t *stats, size_t n_stats);
 /* RepairingBlob::add_chunk (blob.rs:373-394), in the reference's order: chunkset id out of range ->
  * DECDS_ERR_INVALID_CHUNKSET_ID; chunkset already repaired -> DECDS_ERR_CHUNKSET_ALREADY_REPAIRED;
  * BlobHeader::validate_chunk fails -> DECDS_ERR_INVALID_PROOF_IN_CHUNK; chunkset ready ->
  * DECDS_ERR_CHUNKSET_READY_TO_REPAIR; then add_chunk_unvalidated (a piece that does not raise the
- * rank -> DECDS_ERR_CHUNK_DECODING_FAILED). Accepted rows are kept on the device. */
+ * rank -> DECDS_ERR_CHUNK_DECODING_FAILED). Accepted rows are kept on the device (or spilled, above). */
 int decds_repairing_blob_add_chunk(decds_repairing_blob *rb, uint64_t chunkset_id, uint64_t chunk_id,
                                    const uint8_t *data, size_t len, const uint8_t *proof, size_t proof_len);
 /* add_chunk for n_rows chunks in arrival order, validated as one device batch: ids n x (chunkset_id,
@@ -355,7 +374,7 @@ int decds_host_register(const void *ptr, size_t len);
 int decds_host_unregister(const void *ptr);
 /* page-locked host memory the host paths DMA directly (hipHostMalloc + the same registry). Blocks
  * of 64 MiB and more (the library's own, e.g. a Blob's coded store, and these) go to a cache when
- * freed — up to DECDS_PINNED_CACHE_MB (default 16384) — and serve later requests of 80-100 % of
+ * freed — up to DECDS_PINNED_CACHE_MB (default 4096; all of them freed when the last context is destroyed) — and serve later requests of 80-100 % of
  * their size without page-locking again (~0.25 s per GiB); decds_host_cache_trim releases them and
  * returns the bytes released. Memory from the cache is not zeroed. */
 int decds_host_alloc(size_t len, void **out);

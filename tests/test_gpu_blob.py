@@ -223,3 +223,91 @@ def test_repairing_blob_cfg2_slots_span_4gib_windows(ctx):
             continue
         got = rep.get_repaired_chunkset(c, out=out.array)
         assert np.array_equal(got, data[c * CS:min(blob_len, (c + 1) * CS)]), c
+
+
+# the decode-area + one-slab budget of decds_repairing_blob_set_device_budget (blob.cpp RbShard)
+_ROWS = -(-K * F // 256) * 256
+_AREA = _ROWS + CS
+_SLAB = 8 * _ROWS
+
+
+def _arrivals(blob, seed, tamper_every=13):
+    chunks = _all_chunks(blob)
+    out = []
+    for i, k in enumerate(np.random.default_rng(seed).permutation(len(chunks))):
+        c = chunks[int(k)]
+        if i % tamper_every == 4:
+            t = bytearray(c.erasure_coded_data)
+            t[i * 131 % F] ^= 0x40
+            c = decds_amd.Chunk(c.chunkset_id, c.chunk_id, bytes(t), c.proof)
+        out.append(c)
+    return out
+
+
+def _sequential(rep, arrivals):
+    st = []
+    for c in arrivals:
+        try:
+            rep.add_chunk(c)
+            st.append(0)
+        except DecdsError as e:
+            st.append(e.status)
+    return st
+
+
+def test_repairing_blob_sharded_and_spilled_match_one_context(ctx):
+    # blob.rs:321-473 over two contexts (chunksets [0, 5) and [5, 9) of the one device stand in for
+    # two GPUs) and under device budgets that spill accepted rows to page-locked host memory: statuses
+    # of every shuffled arrival (tampered ones included) and every repaired chunkset are identical to
+    # the one-context object with everything resident
+    blob_len = 8 * CS + 54321
+    data, _, blob = _blob(ctx, blob_len, 0x7B70)
+    header = blob.get_blob_header()
+    n = header.get_num_chunksets()
+    assert n == 9
+    arrivals = _arrivals(blob, 0x7B71)
+    ref = decds_amd.RepairingBlob(ctx, header)
+    want = _sequential(ref, arrivals)
+    assert 11 in want and 3 in want
+    ctx2 = decds_amd.Context(0)
+    cases = {
+        "2 contexts, batch": (decds_amd.RepairingBlob([ctx, ctx2], header), True),
+        "2 contexts, all spilled": (decds_amd.RepairingBlob([ctx, ctx2], header, device_budget=0), False),
+        "1 context, 1 slab + 1 area": (decds_amd.RepairingBlob(ctx, header, device_budget=_AREA + _SLAB), True),
+        "2 contexts, 1 slab + 1 area, sequential": (decds_amd.RepairingBlob([ctx, ctx2], header,
+                                                                            device_budget=_AREA + _SLAB), False),
+    }
+    fetch = [4, 8, 0, 5, 2, 7, 1, 3, 6]
+    for name, (rep, batched) in cases.items():
+        got = rep.add_chunks(arrivals).tolist() if batched else _sequential(rep, arrivals)
+        assert got == want, name
+        mem = rep.memory()
+        assert mem["contexts"] == (2 if name.startswith("2") else 1), name
+        # rows on the device / spilled: one slab holds 8 chunksets' rows per context
+        expect = {"2 contexts, batch": (n, 0), "2 contexts, all spilled": (0, n), "1 context, 1 slab + 1 area": (8, 1),
+                  "2 contexts, 1 slab + 1 area, sequential": (n, 0)}[name]
+        assert (mem["device_chunksets"], mem["spilled_chunksets"]) == expect, (name, mem)
+        if "slab" in name or "spilled" in name:
+            batch_area = 256 * (F + 16 + 32 * blob.proof_len() + 32) if batched else 0
+            assert mem["device_bytes"] <= mem["contexts"] * (_AREA + _SLAB + batch_area + (1 << 20)), (name, mem)
+        for c in fetch:
+            assert rep.get_repaired_chunkset(c) == data[c * CS:min(blob_len, (c + 1) * CS)].tobytes(), (name, c)
+        assert rep.memory()["device_chunksets"] == 0 and rep.memory()["spilled_chunksets"] == 0
+        _raises("ChunksetAlreadyRepaired", rep.add_chunk, arrivals[0])
+    del cases, ref
+    ctx2.close()
+
+
+def test_host_buffer_views_keep_the_block_alive(ctx):
+    # a view of HostBuffer.array must not outlive the page-locked block it points into
+    hb = decds_amd.HostBuffer(3 << 20)
+    view = hb.array[1000:2000]
+    view[:] = 7
+    assert hb.free() is False                   # a view is alive: refused
+    del hb
+    assert int(view.sum()) == 7 * 1000          # still readable: the view holds the block
+    other = decds_amd.HostBuffer(3 << 20)
+    other.array[:] = 1
+    assert int(view.sum()) == 7 * 1000          # and no later allocation aliases it
+    assert other.free() is True
+    del view

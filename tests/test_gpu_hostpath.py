@@ -107,7 +107,7 @@ def test_host_registry_rules(ctx):
     hb = decds_amd.HostBuffer(5000)
     assert L.decds_host_is_registered(hb.array.ctypes.data, 5000) == 1
     assert L.decds_host_unregister(hb.array.ctypes.data) == -2    # allocations are freed, not unregistered
-    hb.free()
+    assert hb.free() is True
     # a registered caller buffer used by a host path, unregistered in between calls
     blob = o.fill_random(0xC0C0, CS + 5)
     coeffs = o.fill_random(0xC1C1, 2 * N * K)
@@ -190,6 +190,47 @@ def test_pinned_block_cache_reuse_and_trim(ctx):
             hb.array[:] = fill
         coded = codec.blob_encode_host(ctx, blob, coeffs, batch=2, out=hb.array.reshape(n * N, F))
         assert np.array_equal(coded, want)
-        hb.free()
+        del coded                       # the returned view would keep the block (HostBuffer.free refuses)
+        assert hb.free() is True
     assert ptrs[0] == ptrs[1]
     L.decds_host_cache_trim()
+
+
+def test_chunkset_new_16_concurrent_callers_coalesced(ctx):
+    # ChunkSet::new from 16 threads at once (Blob::new's rayon loop, blob.rs:256-264): the calls are
+    # gathered into shared fused encode + hashing launches with per-request chunkset ids, so unrelated
+    # ids in one batch must each get their own digests (chunk.rs:40-46, id = chunkset_id*16+j), root
+    # and proofs; every chunkset bit-exact against the oracle, several rounds so batches mix callers
+    T, rounds = 16, 3
+    ids = [7 + 1000 * t for t in range(T)]
+    errors, results = [], {}
+
+    def worker(t):
+        try:
+            for rd in range(rounds):
+                data = o.fill_random(0xE000 + 97 * t + rd, CS)
+                coeffs = o.fill_random(0xE100 + 97 * t + rd, N * K)
+                results[(t, rd)] = decds_amd.ChunkSet(ctx, ids[t] + rd, data.tobytes(), coeffs.tobytes())
+        except Exception as e:
+            errors.append(e)
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(T)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not errors, errors
+    for t in range(T):
+        for rd in range(rounds):
+            cid = ids[t] + rd
+            data = o.fill_random(0xE000 + 97 * t + rd, CS)
+            ref = o.chunkset_encode(data, o.fill_random(0xE100 + 97 * t + rd, N * K), nthreads=8)
+            cs = results[(t, rd)]
+            chunks = [cs.get_chunk(j) for j in range(N)]
+            assert all(c.erasure_coded_data == ref[j].tobytes() for j, c in enumerate(chunks)), (t, rd)
+            assert all(c.chunk_id == cid * N + j for j, c in enumerate(chunks))
+            if (t + rd) % 5 == 0:  # commitment spot checks: root and every proof against the oracle
+                leaves = [o.chunk_digest(cid, cid * N + j, ref[j]) for j in range(N)]
+                root, proofs = o.merkle(leaves)
+                assert cs.get_root_commitment() == root, (t, rd)
+                assert [c.proof for c in chunks] == proofs, (t, rd)

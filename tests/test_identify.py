@@ -38,3 +38,37 @@ def test_identify_from_share_file(poly, marker, tmp_path):
     assert (cs_id, chunk_id) == (3, 53) and np.array_equal(parsed, coded)
     hits, m = idf.identify(parsed, data)
     assert hits == [poly] and m == marker
+
+
+def _coded_under(data, cv, poly, marker, prefix, placement):
+    """a full coded piece built under a layout hypothesis (numpy restatement via the oracle's tables)"""
+    t = o.mul_table(poly)
+    padded = np.zeros(10 * o.L, np.uint8)
+    padded[:o.CS] = data
+    if placement == "marker-then-zeros":
+        padded[o.CS] = marker
+    elif placement == "zeros-then-marker":
+        padded[-1] = marker
+    y = np.zeros(o.L, np.uint8)
+    for i in range(10):
+        y ^= t[cv[i], padded[i * o.L:(i + 1) * o.L]]
+    return np.concatenate([cv, y] if prefix == "cv||payload" else [y, cv])
+
+
+@pytest.mark.parametrize("prefix", idf.PREFIXES)
+@pytest.mark.parametrize("placement", idf.MARKERS)
+def test_identify_layout_names_the_hypothesis(prefix, placement):
+    poly, marker = (0x11D, 0x81) if prefix == "cv||payload" else (0x12B, 0x5A)
+    data = o.fill_random(len(prefix) * 31 + len(placement), o.CS)
+    cv = o.fill_random(7 + len(placement), 10)
+    cv[9] |= 1
+    coded = _coded_under(data, cv, poly, marker, prefix, placement)
+    fits = idf.identify_layout(coded, data)
+    want = {"prefix": prefix, "marker_placement": placement, "polynomial": poly,
+            "marker": None if placement == "no-marker" else marker}
+    assert fits == [want]
+
+
+def test_identify_layout_reports_nothing_for_unrelated_bytes():
+    data = o.fill_random(5, o.CS)
+    assert idf.identify_layout(o.fill_random(6, o.F), data) == []

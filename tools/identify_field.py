@@ -9,6 +9,11 @@ y[col] = sum_i c_i * piece_i[col]. Columns below 1,048,567 involve data bytes on
 identify the polynomial among the 30 irreducible degree-8 candidates; column 1,048,567 of piece 9
 holds the marker m, which y then determines as m = (y - sum_{i<9} c_i*piece_i) / c_9.
 
+Layout hypotheses (identify_layout): the coding vector before or after the payload, and the marker
+right after the data (then zeros), at the very end of the padding, or absent; each fit is reported
+with its polynomial and marker, so an unexpected layout is named instead of reported as "no
+polynomial".
+
 usage: python tools/identify_field.py SHARE_FILE CHUNKSET_DATA_FILE
        (CHUNKSET_DATA_FILE = the 10 MiB chunkset, e.g. decds-bin's chunkset.N.data, zero-padded)
 """
@@ -55,13 +60,18 @@ def parse_share(buf):
     return cs_id, chunk_id, np.frombuffer(buf[p:p + n], np.uint8)
 
 
-def identify(coded, chunkset, probe_cols=64):
-    """returns (polys consistent with the data columns, marker or None)"""
+# layout hypotheses the re-pin tries: where the 10-byte coding vector sits in the full
+# coded piece, and where Encoder::new puts the boundary marker in the padded pieces
+PREFIXES = ("cv||payload", "payload||cv")
+MARKERS = ("marker-then-zeros", "zeros-then-marker", "no-marker")
+
+
+def split_piece(coded, prefix):
     coded = np.asarray(coded, np.uint8)
-    cv, y = coded[:K], coded[K:]
-    data = np.asarray(chunkset, np.uint8)
-    rng = np.random.default_rng(0)
-    cols = rng.choice(L - 10, size=min(probe_cols, L - 10), replace=False)
+    return (coded[:K], coded[K:]) if prefix == "cv||payload" else (coded[-K:], coded[:-K])
+
+
+def _polys_for(cv, y, data, cols):
     pieces = np.stack([data[i * L + cols] if i < 9 else data[np.minimum(9 * L + cols, CS - 1)] for i in range(K)])
     hits = []
     for p in irreducible_polys():
@@ -71,15 +81,64 @@ def identify(coded, chunkset, probe_cols=64):
             acc ^= t[cv[i], pieces[i]]
         if np.array_equal(acc, y[cols]):
             hits.append(p)
+    return hits
+
+
+def _marker_for(cv, y, data, poly, placement):
+    """the marker value under `placement`, or None if the tail columns contradict it. Piece 9 holds
+    data bytes up to column CS - 9L, then the padding; the other pieces are data only."""
+    t = gf_mul_table(poly)
+    first = CS - 9 * L                             # piece 9's first padding column
+    mcol = {"marker-then-zeros": first, "zeros-then-marker": L - 1, "no-marker": None}[placement]
+    inv = next(b for b in range(1, 256) if t[cv[9], b] == 1) if cv[9] else None
     marker = None
-    if len(hits) == 1 and cv[9]:
-        t = gf_mul_table(hits[0])
-        col = CS - 9 * L                           # marker column of piece 9
+    for col in range(first, L):
         rest = 0
         for i in range(9):
             rest ^= int(t[cv[i], data[i * L + col]])
-        inv = next(b for b in range(1, 256) if t[cv[9], b] == 1)
-        marker = int(t[inv, int(y[col]) ^ rest])
+        got = int(y[col]) ^ rest                   # = cv[9] * piece9[col]
+        if col == mcol:
+            if inv is None:
+                return None
+            marker = int(t[inv, got])
+            if marker == 0:
+                return None                        # a zero "marker" is the no-marker layout
+        elif got != 0:
+            return None
+    return marker if mcol is not None else "none"
+
+
+def identify_layout(coded, chunkset, probe_cols=64):
+    """every (prefix, marker placement) hypothesis the chunk is consistent with:
+    [{"prefix", "marker_placement", "polynomials", "marker"}]; empty = no known layout fits"""
+    data = np.asarray(chunkset, np.uint8)
+    rng = np.random.default_rng(0)
+    cols = rng.choice(L - 10, size=min(probe_cols, L - 10), replace=False)
+    out = []
+    for prefix in PREFIXES:
+        cv, y = split_piece(coded, prefix)
+        hits = _polys_for(cv, y, data, cols)
+        for placement in MARKERS:
+            for p in hits:
+                m = _marker_for(cv, y, data, p, placement)
+                if m is not None:
+                    out.append({"prefix": prefix, "marker_placement": placement, "polynomial": p,
+                                "marker": None if m == "none" else m})
+    return out
+
+
+def identify(coded, chunkset, probe_cols=64):
+    """the recalled layout only (cv || payload, marker then zeros): (polys consistent with the data
+    columns, marker or None)"""
+    cv, y = split_piece(coded, "cv||payload")
+    data = np.asarray(chunkset, np.uint8)
+    rng = np.random.default_rng(0)
+    cols = rng.choice(L - 10, size=min(probe_cols, L - 10), replace=False)
+    hits = _polys_for(cv, y, data, cols)
+    marker = None
+    if len(hits) == 1:
+        m = _marker_for(cv, y, data, hits[0], "marker-then-zeros")
+        marker = m if isinstance(m, int) else None
     return hits, marker
 
 
@@ -90,9 +149,13 @@ def main():
     data = np.fromfile(data_file, np.uint8)
     if data.size < CS:
         data = np.concatenate([data, np.zeros(CS - data.size, np.uint8)])
-    hits, marker = identify(coded, data[:CS])
-    print(json.dumps({"chunkset_id": cs_id, "chunk_id": chunk_id, "polynomials": [hex(p) for p in hits],
-                      "marker": None if marker is None else hex(marker)}))
+    fits = identify_layout(coded, data[:CS])
+    print(json.dumps({"chunkset_id": cs_id, "chunk_id": chunk_id,
+                      "layouts": [dict(f, polynomial=hex(f["polynomial"]),
+                                       marker=None if f["marker"] is None else hex(f["marker"])) for f in fits],
+                      "verdict": ("no known layout fits: not an rlnc-0.4.0-style piece of this chunkset under any "
+                                  "hypothesis tried (%s x %s)" % (PREFIXES, MARKERS)) if not fits else
+                                 ("pinned" if len(fits) == 1 else "ambiguous")}))
 
 
 if __name__ == "__main__":
