@@ -5,6 +5,7 @@
 #include <stdint.h>
 
 namespace decds {
+hipError_t configure_commit_kernels();  // resolve the commitment kernels eagerly (configure_kernels)
 hipError_t launch_commit(const uint8_t *coded, size_t pitch, size_t n, uint64_t first_chunkset_id, uint8_t *digests,
                          uint8_t *roots, uint8_t *proofs, hipStream_t stream);
 // digests of rows encoded by launch_encode_commit (sub: its subtree values), then the Merkle trees

@@ -26,6 +26,7 @@
 #include <utility>
 
 #include "blake3_impl.h"
+#include "commit_kernels.h"
 #include "rlnc_kernels.h"
 #include "rlnc_layout.h"
 
@@ -41,10 +42,7 @@ constexpr uint32_t LDS_BYTES = K * 2 * TABLE_BYTES;           // 5 KiB
 constexpr uint32_t SWEEP_LDS = 2 * LDS_BYTES + 16;             // two table buffers + the next-tile slot
 
 #ifndef DECDS_BUILD_XOR
-#define DECDS_BUILD_XOR 0  // table builds in a bank-conflict-free row order (build_tables)
-#endif
-#ifndef DECDS_ENC_DBUF
-#define DECDS_ENC_DBUF 0  // sweep encode: double-buffered tables, one barrier per tile
+#define DECDS_BUILD_XOR 1  // table builds in a bank-conflict-free row order (build_tables)
 #endif
 #ifndef DECDS_DEC_UNIT
 #define DECDS_DEC_UNIT 1  // decode tiles per workgroup (+3...+11 % against 8 once the tables stopped being replicated, r02e)
@@ -112,8 +110,11 @@ __device__ __forceinline__ uint32_t table_coeffs_all(const uint8_t *M, uint32_t 
 // Multiplication by a constant is linear over GF(2), so row (i, h, nib) = XOR of the products of
 // C[.][i] with the set bits of nib << 4h: thread (i, h, output quad q) forms the 4 basis words
 // { C[4q+jj][i] * x^(4h+k) : jj < 4 } (xtime chains) and the 16 rows' dwords q by one XOR each
-// (nib & (nib-1) is nib minus its lowest bit). The 16 ds_write_b32 per thread are 8-way conflicted
-// (same row of 8 tables per instruction): ~0.1 µs per build, not worth a staggered order.
+// (nib & (nib-1) is nib minus its lowest bit). The 16 ds_write_b32 per thread go out in a staggered
+// row order (DECDS_BUILD_XOR) so that no two tables of a lane group write the same banks (the plain
+// order was 8-way conflicted: 5 % of the encode's LDS cycles, r05a PMC). In-process A/B (r05b):
+// ±0.3 % — the build is not what bounds the encode; neither is the second barrier per tile (double-
+// buffered tables with one barrier per tile measured the same and were removed).
 template <int NIN, int NOUT>
 __device__ __forceinline__ void build_tables(uint8_t *lds, uint32_t cw, uint32_t poly) {
     const uint32_t p = threadIdx.x;
@@ -645,43 +646,6 @@ void rlnc_encode_sweep_kernel(const uint8_t *__restrict__ src, size_t n, const u
     // the next tile's coefficient bytes, then the lookups with the rolling prefetch of the next tile's
     // inputs and this tile's stores, and a barrier before the tables are rebuilt.
     lds_barrier();  // the edge pass's table readers are done
-#if DECDS_ENC_DBUF
-    // Double-buffered tables, one barrier per tile: tile t's lookups read buffer b while the same
-    // iteration builds the next tile's tables into buffer 1 - b (from coefficient bytes loaded at the
-    // top of the iteration); the barrier at the end both publishes the new tables and retires the old
-    // ones. The counter result travels through two alternating LDS slots (a slot is rewritten only
-    // after every wave has passed the barrier that follows its read).
-    uint32_t *slot = reinterpret_cast<uint32_t *>(lds + 2 * LDS_BYTES);
-    build_tables<K, N>(lds, cw, poly);
-    if constexpr (QUEUE) {
-        asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-        if (threadIdx.x == 0) slot[0] = G + grab;
-    }
-    lds_barrier();
-    auto step = [&](auto tbc) -> bool {
-        constexpr uint32_t B = decltype(tbc)::value;  // this tile's table buffer
-        const uint32_t tn = QUEUE ? slot[B] : t + G;
-        grab = grab_next();
-        const bool nx = tn < total;
-        const uint32_t csn = nx ? tn / T : cs;
-        const uint32_t cwn = table_coeffs_all<K, N>(coeffs + (size_t)csn * N * K, K);
-        combine_block<K, N, DW, B * LDS_BYTES>(x, dst + (size_t)cs * N * pitch, ooff, col_of(t),
-                                               src + (size_t)csn * CS, ioff, nx ? col_of(tn) : OOB_COL);
-        build_tables<K, N>(lds + (1 - B) * LDS_BYTES, cwn, poly);
-        if constexpr (QUEUE) {
-            asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-            if (threadIdx.x == 0) slot[1 - B] = G + grab;
-        }
-        lds_barrier();
-        t = tn;
-        cs = csn;
-        return nx;
-    };
-#pragma unroll 1
-    while (step(std::integral_constant<uint32_t, 0>{}) && step(std::integral_constant<uint32_t, 1>{})) {
-    }
-    (void)cw;
-#else
     uint32_t &s_next = *reinterpret_cast<uint32_t *>(lds + 2 * LDS_BYTES);
     uint32_t more;
 #pragma unroll 1
@@ -703,7 +667,6 @@ void rlnc_encode_sweep_kernel(const uint8_t *__restrict__ src, size_t n, const u
         t = tn;
         cs = csn;
     } while (more);
-#endif
     // the last workgroup out resets the counter pair (tile counter, exit count) for the next launch
     // that takes this slot: no reset launch on the stream (a hipMemsetAsync was ~5 µs per encode)
     if (QUEUE && counter && threadIdx.x == 0) {
@@ -993,7 +956,16 @@ hipError_t configure_kernels() {
         hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, std::max(SWEEP_LDS, FH_LDS<DECDS_FH_DW>));
         if (e != hipSuccess) return e;
     }
-    return hipSuccess;
+    // every other kernel's code object resolved now, on the creating thread, not lazily by the first
+    // launch — which may come from several caller threads at once (the coalesced ChunkSet::new)
+    const void *rest[] = {reinterpret_cast<const void *>(rlnc_plan_kernel), reinterpret_cast<const void *>(fill_random_words_kernel),
+                          reinterpret_cast<const void *>(fill_random_bytes_kernel)};
+    for (const void *f : rest) {
+        hipFuncAttributes a;
+        hipError_t e = hipFuncGetAttributes(&a, f);
+        if (e != hipSuccess) return e;
+    }
+    return configure_commit_kernels();
 }
 
 // resident workgroups of the sweep kernel on this device (occupancy x CUs), once per process
@@ -1041,6 +1013,7 @@ hipError_t launch_encode_commit(const uint8_t *src, size_t n, const uint8_t *coe
                                 hipStream_t stream) {
     if (n == 0) return hipSuccess;
     if (!encode_commit_fusable(dst, pitch)) return hipErrorInvalidValue;
+    (void)hipGetLastError();  // only this launch's status below
     hipLaunchKernelGGL((ENC_HASH), dim3((uint32_t)(n * FH_WG_UNITS)), dim3(WG), FH_LDS<DECDS_FH_DW>, stream, src, n,
                        coeffs, dst, pitch, poly, marker, first_id, ids, sub);
     return hipGetLastError();
@@ -1067,6 +1040,7 @@ hipError_t launch_repair_plan(const uint8_t *coded, size_t pitch, size_t n, cons
         last_poly = poly;
         last_gen = gen;
     }
+    (void)hipGetLastError();  // only this launch's status below
     hipLaunchKernelGGL(rlnc_plan_kernel, dim3((uint32_t)n), dim3(64), 0, stream, coded, pitch, n, cand,
                        reinterpret_cast<RepairPlan *>(plan), verdicts, status, tab);
     return hipGetLastError();
@@ -1078,6 +1052,7 @@ hipError_t launch_decode(const LaunchGeom &, const uint8_t *coded, size_t pitch,
     if (n == 0) return hipSuccess;
     const RepairPlan *pl = reinterpret_cast<const RepairPlan *>(plan);
     constexpr uint32_t U = DEC_UNIT;
+    (void)hipGetLastError();  // only this launch's status below
     hipLaunchKernelGGL(rlnc_decode_kernel<U>, dim3((uint32_t)(n * (TILES<4> / U))), dim3(WG), LDS_BYTES, stream, coded,
                        pitch, n, pl, dst, status, in_bases, out_bases, poly, marker);
     return hipGetLastError();
@@ -1089,10 +1064,12 @@ hipError_t launch_fill_random(uint64_t seed, uint64_t byte_offset, uint8_t *dst,
     if ((byte_offset & 7u) == 0 && (reinterpret_cast<uintptr_t>(dst) & 7u) == 0 && (nbytes & 7u) == 0) {
         const size_t nw = nbytes / 8;
         const uint32_t grid = (uint32_t)((nw + 255) / 256 < 8192 ? (nw + 255) / 256 : 8192);
+        (void)hipGetLastError();  // only this launch's status below
         hipLaunchKernelGGL(fill_random_words_kernel, dim3(grid), dim3(256), 0, stream, seed, byte_offset / 8,
                            reinterpret_cast<uint64_t *>(dst), nw);
     } else {
         const uint32_t grid = (uint32_t)((nbytes + 255) / 256 < 8192 ? (nbytes + 255) / 256 : 8192);
+        (void)hipGetLastError();  // only this launch's status below
         hipLaunchKernelGGL(fill_random_bytes_kernel, dim3(grid), dim3(256), 0, stream, seed, byte_offset, dst,
                            nbytes);
     }

@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--reps", type=int, default=5, help="timed blob-path repetitions per mode (median)")
     ap.add_argument("--modes", default="pageable,host_alloc,host_register")
     ap.add_argument("--blob-only", action="store_true")
+    ap.add_argument("--no-blob", action="store_true", help="only the per-chunkset mirror rows")
     a = ap.parse_args()
     import numpy as np
     import decds_amd
@@ -54,6 +55,7 @@ def main():
             x.join()
         dt = time.perf_counter() - t0
         print(json.dumps({"path": "decds_chunkset_new (ChunkSet::new + commitment)", "threads": T,
+                          "coalesced": os.environ.get("DECDS_CHUNKSET_COALESCE", "1") != "0",
                           "chunksets": sum(counts), "GiBps": round(sum(counts) * CS / GIB / dt, 2)}), flush=True)
         # repair: RepairingChunkSet with 10 chunks already added, repair() timed
         cs = [decds_amd.ChunkSet(ctx, t, datas[t], coeffs[t]) for t in range(T)]
@@ -79,6 +81,8 @@ def main():
         print(json.dumps({"path": "decds_repairing_chunkset_repair (add 10 chunks + repair)", "threads": T,
                           "chunksets": sum(counts), "GiBps": round(sum(counts) * CS / GIB / dt, 2)}), flush=True)
 
+    if a.no_blob:
+        return
     # blob-level host paths over the same kind of data: pageable (staged through the library's rings),
     # library page-locked memory (decds_host_alloc) and registered caller memory (decds_host_register)
     n = max(1, int(a.blob_gib * GIB) // CS)
