@@ -17,6 +17,12 @@ def _ctx_array(ctxs):
     return arr, len(ctxs)
 
 
+def _adopt_by(ctxs, obj):
+    for c in (ctxs if isinstance(ctxs, (list, tuple)) else [ctxs]):
+        if hasattr(c, "_adopt"):
+            c._adopt(obj)
+
+
 class _PinnedBlock:
     """owns one decds_host_alloc block; frees it when the last reference (a HostBuffer or any numpy
     view of its array) is gone, or on release()"""
@@ -84,6 +90,7 @@ class Blob:
         check(lib().decds_blob_new(arr, n_ctx, ctypes.c_void_p(buf.ctypes.data if buf.size else 0), buf.size,
                                    None if cv is None else ctypes.c_void_p(cv.ctypes.data), ctypes.byref(h)))
         self._h = h
+        _adopt_by(ctxs, self)
 
     def get_blob_header(self):
         """Blob::get_blob_header (blob.rs:288-290)"""
@@ -144,6 +151,7 @@ class RepairingBlob:
                                                    header.get_root_commitment(), roots, ctypes.byref(h)))
         self._h = h
         self.header = header
+        _adopt_by(ctxs, self)
         if device_budget is not None:
             check(lib().decds_repairing_blob_set_device_budget(h, int(device_budget)))
 
@@ -217,11 +225,15 @@ class RepairingBlob:
                                                                buf.nbytes, ctypes.byref(got)))
         return buf[:got.value].tobytes() if out is None else buf[:got.value]
 
+    def free(self):
+        """releases the RepairingBlob (device slots, spill memory, streams)"""
+        if self._h:
+            lib().decds_repairing_blob_free(self._h)
+            self._h = None
+
     def __del__(self):
         try:
-            if self._h:
-                lib().decds_repairing_blob_free(self._h)
-                self._h = None
+            self.free()
         except Exception:
             pass
 

@@ -14,10 +14,16 @@ class Context:
     """One gfx950 device (decds_ctx). Defaults: GF(2^8) poly 0x11D, marker 0x81 (rlnc 0.4.0)."""
 
     def __init__(self, device=0):
+        import weakref
         h = ctypes.c_void_p()
         check(lib().decds_ctx_create(int(device), ctypes.byref(h)))
         self._h = h
         self.device = device
+        self._dependents = weakref.WeakSet()  # Blob / RepairingBlob objects built on this context
+
+    def _adopt(self, obj):
+        """obj (with a free() method) is released before this context is destroyed"""
+        self._dependents.add(obj)
 
     @property
     def handle(self):
@@ -32,7 +38,11 @@ class Context:
         return p.value, m.value
 
     def close(self):
+        """destroys the context; objects built on it (Blob, RepairingBlob) are released first, so
+        none of them outlives the device state it uses"""
         if self._h:
+            for d in list(getattr(self, "_dependents", ())):
+                d.free()
             lib().decds_ctx_destroy(self._h)
             self._h = None
 

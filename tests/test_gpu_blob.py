@@ -294,7 +294,7 @@ def test_repairing_blob_sharded_and_spilled_match_one_context(ctx):
             assert rep.get_repaired_chunkset(c) == data[c * CS:min(blob_len, (c + 1) * CS)].tobytes(), (name, c)
         assert rep.memory()["device_chunksets"] == 0 and rep.memory()["spilled_chunksets"] == 0
         _raises("ChunksetAlreadyRepaired", rep.add_chunk, arrivals[0])
-    del cases, ref
+    del cases, ref, rep
     ctx2.close()
 
 
@@ -311,3 +311,17 @@ def test_host_buffer_views_keep_the_block_alive(ctx):
     assert int(view.sum()) == 7 * 1000          # and no later allocation aliases it
     assert other.free() is True
     del view
+
+
+def test_context_close_releases_its_objects_first(ctx):
+    # a RepairingBlob / Blob built on a context that is closed while they are alive is released
+    # first (Context.close): no destructor touches freed device state afterwards
+    data, _, blob = _blob(ctx, CS + 5, 0x8B80)
+    header = blob.get_blob_header()
+    ctx2 = decds_amd.Context(0)
+    rep = decds_amd.RepairingBlob([ctx, ctx2], header)
+    b2 = decds_amd.Blob([ctx2], data)
+    rep.add_chunk(blob.get_chunk(0, 1))
+    ctx2.close()
+    assert rep._h is None and b2._h is None
+    del rep, b2
