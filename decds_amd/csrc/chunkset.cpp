@@ -72,8 +72,10 @@ namespace {
 
 size_t max_lanes() {
     static const size_t m = [] {
+        // 8 lanes: 16 concurrent lanes ran slower than 8 (19.0 against 25.0 GiB/s of ChunkSet::new at 16
+        // callers, r05d) — further callers wait for a free lane instead
         const char *e = std::getenv("DECDS_MAX_LANES");
-        const int v = e ? std::atoi(e) : 16;
+        const int v = e ? std::atoi(e) : 8;
         return (size_t)std::max(1, v);
     }();
     return m;
@@ -143,7 +145,10 @@ std::mt19937_64 &rng() {
 // one fused encode + chunk-hashing launch (rlnc_encode_hash_kernel, per-request chunkset ids) + fold
 // + Merkle, D2H of each request's rows and proofs into its own page-locked block — then wakes the
 // callers, who copy their rows out. Two slots: one batch's D2H overlaps the next batch's H2D.
-// A lone caller runs a batch of one. DECDS_CHUNKSET_COALESCE=0 keeps the per-call lane path.
+// A lone caller runs a batch of one. Opt-in (DECDS_CHUNKSET_COALESCE=1, read per call): measured
+// against per-call lanes capped at 8 it lost at every caller count (1 / 4 / 8 / 16 callers: 6.4 /
+// 18.3 / 21.9 / 23.7 GiB/s against 10.5 / 23.1 / 25.0 / 25.0, r05d): the per-call H2D + kernels +
+// D2H already keep the link busy from 4 callers on, and a batch adds its slowest member's latency.
 constexpr size_t CO_MAX = 16;
 constexpr size_t CO_P = DECDS_CODED_PITCH_ALIGNED;  // rows 16 bytes past a 128-byte boundary: the fused form
 
@@ -193,7 +198,8 @@ constexpr size_t CO_OUT = N * F + 32 + N * PROOF_SIZE * 32;
 
 struct CoSlot {
     hipStream_t s = nullptr;
-    uint8_t *d_src = nullptr, *d_rows = nullptr, *d_small = nullptr, *d_ws = nullptr, *h_small = nullptr;
+    uint8_t *d_src = nullptr, *d_rows = nullptr, *d_packed = nullptr, *d_small = nullptr, *d_ws = nullptr,
+            *h_small = nullptr;
     uint8_t *rows = nullptr;  // message-aligned: row 0 16 bytes past a 128-byte boundary
     bool busy = false;
     // d_small / h_small: cv (CO_MAX x 160) | ids (CO_MAX x 8) | digests | roots | proofs
@@ -204,6 +210,7 @@ struct CoSlot {
         if ((e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking)) ||
             (e = hipMalloc(reinterpret_cast<void **>(&d_src), CO_MAX * CS)) ||
             (e = hipMalloc(reinterpret_cast<void **>(&d_rows), CO_MAX * N * CO_P + 256)) ||
+            (e = hipMalloc(reinterpret_cast<void **>(&d_packed), CO_MAX * N * F)) ||
             (e = hipMalloc(reinterpret_cast<void **>(&d_small), BYTES)) ||
             (e = hipMalloc(reinterpret_cast<void **>(&d_ws), decds_encode_commit_workspace_bytes(CO_MAX))) ||
             (e = hipHostMalloc(reinterpret_cast<void **>(&h_small), BYTES, DECDS_HOST_MALLOC_FLAGS)))
@@ -213,7 +220,7 @@ struct CoSlot {
     }
     ~CoSlot() {
         if (s) (void)hipStreamSynchronize(s);
-        for (uint8_t *p : {d_src, d_rows, d_small, d_ws})
+        for (uint8_t *p : {d_src, d_rows, d_packed, d_small, d_ws})
             if (p) (void)hipFree(p);
         if (h_small) (void)hipHostFree(h_small);
         if (s) (void)hipStreamDestroy(s);
@@ -233,12 +240,10 @@ struct Coalescer {
     }
 };
 
+// off by default: per-call lanes capped at 8 measured faster at 1-16 callers
 bool coalesce_enabled() {
-    static const bool on = [] {
-        const char *e = std::getenv("DECDS_CHUNKSET_COALESCE");
-        return !e || std::atoi(e) != 0;
-    }();
-    return on;
+    const char *e = std::getenv("DECDS_CHUNKSET_COALESCE");
+    return e && std::atoi(e) != 0;
 }
 
 // one batch of m requests on slot sl (the caller holds sl.busy); returns the batch status
@@ -258,9 +263,13 @@ int co_run(decds_ctx *ctx, CoSlot &sl, EncReq *const *req, size_t m) {
                               reinterpret_cast<const uint64_t *>(sl.d_small + CoSlot::O_IDS), sl.d_small + CoSlot::O_DIG,
                               sl.d_small + CoSlot::O_ROOT, sl.d_small + CoSlot::O_PRF, sl.d_ws, sl.s);
     if (s) return s;
+    // rows repacked at pitch F on the device (a blit over HBM), so each request's 16 rows leave in one
+    // contiguous DMA: a host-side 2D copy of odd-length rows was the slow path (r05c: 3.4 GiB/s)
+    if ((e = hipMemcpy2DAsync(sl.d_packed, F, sl.rows, CO_P, F, m * N, hipMemcpyDeviceToDevice, sl.s)))
+        return decds_hip_error(e, "D2D (row repack)");
     for (size_t i = 0; i < m; i++) {
         uint8_t *o = req[i]->out;
-        if ((e = hipMemcpy2DAsync(o, F, sl.rows + i * N * CO_P, CO_P, F, N, hipMemcpyDeviceToHost, sl.s)) ||
+        if ((e = hipMemcpyAsync(o, sl.d_packed + i * N * F, N * F, hipMemcpyDeviceToHost, sl.s)) ||
             (e = hipMemcpyAsync(o + N * F, sl.d_small + CoSlot::O_ROOT + i * 32, 32, hipMemcpyDeviceToHost, sl.s)) ||
             (e = hipMemcpyAsync(o + N * F + 32, sl.d_small + CoSlot::O_PRF + i * N * PROOF_SIZE * 32, N * PROOF_SIZE * 32,
                                 hipMemcpyDeviceToHost, sl.s)))

@@ -236,17 +236,21 @@ __device__ __forceinline__ void xor3_into(uint32_t (&acc)[4], const u32x4 &a, co
 // The row address of a lookup is nibble * 16 (the table base is the instruction's offset): byte p's
 // high nibble masked in place (xw >> 8p) & 0xF0, its low nibble masked and shifted up by 4 — hipcc
 // turns both into one SDWA op each (v_and_b32_sdwa / v_lshlrev_b32_sdwa with a byte select).
-template <int G, int DW, uint32_t TB>
-__device__ __forceinline__ void lds_issue(u32x4 (&r)[8], uint32_t xw) {
-    constexpr int i = G / DW;
+// HB = bytes of the input dword per group (4: 8 reads per group, 16 in flight; 2: 4 reads per group,
+// 8 in flight and half the result registers — for kernels that need the VGPRs for occupancy).
+template <int G, int DW, uint32_t TB, int HB = 4>
+__device__ __forceinline__ void lds_issue(u32x4 (&r)[2 * HB], uint32_t xw) {
+    constexpr int PARTS = 4 / HB, g2 = G / PARTS, part = G % PARTS;
+    constexpr int i = g2 / DW;
     constexpr uint32_t tlo = TB + (2 * i) * TABLE_BYTES, thi = TB + (2 * i + 1) * TABLE_BYTES;
     const uint32_t lo4 = xw & 0x0F0F0F0Fu;
 #pragma unroll
-    for (int p = 0; p < 4; p++) {
+    for (int q = 0; q < HB; q++) {
+        const int p = part * HB + q;
         const uint32_t alo = ((lo4 >> (8 * p)) & 0xFFu) << 4;
         const uint32_t ahi = (xw >> (8 * p)) & 0xF0u;
-        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r[2 * p]) : "v"(alo), "i"(tlo));
-        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r[2 * p + 1]) : "v"(ahi), "i"(thi));
+        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r[2 * q]) : "v"(alo), "i"(tlo));
+        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r[2 * q + 1]) : "v"(ahi), "i"(thi));
     }
 }
 
@@ -257,36 +261,41 @@ __device__ __forceinline__ void lds_wait(u32x4 (&r)[8]) {
                  : "i"(CNT)
                  : "memory");
 }
+template <int CNT>
+__device__ __forceinline__ void lds_wait(u32x4 (&r)[4]) {
+    asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]) : "i"(CNT) : "memory");
+}
 
-// Group G of the lookups; input (G+1)/DW's register takes the next block's bytes (ncol0) as soon
-// as that input's lookups are all issued — before this block's stores: gfx9's vmcnt counts stores
-// too, so a load issued behind the stores would also wait for them.
-template <int NIN, int DW, uint32_t TB, int G>
-__device__ __forceinline__ void lds_step(uint32_t (&acc)[4 * DW][4], u32x4 (&ra)[8], u32x4 (&rb)[8],
+// Group G of the lookups; input i's register takes the next block's bytes (ncol0) as soon as that
+// input's lookups are all issued — before this block's stores: gfx9's vmcnt counts stores too, so
+// a load issued behind the stores would also wait for them.
+template <int NIN, int DW, uint32_t TB, int G, int HB = 4>
+__device__ __forceinline__ void lds_step(uint32_t (&acc)[4 * DW][4], u32x4 (&ra)[2 * HB], u32x4 (&rb)[2 * HB],
                                          Vec<DW> (&x)[NIN], const uint8_t *ibase, const uint32_t (&ioff)[NIN],
                                          uint32_t ncol0) {
-    constexpr int NG = DW * NIN;
-    u32x4(&cur)[8] = (G & 1) ? rb : ra;  // group G's results
-    u32x4(&nxt)[8] = (G & 1) ? ra : rb;
+    constexpr int PARTS = 4 / HB, NGI = DW * PARTS, NG = NGI * NIN;  // groups per input, in all
+    u32x4(&cur)[2 * HB] = (G & 1) ? rb : ra;  // group G's results
+    u32x4(&nxt)[2 * HB] = (G & 1) ? ra : rb;
     if constexpr (G + 1 < NG) {
-        lds_issue<G + 1, DW, TB>(nxt, x[(G + 1) / DW][(G + 1) % DW]);
-        if constexpr (((G + 1) % DW) == DW - 1) x[(G + 1) / DW] = ldrow<DW>(ibase, ioff[(G + 1) / DW] + ncol0);
-        lds_wait<8>(cur);
+        constexpr int H = G + 1, hi = H / NGI, hw = (H / PARTS) % DW;
+        lds_issue<H, DW, TB, HB>(nxt, x[hi][hw]);
+        if constexpr ((H % NGI) == NGI - 1) x[hi] = ldrow<DW>(ibase, ioff[hi] + ncol0);
+        lds_wait<2 * HB>(cur);
     } else {
         lds_wait<0>(cur);
     }
-    constexpr int w = G % DW;
+    constexpr int w = (G / PARTS) % DW, part = G % PARTS;
 #pragma unroll
-    for (int p = 0; p < 4; p++) xor3_into(acc[4 * w + p], cur[2 * p], cur[2 * p + 1]);
+    for (int q = 0; q < HB; q++) xor3_into(acc[4 * w + part * HB + q], cur[2 * q], cur[2 * q + 1]);
 }
 
-template <int NIN, int DW, uint32_t TB, int... Gs>
+template <int NIN, int DW, uint32_t TB, int HB, int... Gs>
 __device__ __forceinline__ void lookups(std::integer_sequence<int, Gs...>, uint32_t (&acc)[4 * DW][4],
                                         Vec<DW> (&x)[NIN], const uint8_t *ibase, const uint32_t (&ioff)[NIN],
                                         uint32_t ncol0) {
-    u32x4 ra[8], rb[8];
-    lds_issue<0, DW, TB>(ra, x[0][0]);
-    (lds_step<NIN, DW, TB, Gs>(acc, ra, rb, x, ibase, ioff, ncol0), ...);
+    u32x4 ra[2 * HB], rb[2 * HB];
+    lds_issue<0, DW, TB, HB>(ra, x[0][0]);
+    (lds_step<NIN, DW, TB, Gs, HB>(acc, ra, rb, x, ibase, ioff, ncol0), ...);
 }
 
 // One lane block of 4*DW columns: out_j[col0 ..) = sum_i M[j][i] * in_i[col0 ..), tables at LDS
@@ -297,7 +306,8 @@ struct NoSink {
     template <typename V>
     __device__ void operator()(int, const V &) const {}
 };
-template <int NIN, int NOUT, int DW, uint32_t TB = 0, typename Sink = NoSink, int SAUX = 0, bool GSTORE = true>
+template <int NIN, int NOUT, int DW, uint32_t TB = 0, typename Sink = NoSink, int SAUX = 0, bool GSTORE = true,
+          int HB = 4>
 __device__ __forceinline__ void combine_block(Vec<DW> (&x)[NIN], uint8_t *obase, const uint32_t (&ooff)[NOUT],
                                               uint32_t col0, const uint8_t *ibase, const uint32_t (&ioff)[NIN],
                                               uint32_t ncol0, Sink sink = Sink{}) {
@@ -306,7 +316,7 @@ __device__ __forceinline__ void combine_block(Vec<DW> (&x)[NIN], uint8_t *obase,
     for (int c = 0; c < 4 * DW; c++)
 #pragma unroll
         for (int q = 0; q < 4; q++) acc[c][q] = 0;
-    lookups<NIN, DW, TB>(std::make_integer_sequence<int, DW * NIN>{}, acc, x, ibase, ioff, ncol0);
+    lookups<NIN, DW, TB, HB>(std::make_integer_sequence<int, DW * NIN * (4 / HB)>{}, acc, x, ibase, ioff, ncol0);
     // columns x outputs -> outputs x columns
 #pragma unroll
     for (int q = 0; q < 4; q++) {
@@ -386,7 +396,7 @@ __device__ __forceinline__ uint32_t tile_col(uint32_t t, uint32_t tb, uint32_t p
 // merges paths that issued no stores and waits with vmcnt(NIN-1) for the next tile's first input:
 // every tile then waited for the previous tile's stores as well; here it waits for the inputs only.
 // HAVE: x already holds tile ta's inputs (loaded before the workgroup's table build).
-template <int NIN, int NOUT, int DW, bool HAVE, bool MSG = false>
+template <int NIN, int NOUT, int DW, bool HAVE, bool MSG = false, int HB = 4>
 __device__ __forceinline__ void stream_range(uint32_t ta, uint32_t tb, uint32_t phase, const uint8_t *ibase,
                                              const uint32_t (&ioff)[NIN], uint8_t *obase,
                                              const uint32_t (&ooff)[NOUT], Vec<DW> (&x)[NIN]) {
@@ -400,7 +410,7 @@ __device__ __forceinline__ void stream_range(uint32_t ta, uint32_t tb, uint32_t 
     uint32_t t = ta;
 #pragma unroll 1
     do {
-        combine_block<NIN, NOUT, DW>(x, obase, ooff, col(t), ibase, ioff, col(t + 1));
+        combine_block<NIN, NOUT, DW, 0, NoSink, 0, true, HB>(x, obase, ooff, col(t), ibase, ioff, col(t + 1));
     } while (++t < tb);
 }
 
@@ -427,6 +437,10 @@ static_assert(MSG_HEAD == 32, "message tiling");
 // coded-row stores non-temporal: the rows are never read back here, and out of L2 they leave it to the
 // input lines whose second half the next step reads (PMC reads 1.69 -> 1.44 GB per cfg2 launch, -0.6 %)
 constexpr int FH_STORE_AUX = 2;
+#ifndef DECDS_FH_HB
+#define DECDS_FH_HB 4  // lookup group size (bytes of an input dword) in the fused kernel: 2 halves its registers
+#endif
+constexpr int FH_HB = DECDS_FH_HB;
 template <int DW> constexpr uint32_t FH_STEP = 16 * COLS<DW>;           // 128 / 256 message bytes per chunk
 template <int DW> constexpr uint32_t FH_LDS = LDS_BYTES + FH_WAVES * 64 * FH_STEP<DW>;  // 37 / 69 KiB
 template <int DW>
@@ -527,7 +541,8 @@ void rlnc_encode_hash_kernel(const uint8_t *__restrict__ src, size_t n, const ui
     uint32_t st = 0;
 #pragma unroll 1
     do {
-        combine_block<K, N, DW, 0, decltype(sink), FH_STORE_AUX>(x, obase, ooff, col(st), ibase, ioff, col(st + 1), sink);
+        combine_block<K, N, DW, 0, decltype(sink), FH_STORE_AUX, true, FH_HB>(x, obase, ooff, col(st), ibase, ioff,
+                                                                             col(st + 1), sink);
         // one wave: its LDS accesses complete in order, no barrier between the slot writes and reads
 #pragma unroll
         for (uint32_t kb = 0; kb < BPS; kb++) {
@@ -684,6 +699,9 @@ void rlnc_encode_sweep_kernel(const uint8_t *__restrict__ src, size_t n, const u
 #ifndef DECDS_DEC_WAVES
 #define DECDS_DEC_WAVES 2  // waves per SIMD (3 measured no faster, r02f)
 #endif
+#ifndef DECDS_DEC_HB
+#define DECDS_DEC_HB 4  // decode lookup group size (2: half the lookup registers, for more waves per SIMD)
+#endif
 template <uint32_t UNIT>
 __global__ __launch_bounds__(WG, DECDS_DEC_WAVES) __attribute__((amdgpu_waves_per_eu(DECDS_DEC_WAVES, DECDS_DEC_WAVES)))
 void rlnc_decode_kernel(const uint8_t *__restrict__ coded, size_t pitch, size_t n, const RepairPlan *__restrict__ plan,
@@ -752,7 +770,7 @@ void rlnc_decode_kernel(const uint8_t *__restrict__ coded, size_t pitch, size_t 
     }
     // (realigning the piece stores — pieces start i bytes past alignment — through LDS staging or a DPP
     // wave shift measured 4-5 % slower / spilled: r02v/w)
-    stream_range<K, K, DW, DECDS_PREFETCH_FIRST>(tile0, tile0 + UNIT, phase, ibase, ioff, obase, ooff, x);
+    stream_range<K, K, DW, DECDS_PREFETCH_FIRST, false, DECDS_DEC_HB>(tile0, tile0 + UNIT, phase, ibase, ioff, obase, ooff, x);
 }
 
 // One wave per chunkset. Replays rlnc's incremental rank test over the candidates' 10-byte coding

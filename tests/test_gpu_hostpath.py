@@ -196,11 +196,15 @@ def test_pinned_block_cache_reuse_and_trim(ctx):
     L.decds_host_cache_trim()
 
 
-def test_chunkset_new_16_concurrent_callers_coalesced(ctx):
-    # ChunkSet::new from 16 threads at once (Blob::new's rayon loop, blob.rs:256-264): the calls are
-    # gathered into shared fused encode + hashing launches with per-request chunkset ids, so unrelated
-    # ids in one batch must each get their own digests (chunk.rs:40-46, id = chunkset_id*16+j), root
-    # and proofs; every chunkset bit-exact against the oracle, several rounds so batches mix callers
+@pytest.mark.parametrize("coalesce", ["0", "1"])
+def test_chunkset_new_16_concurrent_callers(ctx, coalesce, monkeypatch):
+    # ChunkSet::new from 16 threads at once (Blob::new's rayon loop, blob.rs:256-264). Coalesced, the
+    # calls are gathered into shared fused encode + hashing launches with per-request chunkset ids, so
+    # unrelated ids in one batch must each get their own digests (chunk.rs:40-46, id =
+    # chunkset_id*16+j), root and proofs; every chunkset bit-exact against the oracle, several rounds
+    # so batches mix callers
+    # coalesce "0": per-call lanes (8 at most, the rest wait); "1": the opt-in coalesced launches
+    monkeypatch.setenv("DECDS_CHUNKSET_COALESCE", coalesce)
     T, rounds = 16, 3
     ids = [7 + 1000 * t for t in range(T)]
     errors, results = [], {}
