@@ -19,7 +19,7 @@
 //
 // Only the shipped configuration lives here. The round-1 study variants (persistent walks, XCD
 // bands, per-half work shares, per-tile barriers, the warp-specialised kernel, timing hooks) are in
-// tools/study/rlnc_kernels_r01_study.hip with their measurements in DESIGN.md §8.
+// git history (tools/study/rlnc_kernels_r01_study.hip at a5d9101) with their measurements in DESIGN.md §8.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
