@@ -44,6 +44,12 @@ constexpr uint32_t SWEEP_LDS = 2 * LDS_BYTES + 16;             // two table buff
 #ifndef DECDS_BUILD_XOR
 #define DECDS_BUILD_XOR 1  // table builds in a bank-conflict-free row order (build_tables)
 #endif
+// encode lookup groups of 2 bytes (8 reads in flight per wave) against 4 (16 in flight): -1.0...-1.6 %
+// encode time at 103-1639 chunksets (r05g, same 2 waves/SIMD); groups of 1 byte +4.5 %, also at the
+// 3 waves/SIMD they make room for (167 VGPRs, r05g)
+#ifndef DECDS_ENC_HB
+#define DECDS_ENC_HB 2  // encode lookup group size (bytes of an input dword per group)
+#endif
 #ifndef DECDS_DEC_UNIT
 #define DECDS_DEC_UNIT 1  // decode tiles per workgroup (+3...+11 % against 8 once the tables stopped being replicated, r02e)
 #endif
@@ -262,6 +268,10 @@ __device__ __forceinline__ void lds_wait(u32x4 (&r)[8]) {
                  : "memory");
 }
 template <int CNT>
+__device__ __forceinline__ void lds_wait(u32x4 (&r)[2]) {
+    asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(r[0]), "+v"(r[1]) : "i"(CNT) : "memory");
+}
+template <int CNT>
 __device__ __forceinline__ void lds_wait(u32x4 (&r)[4]) {
     asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]) : "i"(CNT) : "memory");
 }
@@ -437,8 +447,10 @@ static_assert(MSG_HEAD == 32, "message tiling");
 // coded-row stores non-temporal: the rows are never read back here, and out of L2 they leave it to the
 // input lines whose second half the next step reads (PMC reads 1.69 -> 1.44 GB per cfg2 launch, -0.6 %)
 constexpr int FH_STORE_AUX = 2;
+// lookup groups of 2 bytes in the fused kernel too: -1.3 % at 103 / 256 chunksets (r05e); at 4
+// waves/SIMD (117 VGPRs) -0.9 / -1.4 %: the compressions, not occupancy, set its time
 #ifndef DECDS_FH_HB
-#define DECDS_FH_HB 4  // lookup group size (bytes of an input dword) in the fused kernel: 2 halves its registers
+#define DECDS_FH_HB 2
 #endif
 constexpr int FH_HB = DECDS_FH_HB;
 template <int DW> constexpr uint32_t FH_STEP = 16 * COLS<DW>;           // 128 / 256 message bytes per chunk
@@ -676,8 +688,8 @@ void rlnc_encode_sweep_kernel(const uint8_t *__restrict__ src, size_t n, const u
         more = tn < total;
         const uint32_t csn = more ? tn / T : cs;
         cw = table_coeffs_all<K, N>(coeffs + (size_t)csn * N * K, K);
-        combine_block<K, N, DW>(x, dst + (size_t)cs * N * pitch, ooff, col_of(t), src + (size_t)csn * CS, ioff,
-                                more ? col_of(tn) : OOB_COL);
+        combine_block<K, N, DW, 0, NoSink, 0, true, DECDS_ENC_HB>(x, dst + (size_t)cs * N * pitch, ooff, col_of(t),
+                                                                  src + (size_t)csn * CS, ioff, more ? col_of(tn) : OOB_COL);
         lds_barrier();
         t = tn;
         cs = csn;
@@ -696,11 +708,15 @@ void rlnc_encode_sweep_kernel(const uint8_t *__restrict__ src, size_t n, const u
 // rows plan.sel[k] of its 16-row group at coded + cs*16*pitch, or — gather form, in_bases != NULL —
 // rows plan.sel[k] at in_bases[cs] + sel*pitch, written to out_bases[cs] (the incremental
 // RepairingBlob keeps each chunkset's accepted rows in its own device slot).
+// 4 waves per SIMD with lookup groups of 2 bytes (8 reads in flight per wave, 128 VGPRs) against
+// round 2's 2 waves with groups of 4 (16 in flight, 149 VGPRs): -2...-6 % decode time at 103-1639
+// chunksets on two boxes (r05e, r05f). More waves keep more piece stores in flight; groups of 1
+// byte (105 VGPRs) lose some of it back, 5 waves spill. (Round 2's 3 waves were with groups of 4.)
 #ifndef DECDS_DEC_WAVES
-#define DECDS_DEC_WAVES 2  // waves per SIMD (3 measured no faster, r02f)
+#define DECDS_DEC_WAVES 4
 #endif
 #ifndef DECDS_DEC_HB
-#define DECDS_DEC_HB 4  // decode lookup group size (2: half the lookup registers, for more waves per SIMD)
+#define DECDS_DEC_HB 2  // decode lookup group size (bytes of an input dword per group)
 #endif
 template <uint32_t UNIT>
 __global__ __launch_bounds__(WG, DECDS_DEC_WAVES) __attribute__((amdgpu_waves_per_eu(DECDS_DEC_WAVES, DECDS_DEC_WAVES)))
