@@ -149,7 +149,10 @@ typedef struct decds_chunkset decds_chunkset;
 /* ChunkSet::new(chunkset_id, data) (chunkset.rs:37-69): RLNC encode + the commitment (16 chunk
  * digests, Merkle root, 16 proofs) on the device. len != 10 MiB -> DECDS_ERR_INVALID_CHUNKSET_SIZE.
  * coeffs: 16 x 10 coding vectors, or NULL to draw them from the library's RNG (the reference
- * draws from rand::rng(), chunkset.rs:42). */
+ * draws from rand::rng(), chunkset.rs:42). Thread-safe: concurrent callers (Blob::new's rayon
+ * workers, blob.rs:256-264) each take one of the context's lanes (stream, device buffers,
+ * page-locked staging; at most DECDS_MAX_LANES, default 8, further callers wait for one), or with
+ * env DECDS_CHUNKSET_COALESCE=1 are gathered into shared fused encode + hashing launches. */
 int decds_chunkset_new(decds_ctx *ctx, size_t chunkset_id, const uint8_t *data, size_t len,
                        const uint8_t *coeffs, decds_chunkset **out);
 /* ChunkSet::get_root_commitment (chunkset.rs:72-74): 32-byte Merkle root of the 16 chunk digests */
