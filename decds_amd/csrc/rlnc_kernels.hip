@@ -718,13 +718,16 @@ void rlnc_encode_sweep_kernel(const uint8_t *__restrict__ src, size_t n, const u
 #ifndef DECDS_DEC_HB
 #define DECDS_DEC_HB 2  // decode lookup group size (bytes of an input dword per group)
 #endif
+#ifndef DECDS_DEC_DW
+#define DECDS_DEC_DW 4  // decode lane-block width in dwords (4: 16 columns per lane)
+#endif
 template <uint32_t UNIT>
 __global__ __launch_bounds__(WG, DECDS_DEC_WAVES) __attribute__((amdgpu_waves_per_eu(DECDS_DEC_WAVES, DECDS_DEC_WAVES)))
 void rlnc_decode_kernel(const uint8_t *__restrict__ coded, size_t pitch, size_t n, const RepairPlan *__restrict__ plan,
                         uint8_t *__restrict__ dst, int32_t *__restrict__ status, const uint64_t *__restrict__ in_bases,
                         const uint64_t *__restrict__ out_bases, uint32_t poly, uint32_t marker) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    constexpr int DW = 4;
+    constexpr int DW = DECDS_DEC_DW;
     constexpr uint32_t T = TILES<DW>;
     static_assert(T % UNIT == 0, "a workgroup's tiles stay in one chunkset");
     constexpr uint32_t phase = 0;  // aligned decode loads measured slower (+3…+5 %)
@@ -1087,7 +1090,7 @@ hipError_t launch_decode(const LaunchGeom &, const uint8_t *coded, size_t pitch,
     const RepairPlan *pl = reinterpret_cast<const RepairPlan *>(plan);
     constexpr uint32_t U = DEC_UNIT;
     (void)hipGetLastError();  // only this launch's status below
-    hipLaunchKernelGGL(rlnc_decode_kernel<U>, dim3((uint32_t)(n * (TILES<4> / U))), dim3(WG), LDS_BYTES, stream, coded,
+    hipLaunchKernelGGL(rlnc_decode_kernel<U>, dim3((uint32_t)(n * (TILES<DECDS_DEC_DW> / U))), dim3(WG), LDS_BYTES, stream, coded,
                        pitch, n, pl, dst, status, in_bases, out_bases, poly, marker);
     return hipGetLastError();
 }
