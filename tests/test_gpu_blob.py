@@ -191,7 +191,8 @@ def test_repairing_blob_all_chunks_shuffled_batch_vs_sequential(ctx):
     assert set(bat.add_chunks(arrivals[:20]).tolist()) == {10}
 
 
-def test_repairing_blob_cfg2_slots_span_4gib_windows(ctx):
+@pytest.mark.parametrize("budget", [None, "2 slabs"])
+def test_repairing_blob_cfg2_slots_span_4gib_windows(ctx, budget):
     # cfg2 through RepairingBlob: 103 chunksets, 10 random survivors each, validated in device batches
     # and decoded from per-chunkset device slots (gather form). The 103 slots span > 2 GiB of slabs, so
     # some slot addresses have bit 31 of their low word set: r02i's fault (a sign-extended
@@ -213,16 +214,24 @@ def test_repairing_blob_cfg2_slots_span_4gib_windows(ctx):
             rows[r] = np.frombuffer(ch.erasure_coded_data, np.uint8)
             ids[r] = (c, ch.chunk_id)
             proofs[r] = np.frombuffer(b"".join(ch.proof), np.uint8)
-    rep = decds_amd.RepairingBlob(ctx, header)
+    # "2 slabs": a device budget of one decode area + 16 chunksets' rows; the other 87 chunksets' rows
+    # spill to page-locked host memory and are staged into the decode area one by one
+    rep = decds_amd.RepairingBlob(ctx, header, device_budget=None if budget is None else _AREA + 2 * _SLAB)
     st = rep.add_rows(rows, ids, proofs, plen)
     del rows
     assert set(st.tolist()) <= {0, 4}  # accepted, or not useful (a dependent survivor)
+    mem = rep.memory()
+    assert mem["spilled_chunksets"] == (0 if budget is None else n - 16), mem
     out = decds_amd.HostBuffer(CS)
     for c in range(n):
         if not rep.is_chunkset_ready_to_repair(c):
             continue
         got = rep.get_repaired_chunkset(c, out=out.array)
         assert np.array_equal(got, data[c * CS:min(blob_len, (c + 1) * CS)]), c
+    del got
+    left = rep.memory()                       # only chunksets that never became ready keep their rows
+    not_ready = sum(not rep.is_chunkset_ready_to_repair(c) and not rep.is_chunkset_already_repaired(c) for c in range(n))
+    assert left["device_chunksets"] + left["spilled_chunksets"] == not_ready, left
 
 
 # the decode-area + one-slab budget of decds_repairing_blob_set_device_budget (blob.cpp RbShard)

@@ -21,6 +21,12 @@ sys.path.insert(0, ROOT)
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gib", type=float, default=1.0)
+    ap.add_argument("--share-major", action="store_true",
+                    help="chunks arrive share by share over all chunksets (every chunkset open at once, as "
+                         "Blob::get_share hands them out) instead of chunkset by chunkset")
+    ap.add_argument("--budgets-mb", default="", help="comma list of RepairingBlob device budgets (MiB) to time "
+                                                       "the sequential add_chunk path under, e.g. 0,512")
+    ap.add_argument("--contexts", type=int, default=1, help="RepairingBlob over this many contexts of device 0")
     a = ap.parse_args()
     import numpy as np
     import torch  # noqa: F401  (torch's HIP runtime first, as the other tools)
@@ -48,14 +54,18 @@ def main():
     # pointers to every picked chunk inside the blob (zero-copy) and its proof
     dp = ctypes.c_void_p()
     chunks = []
-    for c in range(n):
-        for j in picks[c]:
-            proof = ctypes.create_string_buffer(32 * plen)
-            check(L.decds_blob_get_chunk(blob._h, c, int(j), ctypes.byref(dp), proof, len(proof)))
-            chunks.append((c, c * N + int(j), dp.value, proof))
+    order = [(c, k) for k in range(K) for c in range(n)] if a.share_major else [(c, k) for c in range(n) for k in range(K)]
+    res["arrival"] = "share-major" if a.share_major else "chunkset-major"
+    for c, k in order:
+        j = picks[c][k]
+        proof = ctypes.create_string_buffer(32 * plen)
+        check(L.decds_blob_get_chunk(blob._h, c, int(j), ctypes.byref(dp), proof, len(proof)))
+        chunks.append((c, c * N + int(j), dp.value, proof))
+    ctxs = [ctx] + [decds_amd.Context(0) for _ in range(a.contexts - 1)]
+    res["contexts"] = a.contexts
 
-    def repair(batched):
-        rb = RepairingBlob(ctx, header)
+    def repair(batched, budget=None):
+        rb = RepairingBlob(ctxs if len(ctxs) > 1 else ctx, header, device_budget=budget)
         t0 = time.perf_counter()
         if batched:
             m = len(chunks)
@@ -75,6 +85,7 @@ def main():
                 if s not in (0, 4):  # 4: ChunkDecodingFailed (a dependent chunk), which the reference tolerates
                     check(s)
         t_add = time.perf_counter() - t0
+        mem = rb.memory()
         out = HostBuffer(CS)
         t_get = 0.0
         ok = 0
@@ -88,15 +99,21 @@ def main():
             lo = c * CS
             assert np.array_equal(got, data.array[lo:lo + got.size]), c
             ok += 1
+        del got
         out.free()
-        return t_add, t_get, ok
+        rb.free()
+        return t_add, t_get, ok, mem
 
-    for name, batched in (("add_chunk", False), ("add_chunks_batch", True)):
-        t_add, t_get, ok = repair(batched)
+    runs = [("add_chunk", False, None), ("add_chunks_batch", True, None)]
+    runs += [("add_chunk_budget_%sMiB" % b, False, int(b) << 20) for b in a.budgets_mb.split(",") if b != ""]
+    for name, batched, budget in runs:
+        t_add, t_get, ok, mem = repair(batched, budget)
         gib_ok = ok * CS / (1 << 30)
         res[name] = {"add_s": round(t_add, 3), "get_repaired_s": round(t_get, 3), "repaired_chunksets": ok,
                      "GiBps": round(gib_ok / (t_add + t_get), 2),
-                     "per_chunk_add_us": round(t_add / len(chunks) * 1e6, 1)}
+                     "per_chunk_add_us": round(t_add / len(chunks) * 1e6, 1),
+                     "device_chunksets": mem["device_chunksets"], "spilled_chunksets": mem["spilled_chunksets"],
+                     "device_MiB": round(mem["device_bytes"] / 2 ** 20, 1)}
     # a second Blob::new of the same size after the first is freed: its coded store comes from the
     # library's page-locked block cache instead of being page-locked again
     t0 = time.perf_counter()
