@@ -214,9 +214,10 @@ def test_repairing_blob_cfg2_slots_span_4gib_windows(ctx, budget):
             rows[r] = np.frombuffer(ch.erasure_coded_data, np.uint8)
             ids[r] = (c, ch.chunk_id)
             proofs[r] = np.frombuffer(b"".join(ch.proof), np.uint8)
-    # "2 slabs": a device budget of one decode area + 16 chunksets' rows; the other 87 chunksets' rows
-    # spill to page-locked host memory and are staged into the decode area one by one
-    rep = decds_amd.RepairingBlob(ctx, header, device_budget=None if budget is None else _AREA + 2 * _SLAB)
+    # "2 slabs": a device budget of two decode areas (a quarter of the budget goes to areas) + 16
+    # chunksets' rows; the other 87 chunksets' rows spill to page-locked host memory and are staged
+    # into the decode areas at their decode
+    rep = decds_amd.RepairingBlob(ctx, header, device_budget=None if budget is None else 2 * _AREA + 2 * _SLAB)
     st = rep.add_rows(rows, ids, proofs, plen)
     del rows
     assert set(st.tolist()) <= {0, 4}  # accepted, or not useful (a dependent survivor)
