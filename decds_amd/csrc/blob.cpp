@@ -890,18 +890,25 @@ int decds_repairing_blob_add_chunk(decds_repairing_blob *rb, uint64_t chunkset_i
     // chunkset id in range, then the first 4 hashes against the chunkset root (chunk.rs:88-110)
     bool ok = proof && proof_len >= PROOF_SIZE && (data || len == 0);
     if ((s = decds_ctx_bind(sh.ctx))) return s;
-    // a full-length row is copied into a staging piece while it is hashed (the copy is only sent to
-    // the device if the chunk is accepted into a device slot); the caller's buffer is free on return
+    // a full-length row is copied while it is hashed: into a staging piece (sent to the device only if
+    // the chunk is accepted into a device slot), or, for a chunkset whose rows are spilled, straight
+    // into the host slot row it would take (rank unchanged on rejection: the row is simply reused);
+    // the caller's buffer is free on return
     int piece = -1;
-    uint8_t *staged = nullptr;
+    uint8_t *staged = nullptr, *direct = nullptr;
+    {
+        const RbChunkset &cc = rb->cs[chunkset_id];
+        if (cc.hslot >= 0 && cc.rank < K) direct = sh.hslot_rows(cc.hslot) + cc.rank * F;
+    }
     if (ok) {
         uint8_t leaf[32];
         if (len == F && b3h::simd_available()) {
-            hipError_t e = sh.in_ring.stage(&piece, &staged);
+            hipError_t e = direct ? hipSuccess : sh.in_ring.stage(&piece, &staged);
             if (e) return decds_hip_error(e, "staging piece");
+            uint8_t *const to = direct ? direct : staged;
             constexpr size_t HALF = (F + 1) / 2;
             const std::function<void(size_t)> copy = [&](size_t h) {
-                std::memcpy(staged + h * HALF, data + h * HALF, h ? F - HALF : HALF);
+                std::memcpy(to + h * HALF, data + h * HALF, h ? F - HALF : HALF);
             };
             full_piece_digest(chunkset_id, chunk_id, data, leaf, &copy, 2);
         } else {
@@ -917,7 +924,9 @@ int decds_repairing_blob_add_chunk(decds_repairing_blob *rb, uint64_t chunkset_i
     if ((s = rb->accept(chunkset_id, data, len, &row))) return s;
     const RbChunkset &c = rb->cs[chunkset_id];
     if (c.hslot >= 0) {  // spilled: the row stays in page-locked host memory until its decode
-        std::memcpy(sh.hslot_rows(c.hslot) + row * F, staged ? staged : data, F);
+        uint8_t *dst = sh.hslot_rows(c.hslot) + row * F;
+        const bool copied = dst == direct && len == F && b3h::simd_available();  // during the hashing
+        if (!copied) par_memcpy(dst, staged ? staged : data, F);
         return DECDS_OK;
     }
     uint8_t *dst = sh.slot_rows(c.slot) + row * F;
@@ -987,7 +996,7 @@ static int rb_add_rows_shard(decds_repairing_blob *rb, RbShard &sh, const std::v
             if (st == DECDS_OK) {
                 const RbChunkset &c = rb->cs[cid];
                 if (c.hslot >= 0)
-                    std::memcpy(sh.hslot_rows(c.hslot) + row * F, rows + a * F, F);
+                    par_memcpy(sh.hslot_rows(c.hslot) + row * F, rows + a * F, F);
                 else if ((e = hipMemcpyAsync(sh.slot_rows(c.slot) + row * F, sh.d_batch + i * F, F, hipMemcpyDeviceToDevice,
                                              sh.s)))
                     return decds_hip_error(e, "D2D (accepted row)");
