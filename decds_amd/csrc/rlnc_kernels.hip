@@ -308,64 +308,6 @@ __device__ __forceinline__ void lookups(std::integer_sequence<int, Gs...>, uint3
     (lds_step<NIN, DW, TB, Gs, HB>(acc, ra, rb, x, ibase, ioff, ncol0), ...);
 }
 
-// Byte tables (fused kernel study, DECDS_FH_BYTE): BT[i][x] = { C[j][i] * x : j < 16 } at TB + 4096 i
-// + 16 x, built from the nibble tables: one ds_read_b128 per input byte instead of two, and the two
-// inputs of a pair accumulate with one v_bitop3 — half the lookups, address ops and XORs of the
-// nibble form, at the price of 40 KiB of tables (random rows: bank conflicts within a lane group).
-constexpr uint32_t BT_STRIDE = 256 * ROW_BYTES;  // 4 KiB per input
-template <int G, int DW, uint32_t TB>
-__device__ __forceinline__ void lds_issue_byte(u32x4 (&r)[8], uint32_t xa, uint32_t xb) {
-    constexpr int ip = G / DW;
-    constexpr uint32_t ta = TB + (2 * ip) * BT_STRIDE, tb = TB + (2 * ip + 1) * BT_STRIDE;
-#pragma unroll
-    for (int p = 0; p < 4; p++) {
-        const uint32_t aa = ((xa >> (8 * p)) & 0xFFu) << 4, ab = ((xb >> (8 * p)) & 0xFFu) << 4;
-        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r[2 * p]) : "v"(aa), "i"(ta));
-        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r[2 * p + 1]) : "v"(ab), "i"(tb));
-    }
-}
-template <int NIN, int DW, uint32_t TB, int G>
-__device__ __forceinline__ void lds_step_byte(uint32_t (&acc)[4 * DW][4], u32x4 (&ra)[8], u32x4 (&rb)[8],
-                                              Vec<DW> (&x)[NIN], const uint8_t *ibase, const uint32_t (&ioff)[NIN],
-                                              uint32_t ncol0) {
-    static_assert(NIN % 2 == 0, "inputs in pairs");
-    constexpr int NG = DW * (NIN / 2);
-    u32x4(&cur)[8] = (G & 1) ? rb : ra;
-    u32x4(&nxt)[8] = (G & 1) ? ra : rb;
-    if constexpr (G + 1 < NG) {
-        constexpr int H = G + 1, hp = H / DW, hw = H % DW;
-        lds_issue_byte<H, DW, TB>(nxt, x[2 * hp][hw], x[2 * hp + 1][hw]);
-        if constexpr (hw == DW - 1) {
-            x[2 * hp] = ldrow<DW>(ibase, ioff[2 * hp] + ncol0);
-            x[2 * hp + 1] = ldrow<DW>(ibase, ioff[2 * hp + 1] + ncol0);
-        }
-        lds_wait<8>(cur);
-    } else {
-        lds_wait<0>(cur);
-    }
-    constexpr int w = G % DW;
-#pragma unroll
-    for (int p = 0; p < 4; p++) xor3_into(acc[4 * w + p], cur[2 * p], cur[2 * p + 1]);
-}
-template <int NIN, int DW, uint32_t TB, int... Gs>
-__device__ __forceinline__ void lookups_byte(std::integer_sequence<int, Gs...>, uint32_t (&acc)[4 * DW][4],
-                                             Vec<DW> (&x)[NIN], const uint8_t *ibase, const uint32_t (&ioff)[NIN],
-                                             uint32_t ncol0) {
-    u32x4 ra[8], rb[8];
-    lds_issue_byte<0, DW, TB>(ra, x[0][0], x[1][0]);
-    (lds_step_byte<NIN, DW, TB, Gs>(acc, ra, rb, x, ibase, ioff, ncol0), ...);
-}
-// expand the 2*NIN nibble tables at `nib` into NIN byte tables at `bt` (caller brackets with barriers)
-template <int NIN>
-__device__ __forceinline__ void expand_byte_tables(uint8_t *bt, const uint8_t *nib) {
-    for (uint32_t d = threadIdx.x; d < NIN * 256 * 4; d += WG) {
-        const uint32_t i = d / 1024, xv = (d / 4) % 256, q = d % 4;
-        const uint32_t lo = *reinterpret_cast<const uint32_t *>(nib + (i * 2) * TABLE_BYTES + (xv & 15u) * ROW_BYTES + 4 * q);
-        const uint32_t hi = *reinterpret_cast<const uint32_t *>(nib + (i * 2 + 1) * TABLE_BYTES + (xv >> 4) * ROW_BYTES + 4 * q);
-        reinterpret_cast<uint32_t *>(bt)[d] = lo ^ hi;
-    }
-}
-
 // One lane block of 4*DW columns: out_j[col0 ..) = sum_i M[j][i] * in_i[col0 ..), tables at LDS
 // byte TB. x holds this block's inputs on entry and on exit the inputs at column ncol0 of the rows
 // at ibase + ioff (the next block's: the same chunkset's rows, or the next tile's chunkset's).
@@ -375,7 +317,7 @@ struct NoSink {
     __device__ void operator()(int, const V &) const {}
 };
 template <int NIN, int NOUT, int DW, uint32_t TB = 0, typename Sink = NoSink, int SAUX = 0, bool GSTORE = true,
-          int HB = 4, bool BYTE = false>
+          int HB = 4>
 __device__ __forceinline__ void combine_block(Vec<DW> (&x)[NIN], uint8_t *obase, const uint32_t (&ooff)[NOUT],
                                               uint32_t col0, const uint8_t *ibase, const uint32_t (&ioff)[NIN],
                                               uint32_t ncol0, Sink sink = Sink{}) {
@@ -384,10 +326,7 @@ __device__ __forceinline__ void combine_block(Vec<DW> (&x)[NIN], uint8_t *obase,
     for (int c = 0; c < 4 * DW; c++)
 #pragma unroll
         for (int q = 0; q < 4; q++) acc[c][q] = 0;
-    if constexpr (BYTE)
-        lookups_byte<NIN, DW, TB>(std::make_integer_sequence<int, DW * (NIN / 2)>{}, acc, x, ibase, ioff, ncol0);
-    else
-        lookups<NIN, DW, TB, HB>(std::make_integer_sequence<int, DW * NIN * (4 / HB)>{}, acc, x, ibase, ioff, ncol0);
+    lookups<NIN, DW, TB, HB>(std::make_integer_sequence<int, DW * NIN * (4 / HB)>{}, acc, x, ibase, ioff, ncol0);
     // columns x outputs -> outputs x columns
 #pragma unroll
     for (int q = 0; q < 4; q++) {
@@ -515,13 +454,10 @@ constexpr int FH_STORE_AUX = 2;
 #endif
 constexpr int FH_HB = DECDS_FH_HB;
 template <int DW> constexpr uint32_t FH_STEP = 16 * COLS<DW>;           // 128 / 256 message bytes per chunk
-#ifndef DECDS_FH_BYTE
-#define DECDS_FH_BYTE 0  // fused kernel with byte tables (study)
-#endif
-constexpr bool FH_BYTE = DECDS_FH_BYTE != 0;
-constexpr uint32_t FH_TBL = FH_BYTE ? K * BT_STRIDE : LDS_BYTES;  // table bytes: 40 KiB byte / 5 KiB nibble tables
-template <int DW> constexpr uint32_t FH_LDS = FH_TBL + FH_WAVES * 64 * FH_STEP<DW>;  // 37 / 69 KiB (nibble tables)
-static_assert(!FH_BYTE || FH_WAVES * 64 * FH_STEP<2> >= LDS_BYTES, "nibble tables built in the slot area first");
+// (byte tables — one lookup per input byte, 40 KiB of tables, 2 workgroups per CU — measured +2.6 /
+// +2.1 / -2.1 % at 103 / 256 / 1024 chunksets, r05o; in git history at f15b23c)
+constexpr uint32_t FH_TBL = LDS_BYTES;
+template <int DW> constexpr uint32_t FH_LDS = FH_TBL + FH_WAVES * 64 * FH_STEP<DW>;  // 37 / 69 KiB
 template <int DW>
 __device__ __forceinline__ uint32_t fh_key(uint32_t slot) {
     constexpr uint32_t R = 256 / FH_STEP<DW>, P = FH_STEP<DW> / 16;  // slots per bank row, pieces per slot
@@ -575,18 +511,8 @@ void rlnc_encode_hash_kernel(const uint8_t *__restrict__ src, size_t n, const ui
     const uint32_t cw = table_coeffs<K, N>(M, K);
     Vec<DW> x[K];
     load_block<K, DW>(x, ibase, ioff, col(0));
-    if constexpr (FH_BYTE) {  // nibble tables in the (not yet used) slot area, expanded into byte tables
-        build_tables<K, N>(lds + FH_TBL, cw, poly);
-        lds_barrier();
-        expand_byte_tables<K>(lds, lds + FH_TBL);
-    } else {
-        build_tables<K, N>(lds, cw, poly);
-    }
+    build_tables<K, N>(lds, cw, poly);
     lds_barrier();
-    auto tmul = [&](uint32_t i, uint32_t jo, uint32_t xv) -> uint32_t {
-        if constexpr (FH_BYTE) return lds[i * BT_STRIDE + xv * ROW_BYTES + jo];
-        return tbl_mul(lds, i, jo, xv);
-    };
     if (gu == 0) {  // the chunkset's first workgroup: coding-vector prefixes and the edge columns
         for (uint32_t idx = threadIdx.x; idx < N * K; idx += WG) obase[(idx / K) * pitch + idx % K] = M[idx];
         for (uint32_t idx = threadIdx.x; idx < edge_cols<DW, true>(MSG_PHASE) * N; idx += WG) {
@@ -596,7 +522,7 @@ void rlnc_encode_hash_kernel(const uint8_t *__restrict__ src, size_t n, const ui
             for (uint32_t i = 0; i < K; i++) {
                 const uint64_t p = (uint64_t)i * L + c;
                 const uint32_t xv = p < CS ? ibase[p] : (p == CS ? marker : 0u);
-                y ^= tmul(i, j, xv);
+                y ^= tbl_mul(lds, i, j, xv);
             }
             obase[j * pitch + K + c] = (uint8_t)y;
         }
@@ -630,8 +556,8 @@ void rlnc_encode_hash_kernel(const uint8_t *__restrict__ src, size_t n, const ui
     uint32_t st = 0;
 #pragma unroll 1
     do {
-        combine_block<K, N, DW, 0, decltype(sink), FH_STORE_AUX, true, FH_HB, FH_BYTE>(x, obase, ooff, col(st), ibase,
-                                                                                      ioff, col(st + 1), sink);
+        combine_block<K, N, DW, 0, decltype(sink), FH_STORE_AUX, true, FH_HB>(x, obase, ooff, col(st), ibase, ioff,
+                                                                             col(st + 1), sink);
         // one wave: its LDS accesses complete in order, no barrier between the slot writes and reads
 #pragma unroll
         for (uint32_t kb = 0; kb < BPS; kb++) {
