@@ -121,9 +121,12 @@ __device__ __forceinline__ uint32_t table_coeffs_all(const uint8_t *M, uint32_t 
 // order was 8-way conflicted: 5 % of the encode's LDS cycles, r05a PMC). In-process A/B (r05b):
 // ±0.3 % — the build is not what bounds the encode; neither is the second barrier per tile (double-
 // buffered tables with one barrier per tile measured the same and were removed).
-template <int NIN, int NOUT>
+// REMAT: recompute the thread's row addresses at every call. In a loop the compiler otherwise hoists
+// the 16 per-lane ds_write addresses of the XOR order out of it, and a 4-wave kernel spills them.
+template <int NIN, int NOUT, bool REMAT = false>
 __device__ __forceinline__ void build_tables(uint8_t *lds, uint32_t cw, uint32_t poly) {
-    const uint32_t p = threadIdx.x;
+    uint32_t p = threadIdx.x;
+    if constexpr (REMAT) asm volatile("" : "+v"(p));
     if (p < NIN * 8) {
         const uint32_t q = p & 3u, h = (p >> 2) & 1u, i = p >> 3;
         uint32_t bw[4] = {0, 0, 0, 0};
@@ -186,30 +189,33 @@ template <int DW> using Vec = typename VecT<DW>::T;
 constexpr uint32_t BUF_RECORDS = 0x80000000u;
 constexpr uint32_t OOB_COL = 0x80000000u;
 
+// A row access at byte soff + voff of base: soff is wave-uniform (a row's offset), voff the lane's
+// column; both go into the VGPR offset. (The row offset in the instructions' SGPR offset field
+// instead, sharing one column VGPR across a tile's rows, measured 1.5 % slower encodes, r05p.)
 template <int DW>
-__device__ __forceinline__ Vec<DW> ldrow(const uint8_t *base, uint32_t off) {
+__device__ __forceinline__ Vec<DW> ldrow(const uint8_t *base, uint32_t soff, uint32_t voff) {
     const __amdgpu_buffer_rsrc_t r =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(base), 0, BUF_RECORDS, 0x00020000);
     if constexpr (DW == 4)
-        return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+        return __builtin_amdgcn_raw_buffer_load_b128(r, soff + voff, 0, 0);
     else
-        return __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0);
+        return __builtin_amdgcn_raw_buffer_load_b64(r, soff + voff, 0, 0);
 }
 
 template <int DW, int AUX = 0>
-__device__ __forceinline__ void strow(uint8_t *base, uint32_t off, Vec<DW> v) {
+__device__ __forceinline__ void strow(uint8_t *base, uint32_t soff, uint32_t voff, Vec<DW> v) {
     const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, 0, BUF_RECORDS, 0x00020000);
     if constexpr (DW == 4)
-        __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, AUX);
+        __builtin_amdgcn_raw_buffer_store_b128(v, r, soff + voff, 0, AUX);
     else
-        __builtin_amdgcn_raw_buffer_store_b64(v, r, off, 0, AUX);
+        __builtin_amdgcn_raw_buffer_store_b64(v, r, soff + voff, 0, AUX);
 }
 
 template <int NIN, int DW>
 __device__ __forceinline__ void load_block(Vec<DW> (&x)[NIN], const uint8_t *ibase, const uint32_t (&ioff)[NIN],
                                            uint32_t col0) {
 #pragma unroll
-    for (int i = 0; i < NIN; i++) x[i] = ldrow<DW>(ibase, ioff[i] + col0);
+    for (int i = 0; i < NIN; i++) x[i] = ldrow<DW>(ibase, ioff[i], col0);
 }
 
 // 4x4 byte transpose: out[b].byte[p] = in[p].byte[b]
@@ -289,7 +295,7 @@ __device__ __forceinline__ void lds_step(uint32_t (&acc)[4 * DW][4], u32x4 (&ra)
     if constexpr (G + 1 < NG) {
         constexpr int H = G + 1, hi = H / NGI, hw = (H / PARTS) % DW;
         lds_issue<H, DW, TB, HB>(nxt, x[hi][hw]);
-        if constexpr ((H % NGI) == NGI - 1) x[hi] = ldrow<DW>(ibase, ioff[hi] + ncol0);
+        if constexpr ((H % NGI) == NGI - 1) x[hi] = ldrow<DW>(ibase, ioff[hi], ncol0);
         lds_wait<2 * HB>(cur);
     } else {
         lds_wait<0>(cur);
@@ -343,7 +349,7 @@ __device__ __forceinline__ void combine_block(Vec<DW> (&x)[NIN], uint8_t *obase,
 #pragma unroll
             for (int w = 0; w < DW; w++) v[w] = o[b][w];
             if (j < NOUT) {
-                if constexpr (GSTORE) strow<DW, SAUX>(obase, ooff[j] + col0, v);
+                if constexpr (GSTORE) strow<DW, SAUX>(obase, ooff[j], col0, v);
                 sink(j, v);
             }
         }
@@ -414,7 +420,7 @@ __device__ __forceinline__ void stream_range(uint32_t ta, uint32_t tb, uint32_t 
     if constexpr (!HAVE) load_block<NIN, DW>(x, ibase, ioff, col(ta));
     asm volatile("" ::: "memory");  // keep the dropped stores after the loads, as in the loop
 #pragma unroll
-    for (int j = 0; j < NOUT; j++) strow<DW>(obase, OOB_COL + ooff[j], Vec<DW>{});
+    for (int j = 0; j < NOUT; j++) strow<DW>(obase, ooff[j], OOB_COL, Vec<DW>{});
     // ta < tb (callers): a do-while, so no zero-trip guard lets hipcc sink the prologue loads
     // below the dropped stores (it did: vmcnt(9) again)
     uint32_t t = ta;
@@ -536,7 +542,7 @@ void rlnc_encode_hash_kernel(const uint8_t *__restrict__ src, size_t n, const ui
             __builtin_amdgcn_make_buffer_rsrc(obase, 0, BUF_RECORDS, 0x00020000), j * (uint32_t)pitch, 0, 1);
     asm volatile("" ::: "memory");  // the loop's memory-counter picture: inputs, then 16 dropped stores
 #pragma unroll
-    for (int jj = 0; jj < (int)N; jj++) strow<DW>(obase, OOB_COL + ooff[jj], Vec<DW>{});
+    for (int jj = 0; jj < (int)N; jj++) strow<DW>(obase, ooff[jj], OOB_COL, Vec<DW>{});
     uint8_t *wl = lds + FH_TBL + (threadIdx.x >> 6) * 64 * STEP;
     // encode lane's LDS address for rows jj = jm (mod 4) (the swizzle key of slot 4jj + eq depends on
     // jj mod 4 only); row jj adds 4 jj slots
@@ -670,7 +676,7 @@ void rlnc_encode_sweep_kernel(const uint8_t *__restrict__ src, size_t n, const u
     uint32_t grab = grab_next();  // -> the tile after the next
     asm volatile("" ::: "memory");
 #pragma unroll
-    for (int j = 0; j < (int)N; j++) strow<DW>(dst, OOB_COL + ooff[j], Vec<DW>{});
+    for (int j = 0; j < (int)N; j++) strow<DW>(dst, ooff[j], OOB_COL, Vec<DW>{});
     // One tile per iteration: build its tables from the coefficient bytes the previous iteration
     // loaded (issued before that iteration's stores, so the build waits for them alone), barrier, load
     // the next tile's coefficient bytes, then the lookups with the rolling prefetch of the next tile's
@@ -793,6 +799,191 @@ void rlnc_decode_kernel(const uint8_t *__restrict__ coded, size_t pitch, size_t 
     // (realigning the piece stores — pieces start i bytes past alignment — through LDS staging or a DPP
     // wave shift measured 4-5 % slower / spilled: r02v/w)
     stream_range<K, K, DW, DECDS_PREFETCH_FIRST, false, DECDS_DEC_HB>(tile0, tile0 + UNIT, phase, ibase, ioff, obase, ooff, x);
+}
+
+#ifndef DECDS_DEC_SWEEP
+#define DECDS_DEC_SWEEP 0  // 1: the decode as a persistent tile sweep (rlnc_decode_sweep_kernel)
+#endif
+// 3 waves/SIMD: at 4 (128 VGPRs) the loop spills, the tile counter's pending return register among
+// what it spills (tests/test_isa.py checks the built code for exactly that)
+#ifndef DECDS_DEC_SWEEP_WAVES
+#define DECDS_DEC_SWEEP_WAVES 3
+#endif
+#ifndef DECDS_DEC_SWEEP_XR
+#define DECDS_DEC_SWEEP_XR 8  // decode sweep: consecutive tiles per XCD (1 = one global counter)
+#endif
+// table_coeffs_all for a K x K inverse, in the decode sweep's loop: one buffer load base (the plan's
+// inverse, wave-uniform) and one lane offset, recomputed per call (a hoisted per-lane address set
+// spills at 4 waves/SIMD). Lane quad q needs rows 4q..4q+3; rows past NOUT-1 are zero. It loads rows
+// r0..r0+3 with r0 = min(4q, NOUT-4) — never past the inverse — and shifts the word down by the
+// rows it read before 4q.
+template <int NIN, int NOUT>
+__device__ __forceinline__ uint32_t table_coeffs_inv(const uint8_t *M, uint32_t ldm) {
+    static_assert(NOUT >= 4 && NOUT <= 16, "quads of outputs");
+    uint32_t p = threadIdx.x;
+    asm volatile("" : "+v"(p));
+    const bool live = p < NIN * 8;
+    p = live ? p : 0u;
+    const uint32_t q = p & 3u, i = p >> 3;
+    const uint32_t r0 = 4 * q < (uint32_t)NOUT - 4 ? 4 * q : (uint32_t)NOUT - 4, sh = 8 * (4 * q - r0);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(M), 0, NOUT * ldm, 0x00020000);
+    const uint32_t o = r0 * ldm + i;
+    uint32_t w = 0;
+#pragma unroll
+    for (uint32_t jj = 0; jj < 4; jj++) w |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rs, o + jj * ldm, 0, 0) << (8 * jj);
+    w = sh < 32 ? w >> sh : 0u;
+    return live ? w : 0u;
+}
+
+// A chunkset's decode operands: coded-row offsets of the accepted chunks, input/output bases and
+// whether it is ready. The raw loads are issued first (load) and turned into wave-uniform values
+// later (resolve), so their latency hides behind whatever the caller issues in between.
+struct DecodeDesc {
+    uint32_t v0, v1, v2;
+    uint64_t vin, vout;
+    uint32_t ioff[K];
+    const uint8_t *ibase;
+    uint8_t *obase;
+    bool ready;
+    __device__ __forceinline__ void load(const RepairPlan *plan, const uint64_t *in_bases, const uint64_t *out_bases,
+                                         uint32_t c) {
+        const uint32_t *pw = reinterpret_cast<const uint32_t *>(plan + c);
+        v0 = pw[0];
+        v1 = pw[1];
+        v2 = pw[2];
+        if (in_bases) {
+            vin = in_bases[c];
+            vout = out_bases[c];
+        }
+    }
+    __device__ __forceinline__ void resolve(const uint8_t *coded, uint8_t *dst, size_t pitch,
+                                            const uint64_t *in_bases, uint32_t c) {
+        const uint32_t w0 = __builtin_amdgcn_readfirstlane(v0), w1 = __builtin_amdgcn_readfirstlane(v1),
+                       w2 = __builtin_amdgcn_readfirstlane(v2);
+        ready = ((w2 >> 16) & 0xFFu) == K;  // RepairPlan::rank at byte 10
+        const uint32_t sel[K] = {w0 & 0xFFu, (w0 >> 8) & 0xFFu, (w0 >> 16) & 0xFFu, w0 >> 24,
+                                 w1 & 0xFFu, (w1 >> 8) & 0xFFu, (w1 >> 16) & 0xFFu, w1 >> 24,
+                                 w2 & 0xFFu, (w2 >> 8) & 0xFFu};
+#pragma unroll
+        for (int k = 0; k < (int)K; k++) ioff[k] = (uint32_t)((sel[k] & 15u) * pitch + K);
+        if (in_bases) {
+            ibase = reinterpret_cast<const uint8_t *>(uniform_u64(vin));
+            obase = reinterpret_cast<uint8_t *>(uniform_u64(vout));
+        } else {
+            ibase = coded + (size_t)c * N * pitch;
+            obase = dst + (size_t)c * CS;
+        }
+    }
+};
+
+// The decode as a persistent sweep (study variant, DECDS_DEC_SWEEP): resident workgroups take tiles
+// in global order from a tile counter, like the encode sweep, so a workgroup's next tile's coded
+// rows load while it combines the current one (the one-tile workgroups of rlnc_decode_kernel wait
+// for their loads up front: 42 % of their wave cycles are spent waiting, r05h PMC). A tile's rows
+// depend on its chunkset's plan, so the counter runs one tile further ahead than in the encode: the
+// next tile is known at the top of an iteration and its plan loads there, under the table build.
+template <int DW, int WAVES, int HB, uint32_t XR>
+__global__ __launch_bounds__(WG, WAVES) __attribute__((amdgpu_waves_per_eu(WAVES, WAVES)))
+void rlnc_decode_sweep_kernel(const uint8_t *__restrict__ coded, size_t pitch, size_t n,
+                              const RepairPlan *__restrict__ plan, uint8_t *__restrict__ dst,
+                              int32_t *__restrict__ status, const uint64_t *__restrict__ in_bases,
+                              const uint64_t *__restrict__ out_bases, uint32_t poly, uint32_t marker,
+                              uint32_t *__restrict__ counter) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    constexpr uint32_t T = TILES<DW>;
+    constexpr uint32_t phase = 0;
+    uint32_t ooff[K];
+#pragma unroll
+    for (int i = 0; i < (int)K; i++) ooff[i] = (uint32_t)(i * L);
+    // 1. edge columns of the ready chunksets b, b + gridDim, ... (tables in buffer 1)
+    for (uint32_t c = blockIdx.x; c < n; c += gridDim.x) {
+        DecodeDesc d;
+        d.load(plan, in_bases, out_bases, c);
+        d.resolve(coded, dst, pitch, in_bases, c);
+        if (!d.ready) continue;
+        const uint32_t cw = table_coeffs<K, K>(plan[c].inv, K);
+        lds_barrier();
+        build_tables<K, K>(lds + LDS_BYTES, cw, poly);
+        lds_barrier();
+        // piece 9's must decode to marker || zeros (chunkset.rs:202-204, as rlnc_decode_kernel)
+        bool ok = true;
+        for (uint32_t idx = threadIdx.x; idx < edge_cols<DW, false>(phase) * K; idx += WG) {
+            const uint32_t i = idx % K, col = edge_col<DW, false>(idx / K, phase);
+            uint32_t z = 0;
+#pragma unroll
+            for (uint32_t k = 0; k < K; k++) z ^= tbl_mul(lds + LDS_BYTES, k, i, d.ibase[d.ioff[k] + col]);
+            const uint64_t p = (uint64_t)i * L + col;
+            if (p < CS)
+                d.obase[p] = (uint8_t)z;
+            else
+                ok &= z == (p == CS ? marker : 0u);
+        }
+        if (__any(!ok) && (threadIdx.x & 63u) == 0) status[c] = 6;  // DECDS_ERR_CHUNKSET_REPAIRING_FAILED
+    }
+    // 2. the sweep. With XR > 1 (and a counter) tiles go out in runs of XR consecutive tiles per XCD —
+    // run r to XCD r mod 8, each XCD with its own counter — as rlnc_decode_kernel's DEC_XCD_RUN: piece
+    // i's stores start i bytes past a line boundary, so the line at a tile edge is written by both
+    // neighbours, and only every XR-th edge then crosses an L2. Workgroup b runs on XCD b mod 8.
+    const uint64_t total = (uint64_t)n * T;
+    const uint32_t G = gridDim.x;
+    const bool xcd = XR > 1 && counter && G % 8 == 0 && total % (8 * XR) == 0;
+    const uint32_t x8 = blockIdx.x & 7u, lim = xcd ? (uint32_t)(total / 8) : (uint32_t)total, step = xcd ? G / 8 : G;
+    uint32_t *ctr = counter ? counter + (xcd ? x8 : 0u) : nullptr;
+    auto tile_of = [&](uint32_t k) { return xcd ? ((k / XR) * 8 + x8) * XR + k % XR : k; };
+    uint32_t k = xcd ? blockIdx.x >> 3 : blockIdx.x;  // this workgroup's k-th tile of its sequence
+    if (k >= lim) return;
+    auto col_of = [&](uint32_t tt) { return tile_col<DW, false>(tt % T, T, phase); };
+    auto grab_next = [&]() -> uint32_t {  // inline asm for the reason given in rlnc_encode_sweep_kernel
+        uint32_t r = 0;
+        if (ctr && threadIdx.x == 0)
+            asm volatile("global_atomic_add %0, %1, %2, off sc0" : "=v"(r) : "v"(ctr), "v"(1u) : "memory");
+        return r;
+    };
+    uint32_t &s_next = *reinterpret_cast<uint32_t *>(lds + 2 * LDS_BYTES);
+    uint32_t t = tile_of(k), cs = t / T;
+    DecodeDesc cur, nxt;
+    cur.load(plan, in_bases, out_bases, cs);
+    uint32_t cw = table_coeffs_inv<K, K>(plan[cs].inv, K);
+    cur.resolve(coded, dst, pitch, in_bases, cs);
+    uint32_t colt = cur.ready ? col_of(t) : OOB_COL;
+    Vec<DW> x[K];
+    load_block<K, DW>(x, cur.ibase, cur.ioff, colt);
+    uint32_t grab = grab_next();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (threadIdx.x == 0) s_next = ctr ? step + grab : k + step;
+    lds_barrier();  // also: the edge pass's table readers are done
+    uint32_t kn = s_next;
+    uint32_t more;
+#pragma unroll 1
+    do {
+        more = kn < lim;
+        const uint32_t tn = tile_of(more ? kn : k), csn = tn / T;
+        nxt.load(plan, in_bases, out_bases, csn);
+        const uint32_t cwn = table_coeffs_inv<K, K>(plan[csn].inv, K);
+        build_tables<K, K, true>(lds, cw, poly);
+        lds_barrier();
+        grab = grab_next();  // -> the tile after the next
+        asm volatile("" ::: "memory");
+        nxt.resolve(coded, dst, pitch, in_bases, csn);
+        const uint32_t coln = more && nxt.ready ? col_of(tn) : OOB_COL;
+        combine_block<K, K, DW, 0, NoSink, 0, true, HB>(x, cur.obase, ooff, colt, nxt.ibase, nxt.ioff, coln);
+        // the counter's answer: everything but this tile's 2K prefetch loads and stores has landed
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * K) : "memory");
+        if (threadIdx.x == 0) s_next = ctr ? step + grab : kn + step;
+        lds_barrier();
+        k = kn;
+        kn = s_next;
+        cur = nxt;
+        cw = cwn;
+        colt = coln;
+    } while (more);
+    // the last workgroup out resets the counters (tile counter(s), then the exit count)
+    if (counter && threadIdx.x == 0) {
+        const uint32_t nc = xcd ? 8u : 1u;
+        if (atomicAdd(counter + nc, 1u) == G - 1) {
+            for (uint32_t c = 0; c <= nc; c++) __atomic_store_n(counter + c, 0u, __ATOMIC_RELAXED);
+        }
+    }
 }
 
 // One wave per chunkset. Replays rlnc's incremental rank test over the candidates' 10-byte coding
@@ -987,11 +1178,13 @@ constexpr bool MSG_OK = DECDS_ENC_DW == 4;
 #ifndef DECDS_ENC_QUEUE
 #define DECDS_ENC_QUEUE 1
 #endif
+#define DEC_SWEEP rlnc_decode_sweep_kernel<DECDS_DEC_DW, DECDS_DEC_SWEEP_WAVES, DECDS_DEC_HB, DECDS_DEC_SWEEP_XR>
 #define ENC_SWEEP(MSG) rlnc_encode_sweep_kernel<DECDS_ENC_DW, DECDS_ENC_WAVES, MSG, (DECDS_ENC_QUEUE != 0)>
 
 hipError_t configure_kernels() {
     const void *fns[] = {reinterpret_cast<const void *>(ENC_SWEEP(false)), reinterpret_cast<const void *>(ENC_SWEEP(MSG_OK)),
-                         reinterpret_cast<const void *>(ENC_HASH), reinterpret_cast<const void *>(rlnc_decode_kernel<DEC_UNIT>)};
+                         reinterpret_cast<const void *>(ENC_HASH), reinterpret_cast<const void *>(rlnc_decode_kernel<DEC_UNIT>),
+                         reinterpret_cast<const void *>(DEC_SWEEP)};
     for (const void *f : fns) {
         hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, std::max(SWEEP_LDS, FH_LDS<DECDS_FH_DW>));
         if (e != hipSuccess) return e;
@@ -1042,7 +1235,7 @@ hipError_t launch_encode(const LaunchGeom &geom, const uint8_t *src, size_t n, c
     return hipLaunchKernel(fn, dim3(grid), dim3(WG), args, SWEEP_LDS, stream);
 }
 
-const char *decode_kernel_name(size_t) { return "rlnc_decode_kernel"; }
+const char *decode_kernel_name(size_t) { return DECDS_DEC_SWEEP ? "rlnc_decode_sweep_kernel" : "rlnc_decode_kernel"; }
 
 const char *encode_kernel_name(size_t) { return "rlnc_encode_sweep_kernel"; }
 
@@ -1089,11 +1282,30 @@ hipError_t launch_repair_plan(const uint8_t *coded, size_t pitch, size_t n, cons
     return hipGetLastError();
 }
 
-hipError_t launch_decode(const LaunchGeom &, const uint8_t *coded, size_t pitch, size_t n, const uint8_t *plan,
+hipError_t launch_decode(const LaunchGeom &geom, const uint8_t *coded, size_t pitch, size_t n, const uint8_t *plan,
                          uint8_t *dst, int32_t *status, const uint64_t *in_bases, const uint64_t *out_bases,
                          uint32_t poly, uint32_t marker, hipStream_t stream) {
     if (n == 0) return hipSuccess;
     const RepairPlan *pl = reinterpret_cast<const RepairPlan *>(plan);
+    if constexpr (DECDS_DEC_SWEEP) {
+        static uint32_t resident = 0;
+        if (!resident) {
+            int per_cu = 0;
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void *>(DEC_SWEEP), WG,
+                                                             SWEEP_LDS) != hipSuccess || per_cu < 1)
+                per_cu = DECDS_DEC_SWEEP_WAVES;
+            resident = (uint32_t)per_cu * (uint32_t)(geom.num_cus > 0 ? geom.num_cus : 256);
+        }
+        const uint64_t tiles = (uint64_t)n * TILES<DECDS_DEC_DW>;
+        const uint32_t grid = (uint32_t)std::min<uint64_t>(tiles, resident);
+        uint32_t *counter = nullptr;
+        if (tiles > grid) {
+            if (!geom.counters) return hipErrorInvalidValue;
+            counter = geom.counters + (geom.counter_next.fetch_add(1) % LaunchGeom::N_COUNTERS) * LaunchGeom::COUNTER_STRIDE;
+        }
+        void *args[] = {&coded, &pitch, &n, &pl, &dst, &status, &in_bases, &out_bases, &poly, &marker, &counter};
+        return hipLaunchKernel(reinterpret_cast<const void *>(DEC_SWEEP), dim3(grid), dim3(WG), args, SWEEP_LDS, stream);
+    }
     constexpr uint32_t U = DEC_UNIT;
     (void)hipGetLastError();  // only this launch's status below
     hipLaunchKernelGGL(rlnc_decode_kernel<U>, dim3((uint32_t)(n * (TILES<DECDS_DEC_DW> / U))), dim3(WG), LDS_BYTES, stream, coded,

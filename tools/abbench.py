@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--warmup-s", type=float, default=3.0)
     ap.add_argument("--alloc-n", type=int, default=0, help="size the buffers for this many chunksets (>= n)")
     ap.add_argument("--at", type=int, default=0, help="run on chunksets [at, at + n) of the buffers")
+    ap.add_argument("--check", action="store_true", help="verify every build's repaired chunksets against the source")
     ap.add_argument("libs", nargs="+")
     a = ap.parse_args()
     import numpy as np
@@ -92,13 +93,26 @@ def main():
             run(b, ev)
             st.synchronize()
             b["t"].append([ev[0].elapsed_time(ev[1]), ev[1].elapsed_time(ev[2]), ev[2].elapsed_time(ev[3])])
+    if a.check:  # every ready chunkset must repair to its source bytes
+        for b in builds:
+            out.fill_(0xA5)
+            run(b)
+            st.synchronize()
+            ok = status[:n].cpu().numpy() == 0
+            same = (out[:n * CS].view(n, CS) == src[:n * CS].view(n, CS)).all(dim=1).cpu().numpy()
+            st_np = status[:n].cpu().numpy()
+            idle = (st_np != 0) & (st_np != 6)  # not ready: the decode must leave the output alone
+            kept = (out[:n * CS].view(n, CS) == 0xA5).all(dim=1).cpu().numpy()
+            b["check"] = {"ready": int(ok.sum()), "bad": int((ok & ~same).sum()), "not_ready": int(idle.sum()),
+                          "not_ready_written": int((idle & ~kept).sum())}
     for b in builds:
         t = np.array(b["t"])
         med, mn = np.median(t, axis=0), t.min(axis=0)
         print(json.dumps({"tag": b["tag"], "n": n, "alloc_n": na, "at": a.at, "pitch": b["pitch"], "encode_ms": round(med[0], 4),
                           "encode_min_ms": round(mn[0], 4), "plan_ms": round(med[1], 4), "decode_ms": round(med[2], 4),
                           "decode_min_ms": round(mn[2], 4), "encode_GBps": round(n * (CS + N * F) / med[0] / 1e6, 1),
-                          "decode_GBps": round(n * (K * F + CS) / med[2] / 1e6, 1)}), flush=True)
+                          "decode_GBps": round(n * (K * F + CS) / med[2] / 1e6, 1), **({"check": b["check"]} if "check" in b else {})}),
+              flush=True)
 
 
 if __name__ == "__main__":
