@@ -21,6 +21,7 @@
 // bands, per-half work shares, per-tile barriers, the warp-specialised kernel, timing hooks) are in
 // git history (tools/study/rlnc_kernels_r01_study.hip at a5d9101) with their measurements in DESIGN.md §8.
 #include <hip/hip_runtime.h>
+#include <cstdlib>
 
 #include <algorithm>
 #include <utility>
@@ -801,17 +802,12 @@ void rlnc_decode_kernel(const uint8_t *__restrict__ coded, size_t pitch, size_t 
     stream_range<K, K, DW, DECDS_PREFETCH_FIRST, false, DECDS_DEC_HB>(tile0, tile0 + UNIT, phase, ibase, ioff, obase, ooff, x);
 }
 
-#ifndef DECDS_DEC_SWEEP
-#define DECDS_DEC_SWEEP 0  // 1: the decode as a persistent tile sweep (rlnc_decode_sweep_kernel)
-#endif
-// 3 waves/SIMD: at 4 (128 VGPRs) the loop spills, the tile counter's pending return register among
-// what it spills (tests/test_isa.py checks the built code for exactly that)
+// 3 waves/SIMD for the decode sweep: at 4 (128 VGPRs) its loop spills, the tile counter's pending
+// return register among what it spills (tests/test_isa.py checks the built code for exactly that)
 #ifndef DECDS_DEC_SWEEP_WAVES
 #define DECDS_DEC_SWEEP_WAVES 3
 #endif
-#ifndef DECDS_DEC_SWEEP_XR
-#define DECDS_DEC_SWEEP_XR 8  // decode sweep: consecutive tiles per XCD (1 = one global counter)
-#endif
+
 // table_coeffs_all for a K x K inverse, in the decode sweep's loop: one buffer load base (the plan's
 // inverse, wave-uniform) and one lane offset, recomputed per call (a hoisted per-lane address set
 // spills at 4 waves/SIMD). Lane quad q needs rows 4q..4q+3; rows past NOUT-1 are zero. It loads rows
@@ -882,7 +878,7 @@ struct DecodeDesc {
 // for their loads up front: 42 % of their wave cycles are spent waiting, r05h PMC). A tile's rows
 // depend on its chunkset's plan, so the counter runs one tile further ahead than in the encode: the
 // next tile is known at the top of an iteration and its plan loads there, under the table build.
-template <int DW, int WAVES, int HB, uint32_t XR>
+template <int DW, int WAVES, int HB>
 __global__ __launch_bounds__(WG, WAVES) __attribute__((amdgpu_waves_per_eu(WAVES, WAVES)))
 void rlnc_decode_sweep_kernel(const uint8_t *__restrict__ coded, size_t pitch, size_t n,
                               const RepairPlan *__restrict__ plan, uint8_t *__restrict__ dst,
@@ -920,44 +916,37 @@ void rlnc_decode_sweep_kernel(const uint8_t *__restrict__ coded, size_t pitch, s
         }
         if (__any(!ok) && (threadIdx.x & 63u) == 0) status[c] = 6;  // DECDS_ERR_CHUNKSET_REPAIRING_FAILED
     }
-    // 2. the sweep. With XR > 1 (and a counter) tiles go out in runs of XR consecutive tiles per XCD —
-    // run r to XCD r mod 8, each XCD with its own counter — as rlnc_decode_kernel's DEC_XCD_RUN: piece
-    // i's stores start i bytes past a line boundary, so the line at a tile edge is written by both
-    // neighbours, and only every XR-th edge then crosses an L2. Workgroup b runs on XCD b mod 8.
-    const uint64_t total = (uint64_t)n * T;
-    const uint32_t G = gridDim.x;
-    const bool xcd = XR > 1 && counter && G % 8 == 0 && total % (8 * XR) == 0;
-    const uint32_t x8 = blockIdx.x & 7u, lim = xcd ? (uint32_t)(total / 8) : (uint32_t)total, step = xcd ? G / 8 : G;
-    uint32_t *ctr = counter ? counter + (xcd ? x8 : 0u) : nullptr;
-    auto tile_of = [&](uint32_t k) { return xcd ? ((k / XR) * 8 + x8) * XR + k % XR : k; };
-    uint32_t k = xcd ? blockIdx.x >> 3 : blockIdx.x;  // this workgroup's k-th tile of its sequence
-    if (k >= lim) return;
+    // 2. the sweep (tiles in runs per XCD, each XCD with its own counter — rlnc_decode_kernel's
+    // DEC_XCD_RUN — measured 1-2 % slower here at runs of 4, 8 and 16, r05q)
+    const uint32_t total = (uint32_t)((uint64_t)n * T), G = gridDim.x;
+    uint32_t k = blockIdx.x;  // this workgroup's tile
+    if (k >= total) return;
     auto col_of = [&](uint32_t tt) { return tile_col<DW, false>(tt % T, T, phase); };
     auto grab_next = [&]() -> uint32_t {  // inline asm for the reason given in rlnc_encode_sweep_kernel
         uint32_t r = 0;
-        if (ctr && threadIdx.x == 0)
-            asm volatile("global_atomic_add %0, %1, %2, off sc0" : "=v"(r) : "v"(ctr), "v"(1u) : "memory");
+        if (counter && threadIdx.x == 0)
+            asm volatile("global_atomic_add %0, %1, %2, off sc0" : "=v"(r) : "v"(counter), "v"(1u) : "memory");
         return r;
     };
     uint32_t &s_next = *reinterpret_cast<uint32_t *>(lds + 2 * LDS_BYTES);
-    uint32_t t = tile_of(k), cs = t / T;
+    uint32_t cs = k / T;
     DecodeDesc cur, nxt;
     cur.load(plan, in_bases, out_bases, cs);
     uint32_t cw = table_coeffs_inv<K, K>(plan[cs].inv, K);
     cur.resolve(coded, dst, pitch, in_bases, cs);
-    uint32_t colt = cur.ready ? col_of(t) : OOB_COL;
+    uint32_t colt = cur.ready ? col_of(k) : OOB_COL;
     Vec<DW> x[K];
     load_block<K, DW>(x, cur.ibase, cur.ioff, colt);
     uint32_t grab = grab_next();
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (threadIdx.x == 0) s_next = ctr ? step + grab : k + step;
+    if (threadIdx.x == 0) s_next = counter ? G + grab : k + G;
     lds_barrier();  // also: the edge pass's table readers are done
     uint32_t kn = s_next;
     uint32_t more;
 #pragma unroll 1
     do {
-        more = kn < lim;
-        const uint32_t tn = tile_of(more ? kn : k), csn = tn / T;
+        more = kn < total;
+        const uint32_t csn = more ? kn / T : cs;
         nxt.load(plan, in_bases, out_bases, csn);
         const uint32_t cwn = table_coeffs_inv<K, K>(plan[csn].inv, K);
         build_tables<K, K, true>(lds, cw, poly);
@@ -965,23 +954,23 @@ void rlnc_decode_sweep_kernel(const uint8_t *__restrict__ coded, size_t pitch, s
         grab = grab_next();  // -> the tile after the next
         asm volatile("" ::: "memory");
         nxt.resolve(coded, dst, pitch, in_bases, csn);
-        const uint32_t coln = more && nxt.ready ? col_of(tn) : OOB_COL;
+        const uint32_t coln = more && nxt.ready ? col_of(kn) : OOB_COL;
         combine_block<K, K, DW, 0, NoSink, 0, true, HB>(x, cur.obase, ooff, colt, nxt.ibase, nxt.ioff, coln);
         // the counter's answer: everything but this tile's 2K prefetch loads and stores has landed
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * K) : "memory");
-        if (threadIdx.x == 0) s_next = ctr ? step + grab : kn + step;
+        if (threadIdx.x == 0) s_next = counter ? G + grab : kn + G;
         lds_barrier();
         k = kn;
         kn = s_next;
+        cs = csn;
         cur = nxt;
         cw = cwn;
         colt = coln;
     } while (more);
-    // the last workgroup out resets the counters (tile counter(s), then the exit count)
-    if (counter && threadIdx.x == 0) {
-        const uint32_t nc = xcd ? 8u : 1u;
-        if (atomicAdd(counter + nc, 1u) == G - 1) {
-            for (uint32_t c = 0; c <= nc; c++) __atomic_store_n(counter + c, 0u, __ATOMIC_RELAXED);
+    if (counter && threadIdx.x == 0) {  // the last workgroup out resets the counter pair
+        if (atomicAdd(counter + 1, 1u) == G - 1) {
+            __atomic_store_n(counter, 0u, __ATOMIC_RELAXED);
+            __atomic_store_n(counter + 1, 0u, __ATOMIC_RELAXED);
         }
     }
 }
@@ -1178,7 +1167,7 @@ constexpr bool MSG_OK = DECDS_ENC_DW == 4;
 #ifndef DECDS_ENC_QUEUE
 #define DECDS_ENC_QUEUE 1
 #endif
-#define DEC_SWEEP rlnc_decode_sweep_kernel<DECDS_DEC_DW, DECDS_DEC_SWEEP_WAVES, DECDS_DEC_HB, DECDS_DEC_SWEEP_XR>
+#define DEC_SWEEP rlnc_decode_sweep_kernel<DECDS_DEC_DW, DECDS_DEC_SWEEP_WAVES, DECDS_DEC_HB>
 #define ENC_SWEEP(MSG) rlnc_encode_sweep_kernel<DECDS_ENC_DW, DECDS_ENC_WAVES, MSG, (DECDS_ENC_QUEUE != 0)>
 
 hipError_t configure_kernels() {
@@ -1235,7 +1224,19 @@ hipError_t launch_encode(const LaunchGeom &geom, const uint8_t *src, size_t n, c
     return hipLaunchKernel(fn, dim3(grid), dim3(WG), args, SWEEP_LDS, stream);
 }
 
-const char *decode_kernel_name(size_t) { return DECDS_DEC_SWEEP ? "rlnc_decode_sweep_kernel" : "rlnc_decode_kernel"; }
+// The decode's two forms: batches of DECDS_DEC_SWEEP_MIN_N chunksets or more run the
+// persistent sweep (-1.5...-3.3 % decode time at 256-1639 chunksets, r05p-r05s), smaller ones one-tile
+// workgroups (the sweep measured 1.5-2.6 % slower at 103, r05p/r05q). The environment variable of that
+// name overrides the threshold per launch (tests force either form at any size).
+#ifndef DECDS_DEC_SWEEP_MIN_N
+#define DECDS_DEC_SWEEP_MIN_N 256
+#endif
+static bool decode_sweeps(size_t n) {
+    const char *e = std::getenv("DECDS_DEC_SWEEP_MIN_N");
+    const unsigned long long min_n = e && *e ? std::strtoull(e, nullptr, 10) : DECDS_DEC_SWEEP_MIN_N;
+    return n >= min_n;
+}
+const char *decode_kernel_name(size_t n) { return decode_sweeps(n) ? "rlnc_decode_sweep_kernel" : "rlnc_decode_kernel"; }
 
 const char *encode_kernel_name(size_t) { return "rlnc_encode_sweep_kernel"; }
 
@@ -1287,7 +1288,7 @@ hipError_t launch_decode(const LaunchGeom &geom, const uint8_t *coded, size_t pi
                          uint32_t poly, uint32_t marker, hipStream_t stream) {
     if (n == 0) return hipSuccess;
     const RepairPlan *pl = reinterpret_cast<const RepairPlan *>(plan);
-    if constexpr (DECDS_DEC_SWEEP) {
+    if (decode_sweeps(n)) {
         static uint32_t resident = 0;
         if (!resident) {
             int per_cu = 0;
@@ -1297,6 +1298,7 @@ hipError_t launch_decode(const LaunchGeom &geom, const uint8_t *coded, size_t pi
             resident = (uint32_t)per_cu * (uint32_t)(geom.num_cus > 0 ? geom.num_cus : 256);
         }
         const uint64_t tiles = (uint64_t)n * TILES<DECDS_DEC_DW>;
+        if (tiles >= (1ull << 31)) return hipErrorInvalidValue;  // tile indices are 32-bit
         const uint32_t grid = (uint32_t)std::min<uint64_t>(tiles, resident);
         uint32_t *counter = nullptr;
         if (tiles > grid) {
@@ -1304,6 +1306,7 @@ hipError_t launch_decode(const LaunchGeom &geom, const uint8_t *coded, size_t pi
             counter = geom.counters + (geom.counter_next.fetch_add(1) % LaunchGeom::N_COUNTERS) * LaunchGeom::COUNTER_STRIDE;
         }
         void *args[] = {&coded, &pitch, &n, &pl, &dst, &status, &in_bases, &out_bases, &poly, &marker, &counter};
+        (void)hipGetLastError();  // only this launch's status below
         return hipLaunchKernel(reinterpret_cast<const void *>(DEC_SWEEP), dim3(grid), dim3(WG), args, SWEEP_LDS, stream);
     }
     constexpr uint32_t U = DEC_UNIT;

@@ -36,3 +36,12 @@ def _device_status_after_gpu_test(request):
     from decds_amd._capi import check, lib
     torch.cuda.synchronize()
     check(lib().decds_device_status(request.getfixturevalue("ctx").handle))
+
+
+@pytest.fixture(params=["tiles", "sweep"])
+def decode_form(request, monkeypatch):
+    """Run a decoding test through both decode kernels whatever its batch size: one-tile workgroups
+    (rlnc_decode_kernel) and the persistent sweep (rlnc_decode_sweep_kernel). launch_decode reads
+    DECDS_DEC_SWEEP_MIN_N at every launch (rlnc_kernels.hip decode_sweeps)."""
+    monkeypatch.setenv("DECDS_DEC_SWEEP_MIN_N", "1" if request.param == "sweep" else str(1 << 62))
+    return request.param

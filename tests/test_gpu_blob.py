@@ -101,6 +101,7 @@ def test_repairing_blob_add_chunk_like_reference(ctx):
     _raises("ChunksetAlreadyRepaired", ready.add_chunk, chunks[0])
 
 
+@pytest.mark.usefixtures("decode_form")
 def test_repairing_blob_get_repaired_chunkset_like_reference(ctx):
     # blob.rs:765-837: 2.5 chunksets, the partial last one truncated
     blob_len = 2 * CS + CS // 2
@@ -152,6 +153,7 @@ def test_repairing_blob_error_branches(ctx):
     _raises("ChunksetAlreadyRepaired", rep.add_chunk, c0)
 
 
+@pytest.mark.usefixtures("decode_form")
 def test_repairing_blob_all_chunks_shuffled_batch_vs_sequential(ctx):
     # tests.rs:4-57 through RepairingBlob: every chunk of every chunkset in one shuffled order, some
     # tampered; the batched add_chunks must return exactly the sequential add_chunk results, and
@@ -265,6 +267,7 @@ def _sequential(rep, arrivals):
     return st
 
 
+@pytest.mark.usefixtures("decode_form")
 def test_repairing_blob_sharded_and_spilled_match_one_context(ctx):
     # blob.rs:321-473 over two contexts (chunksets [0, 5) and [5, 9) of the one device stand in for
     # two GPUs) and under device budgets that spill accepted rows to page-locked host memory: statuses

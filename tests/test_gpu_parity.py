@@ -77,6 +77,7 @@ def test_encode_every_column_phase(ctx):
             assert np.array_equal(coded[c * N:(c + 1) * N], refs[c]), (off, c)
 
 
+@pytest.mark.usefixtures("decode_form")
 def test_encode_decode_at_the_largest_pitch(ctx):
     # a chunkset's 16 rows must fit one 2 GiB buffer descriptor (include/decds_rlnc.h): the largest
     # pitch is bit-exact through encode and repair (lanes past the last block use out-of-range
@@ -158,6 +159,7 @@ def _oracle_verdicts(coded, cand):
     return out, dec.rank()
 
 
+@pytest.mark.usefixtures("decode_form")
 def test_repair_batch_roundtrip_dependent_and_not_ready(ctx):
     n = 6
     data = o.fill_random(0xDEC05003, n * CS)
@@ -255,6 +257,7 @@ def test_repair_plan_fuzz_low_rank_and_repeats(ctx):
     assert len(ranks) >= 8  # the draws cover most ranks
 
 
+@pytest.mark.usefixtures("decode_form")
 def test_decode_tail_corruption_is_repairing_failed(ctx):
     data = o.fill_random(41, CS)
     coeffs = o.fill_random(42, N * K)
@@ -279,6 +282,7 @@ def test_decode_tail_corruption_is_repairing_failed(ctx):
     assert int(t[inv[9, k], 0x5A]) != 0
 
 
+@pytest.mark.usefixtures("decode_form")
 def test_chunkset_mirror_roundtrip_like_reference(ctx):
     # chunkset.rs:257-283 (fixed seeds instead of rand::rng())
     for it in range(3):
@@ -405,6 +409,7 @@ def test_cfg2_one_gib_encode_repair_device_resident(ctx):
 
 
 @pytest.mark.parametrize("pitch,off", [(F + 4093, 0), (F + 5, 0), (F + 5, 9)])
+@pytest.mark.usefixtures("decode_form")
 def test_repair_pitch_and_repeated_candidates(ctx, pitch, off):
     # decode from a padded coded layout (16-byte-aligned pitches: block loads at a column phase);
     # a candidate row repeated in the arrival order is not useful
@@ -436,6 +441,7 @@ def test_repair_pitch_and_repeated_candidates(ctx, pitch, off):
 
 
 @pytest.mark.parametrize("blob_len", [1, 4093, CS - 1, CS, CS + 1, 3 * CS + 12345])
+@pytest.mark.usefixtures("decode_form")
 def test_blob_all_chunks_shuffled_roundtrip(ctx, blob_len):
     """tests.rs:4-57: build a blob, shuffle ALL 16*n chunks of all chunksets together, feed them to
     the repairing blob in that order (each chunkset sees its own chunks in their global order), and
@@ -457,6 +463,7 @@ def test_blob_all_chunks_shuffled_roundtrip(ctx, blob_len):
     assert (status == 0).all() and np.array_equal(out, blob)
 
 
+@pytest.mark.usefixtures("decode_form")
 def test_blob_host_not_ready_chunkset(ctx):
     blob_len = CS + 777
     blob = o.fill_random(0xB10C, blob_len)
@@ -500,6 +507,7 @@ def test_encode_batch_above_512_bitexact(ctx):
 
 
 @pytest.mark.parametrize("trial", range(6))
+@pytest.mark.usefixtures("decode_form")
 def test_randomized_layouts_encode_repair(ctx, trial):
     # seeded random batch shapes through both kernels: batch sizes that pick every unit size
     # (encode 4 / decode 2 / 4 / 8 tiles), rlnc-pitch and 16-byte-aligned pitches at any base offset
@@ -535,6 +543,7 @@ def test_randomized_layouts_encode_repair(ctx, trial):
 
 
 @pytest.mark.parametrize("n", [3, 20])
+@pytest.mark.usefixtures("decode_form")
 def test_aligned_device_layout_roundtrip(ctx, n):
     # the recommended device layout (include/decds_rlnc.h): pitch 1,048,704, payloads 128-byte aligned;
     # n = 3 runs the small-batch encode (units of 1 tile), n = 20 the units of 4 with XCD eighths

@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--alloc-n", type=int, default=0, help="size the buffers for this many chunksets (>= n)")
     ap.add_argument("--at", type=int, default=0, help="run on chunksets [at, at + n) of the buffers")
     ap.add_argument("--check", action="store_true", help="verify every build's repaired chunksets against the source")
+    ap.add_argument("--check-reps", type=int, default=1, help="repeat the output check this many times")
     ap.add_argument("libs", nargs="+")
     a = ap.parse_args()
     import numpy as np
@@ -65,12 +66,12 @@ def main():
     torch.cuda.synchronize()
     sp = vp(st.cuda_stream)
 
-    def run(b, ev=None):
+    def run(b, ev=None, encode=True):
         L, h, p = b["lib"], b["ctx"], b["pitch"]
         coded = coded0[b["off"]:]
         if ev:
             ev[0].record(st)
-        assert L.decds_encode_batch(h, vp(src.data_ptr()), n, vp(coeffs.data_ptr()), vp(coded.data_ptr()), p, sp) == 0
+        assert not encode or L.decds_encode_batch(h, vp(src.data_ptr()), n, vp(coeffs.data_ptr()), vp(coded.data_ptr()), p, sp) == 0
         if ev:
             ev[1].record(st)
         assert L.decds_repair_plan_batch(h, vp(coded.data_ptr()), p, n, vp(cand.data_ptr()), vp(plan.data_ptr()),
@@ -94,8 +95,9 @@ def main():
             st.synchronize()
             b["t"].append([ev[0].elapsed_time(ev[1]), ev[1].elapsed_time(ev[2]), ev[2].elapsed_time(ev[3])])
     if a.check:  # every ready chunkset must repair to its source bytes
-        for b in builds:
+        for b, _ in [(b, r) for r in range(a.check_reps) for b in builds]:
             out.fill_(0xA5)
+            torch.cuda.synchronize()  # the fill runs on torch's stream, the codec on st
             run(b)
             st.synchronize()
             ok = status[:n].cpu().numpy() == 0
@@ -103,8 +105,27 @@ def main():
             st_np = status[:n].cpu().numpy()
             idle = (st_np != 0) & (st_np != 6)  # not ready: the decode must leave the output alone
             kept = (out[:n * CS].view(n, CS) == 0xA5).all(dim=1).cpu().numpy()
+            prev = b.get("check")
             b["check"] = {"ready": int(ok.sum()), "bad": int((ok & ~same).sum()), "not_ready": int(idle.sum()),
                           "not_ready_written": int((idle & ~kept).sum())}
+            where = []  # first bad chunksets: (chunkset, mismatching bytes, first/last piece:column)
+            for c in np.nonzero(ok & ~same)[0][:8]:
+                d = np.nonzero((out[c * CS:(c + 1) * CS] != src[c * CS:(c + 1) * CS]).cpu().numpy())[0]
+                Lp = (CS + K - 1) // K + 1  # piece length L
+                where.append([int(c), int(d.size), "%d:%d" % divmod(int(d[0]), Lp), "%d:%d" % divmod(int(d[-1]), Lp)])
+            if where:
+                b["check"]["where"] = where
+                # the same coded rows planned and decoded again: a decode race comes out different
+                out.fill_(0xA5)
+                torch.cuda.synchronize()
+                run(b, encode=False)
+                st.synchronize()
+                again = (out[:n * CS].view(n, CS) == src[:n * CS].view(n, CS)).all(dim=1).cpu().numpy()
+                b["check"]["bad_redecode"] = int((ok & ~again).sum())
+            if prev:  # repeated checks: bad counts per repetition, first failure kept
+                b["check"]["bad_reps"] = prev.get("bad_reps", [prev["bad"]]) + [b["check"]["bad"]]
+                if "where" in prev:
+                    b["check"]["where"] = prev["where"]
     for b in builds:
         t = np.array(b["t"])
         med, mn = np.median(t, axis=0), t.min(axis=0)
