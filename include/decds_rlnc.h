@@ -123,8 +123,9 @@ int decds_decode_batch(decds_ctx *ctx, const uint8_t *coded, size_t coded_pitch,
                        size_t n_chunksets, const uint8_t *plan, uint8_t *dst, int32_t *status,
                        void *stream);
 
-/* name of the gfx950 kernel decds_decode_batch launches for n chunksets (for profiles and traces:
- * rlnc_decode_kernel) */
+/* name of the gfx950 kernel decds_decode_batch launches for n chunksets (for profiles and traces):
+ * rlnc_decode_sweep_kernel from DECDS_DEC_SWEEP_MIN_N chunksets on (environment variable, read per
+ * launch; default 256), rlnc_decode_kernel below */
 const char *decds_decode_kernel_name(size_t n_chunksets);
 
 /* plan + decode in one call (the RepairingBlob::add_chunk loop + get_repaired_chunkset,
