@@ -538,10 +538,13 @@ struct RbShard {
             std::memset(&plans[i], 0, sizeof(RepairPlan));
             for (uint32_t k = 0; k < K; k++) plans[i].sel[k] = (uint8_t)k;
             plans[i].rank = K;
-            if (!host_gf_invert(&c.cv[0][0], plans[i].inv, ctx->poly)) {
+            uint8_t inv[K * K];
+            if (!host_gf_invert(&c.cv[0][0], inv, ctx->poly)) {
                 st = decds_set_error(DECDS_ERR_CHUNKSET_REPAIRING_FAILED, "accepted coding vectors are singular");
                 break;
             }
+            for (uint32_t r = 0; r < K; r++)  // RepairPlan::inv is input-major
+                for (uint32_t k = 0; k < K; k++) plans[i].inv[k * K + r] = inv[r * K + k];
             if (c.slot >= 0) {
                 inb[i] = reinterpret_cast<uint64_t>(slot_rows(c.slot));
             } else {  // spilled: stage its rows into the area (page-locked host memory: direct DMA)

@@ -86,7 +86,7 @@ __device__ __forceinline__ void lds_barrier() {
 // The 4 coefficient bytes thread p = 8i + 4h + q (< NIN*8) of build_tables combines:
 // M[(4q + jj) * ldm + i], jj < 4 (zero for outputs >= NOUT and for idle threads).
 template <int NIN, int NOUT>
-__device__ __forceinline__ uint32_t table_coeffs(const uint8_t *M, uint32_t ldm) {
+__device__ __forceinline__ uint32_t table_coeffs(const uint8_t *M, uint32_t ldm, uint32_t ldi = 1) {
     static_assert(NIN * 8 <= (int)WG, "one coefficient word per thread");
     const uint32_t p = threadIdx.x;
     uint32_t w = 0;
@@ -94,7 +94,7 @@ __device__ __forceinline__ uint32_t table_coeffs(const uint8_t *M, uint32_t ldm)
         const uint32_t q = p & 3u, i = p >> 3;
 #pragma unroll
         for (uint32_t jj = 0; jj < 4; jj++)
-            if (4 * q + jj < (uint32_t)NOUT) w |= (uint32_t)M[(4 * q + jj) * ldm + i] << (8 * jj);
+            if (4 * q + jj < (uint32_t)NOUT) w |= (uint32_t)M[(4 * q + jj) * ldm + i * ldi] << (8 * jj);
     }
     return w;
 }
@@ -109,6 +109,27 @@ __device__ __forceinline__ uint32_t table_coeffs_all(const uint8_t *M, uint32_t 
     uint32_t w = 0;
 #pragma unroll
     for (uint32_t jj = 0; jj < 4; jj++) w |= (uint32_t)M[(4 * q + jj) * ldm + i] << (8 * jj);
+    return live ? w : 0u;
+}
+
+// table_coeffs_all for the decode sweep's loop, from the plan's input-major inverse (input i's
+// coefficients for outputs 0..9 are the 10 bytes at i * K): lane quad q's word is those of outputs
+// 4q..4q+3 — one dword load, not four byte loads (fewer registers pending across the lookups). It
+// loads outputs r0..r0+3 with r0 = min(4q, NOUT-4), never past input i's row, and shifts the word
+// down by the outputs it read before 4q (outputs past NOUT-1 are zero). One buffer base (wave-
+// uniform) and one lane offset, recomputed per call (not hoisted into a register).
+template <int NIN, int NOUT>
+__device__ __forceinline__ uint32_t table_coeffs_imaj(const uint8_t *M) {
+    static_assert(NOUT >= 4 && NOUT <= 16, "quads of outputs");
+    uint32_t p = threadIdx.x;
+    asm volatile("" : "+v"(p));
+    const bool live = p < NIN * 8;
+    p = live ? p : 0u;
+    const uint32_t q = p & 3u, i = p >> 3;
+    const uint32_t r0 = 4 * q < (uint32_t)NOUT - 4 ? 4 * q : (uint32_t)NOUT - 4, sh = 8 * (4 * q - r0);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(M), 0, NIN * NOUT, 0x00020000);
+    uint32_t w = __builtin_amdgcn_raw_buffer_load_b32(rs, i * NOUT + r0, 0, 0);
+    w = sh < 32 ? w >> sh : 0u;
     return live ? w : 0u;
 }
 
@@ -758,7 +779,7 @@ void rlnc_decode_kernel(const uint8_t *__restrict__ coded, size_t pitch, size_t 
     const uint32_t w1 = __builtin_amdgcn_readfirstlane(pw[1]);
     const uint32_t w2 = __builtin_amdgcn_readfirstlane(pw[2]);
     if (((w2 >> 16) & 0xFFu) != K) return;  // RepairPlan::rank at byte 10: not ready
-    const uint32_t cw = table_coeffs<K, K>(plan[cs].inv, K);
+    const uint32_t cw = table_coeffs<K, K>(plan[cs].inv, 1, K);  // input-major inverse
     const uint32_t sel[K] = {w0 & 0xFFu, (w0 >> 8) & 0xFFu, (w0 >> 16) & 0xFFu, w0 >> 24,
                              w1 & 0xFFu, (w1 >> 8) & 0xFFu, (w1 >> 16) & 0xFFu, w1 >> 24,
                              w2 & 0xFFu, (w2 >> 8) & 0xFFu};
@@ -807,29 +828,6 @@ void rlnc_decode_kernel(const uint8_t *__restrict__ coded, size_t pitch, size_t 
 #ifndef DECDS_DEC_SWEEP_WAVES
 #define DECDS_DEC_SWEEP_WAVES 3
 #endif
-
-// table_coeffs_all for a K x K inverse, in the decode sweep's loop: one buffer load base (the plan's
-// inverse, wave-uniform) and one lane offset, recomputed per call (a hoisted per-lane address set
-// spills at 4 waves/SIMD). Lane quad q needs rows 4q..4q+3; rows past NOUT-1 are zero. It loads rows
-// r0..r0+3 with r0 = min(4q, NOUT-4) — never past the inverse — and shifts the word down by the
-// rows it read before 4q.
-template <int NIN, int NOUT>
-__device__ __forceinline__ uint32_t table_coeffs_inv(const uint8_t *M, uint32_t ldm) {
-    static_assert(NOUT >= 4 && NOUT <= 16, "quads of outputs");
-    uint32_t p = threadIdx.x;
-    asm volatile("" : "+v"(p));
-    const bool live = p < NIN * 8;
-    p = live ? p : 0u;
-    const uint32_t q = p & 3u, i = p >> 3;
-    const uint32_t r0 = 4 * q < (uint32_t)NOUT - 4 ? 4 * q : (uint32_t)NOUT - 4, sh = 8 * (4 * q - r0);
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(M), 0, NOUT * ldm, 0x00020000);
-    const uint32_t o = r0 * ldm + i;
-    uint32_t w = 0;
-#pragma unroll
-    for (uint32_t jj = 0; jj < 4; jj++) w |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rs, o + jj * ldm, 0, 0) << (8 * jj);
-    w = sh < 32 ? w >> sh : 0u;
-    return live ? w : 0u;
-}
 
 // A chunkset's decode operands: coded-row offsets of the accepted chunks, input/output bases and
 // whether it is ready. The raw loads are issued first (load) and turned into wave-uniform values
@@ -897,7 +895,7 @@ void rlnc_decode_sweep_kernel(const uint8_t *__restrict__ coded, size_t pitch, s
         d.load(plan, in_bases, out_bases, c);
         d.resolve(coded, dst, pitch, in_bases, c);
         if (!d.ready) continue;
-        const uint32_t cw = table_coeffs<K, K>(plan[c].inv, K);
+        const uint32_t cw = table_coeffs<K, K>(plan[c].inv, 1, K);  // input-major inverse
         lds_barrier();
         build_tables<K, K>(lds + LDS_BYTES, cw, poly);
         lds_barrier();
@@ -932,7 +930,7 @@ void rlnc_decode_sweep_kernel(const uint8_t *__restrict__ coded, size_t pitch, s
     uint32_t cs = k / T;
     DecodeDesc cur, nxt;
     cur.load(plan, in_bases, out_bases, cs);
-    uint32_t cw = table_coeffs_inv<K, K>(plan[cs].inv, K);
+    uint32_t cw = table_coeffs_imaj<K, K>(plan[cs].inv);
     cur.resolve(coded, dst, pitch, in_bases, cs);
     uint32_t colt = cur.ready ? col_of(k) : OOB_COL;
     Vec<DW> x[K];
@@ -948,7 +946,7 @@ void rlnc_decode_sweep_kernel(const uint8_t *__restrict__ coded, size_t pitch, s
         more = kn < total;
         const uint32_t csn = more ? kn / T : cs;
         nxt.load(plan, in_bases, out_bases, csn);
-        const uint32_t cwn = table_coeffs_inv<K, K>(plan[csn].inv, K);
+        const uint32_t cwn = table_coeffs_imaj<K, K>(plan[csn].inv);
         build_tables<K, K, true>(lds, cw, poly);
         lds_barrier();
         grab = grab_next();  // -> the tile after the next
@@ -1100,10 +1098,12 @@ __global__ __launch_bounds__(64) void rlnc_plan_kernel(const uint8_t *__restrict
         if (lane == 0) status[cs] = 5;  // DECDS_ERR_CHUNKSET_NOT_YET_READY
         return;
     }
-    // inverse row piv[e] = combination part of basis row e: lane 10 + k writes inv[piv[e]][k]
+    // inverse row piv[e] = combination part of basis row e: lane 10 + k writes inverse entry
+    // (piv[e], k), stored input-major at k * K + piv[e] (so a table build reads 4 outputs' coefficients
+    // of one input as one dword, table_coeffs_imaj)
     if (lane >= K && lane < 2 * K) {
 #pragma unroll
-        for (int e = 0; e < (int)K; e++) pl->inv[piv[e] * K + (lane - K)] = (uint8_t)basis[e];
+        for (int e = 0; e < (int)K; e++) pl->inv[(lane - K) * K + piv[e]] = (uint8_t)basis[e];
     }
     if (lane == 0) {
 #pragma unroll

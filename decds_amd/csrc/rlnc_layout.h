@@ -32,7 +32,7 @@ struct alignas(16) RepairPlan {
     uint8_t sel[K];      // coded-row index (0..15) of the k-th accepted chunk, acceptance order
     uint8_t rank;        // decoder rank after all candidates (== K -> ready to repair)
     uint8_t pad0[5];
-    uint8_t inv[K * K];  // inverse of the accepted coding vectors: piece_i = sum_k inv[i][k] * y_k
+    uint8_t inv[K * K];  // inverse of the accepted coding vectors, input-major: piece_i = sum_k inv[k * K + i] * y_k
     uint8_t pad1[12];
 };
 static_assert(sizeof(RepairPlan) == 128, "plan is 128 B");

@@ -246,7 +246,7 @@ def test_repair_plan_fuzz_low_rank_and_repeats(ctx):
         assert st[c] == 0, c
         acc = [int(cand[c, a]) for a in range(N) if ov[a] == OKV]
         assert list(pl[c, :K]) == acc, c
-        inv = pl[c, 16:16 + K * K].reshape(K, K)
+        inv = pl[c, 16:16 + K * K].reshape(K, K).T  # stored input-major (rlnc_layout.h RepairPlan)
         m = vecs[c, acc]
         for i in range(K):
             for j in range(K):
