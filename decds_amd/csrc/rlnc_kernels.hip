@@ -825,6 +825,11 @@ void rlnc_decode_kernel(const uint8_t *__restrict__ coded, size_t pitch, size_t 
 
 // 3 waves/SIMD for the decode sweep: at 4 (128 VGPRs) its loop spills, the tile counter's pending
 // return register among what it spills (tests/test_isa.py checks the built code for exactly that)
+#ifndef DECDS_DEC_REMAT
+// the decode sweep recomputes its table-build addresses per tile: 149 against 165 VGPRs, time ±0.1 %
+// (r05v); the same in the encode sweep cost 5.6 % (r05u, not used there)
+#define DECDS_DEC_REMAT 1
+#endif
 #ifndef DECDS_DEC_SWEEP_WAVES
 #define DECDS_DEC_SWEEP_WAVES 3
 #endif
@@ -947,7 +952,7 @@ void rlnc_decode_sweep_kernel(const uint8_t *__restrict__ coded, size_t pitch, s
         const uint32_t csn = more ? kn / T : cs;
         nxt.load(plan, in_bases, out_bases, csn);
         const uint32_t cwn = table_coeffs_imaj<K, K>(plan[csn].inv);
-        build_tables<K, K, true>(lds, cw, poly);
+        build_tables<K, K, DECDS_DEC_REMAT>(lds, cw, poly);
         lds_barrier();
         grab = grab_next();  // -> the tile after the next
         asm volatile("" ::: "memory");
