@@ -90,3 +90,17 @@ def test_layout_constants():
     assert _capi.PIECE_BYTES == o.L == 1048577
     assert _capi.CODED_PIECE_BYTES == o.F
     assert _capi.CHUNKSET_BYTES == o.CS
+
+
+def test_decode_kernel_by_batch_size(monkeypatch):
+    # launch_decode (rlnc_kernels.hip decode_sweeps): the persistent sweep from 256 chunksets on,
+    # one-tile workgroups below; DECDS_DEC_SWEEP_MIN_N moves the threshold per launch
+    lib = _capi.lib()
+    monkeypatch.delenv("DECDS_DEC_SWEEP_MIN_N", raising=False)
+    name = lambda n: lib.decds_decode_kernel_name(n).decode()  # noqa: E731
+    assert name(1) == name(255) == "rlnc_decode_kernel"
+    assert name(256) == name(1639) == "rlnc_decode_sweep_kernel"
+    monkeypatch.setenv("DECDS_DEC_SWEEP_MIN_N", "1")
+    assert name(1) == "rlnc_decode_sweep_kernel"
+    monkeypatch.setenv("DECDS_DEC_SWEEP_MIN_N", str(1 << 40))
+    assert name(1639) == "rlnc_decode_kernel"
