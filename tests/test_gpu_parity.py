@@ -202,6 +202,27 @@ def test_repair_batch_roundtrip_dependent_and_not_ready(ctx):
     assert NOT_USEFUL in list(v[1]) and NOT_USEFUL in list(v[2])
 
 
+@pytest.mark.usefixtures("decode_form")
+def test_repair_batch_nothing_ready_leaves_every_output(ctx):
+    # every chunkset one chunk short (chunkset.rs:206: not yet ready): the decode's tiles all run with
+    # out-of-range columns (the sweep's whole grid, incl. its tile counter) and write nothing
+    n = 5
+    data = o.fill_random(0xDEC05009, n * CS)
+    coeffs = o.fill_random(0xC0EF0009, n * N * K)
+    coded_d = torch.empty(n * N * F, dtype=torch.uint8, device="cuda")
+    codec.encode_batch(ctx, dev(data), n, dev(coeffs), coded_d)
+    cand = np.full((n, N), 0xFF, np.uint8)
+    rng = np.random.default_rng(9)
+    for c in range(n):
+        cand[c, :K - 1] = rng.permutation(N)[:K - 1]
+    plan = torch.empty(n * 128, dtype=torch.uint8, device="cuda")
+    verd = torch.empty(n * N, dtype=torch.int8, device="cuda")
+    status = torch.full((n,), -7, dtype=torch.int32, device="cuda")
+    out = torch.full((n * CS,), 0x5A, dtype=torch.uint8, device="cuda")
+    codec.repair_batch(ctx, coded_d, n, dev(cand), plan, verd, out, status)
+    assert list(host(status)) == [5] * n
+    assert (host(out) == 0x5A).all()
+
 def test_repair_plan_fuzz_low_rank_and_repeats(ctx):
     """The plan kernel alone (chunkset.rs:173-184 replayed per candidate) on 96 chunksets of
     rank-deficient coding vectors: rows drawn from random subspaces of rank 1..10, zero and repeated
