@@ -272,20 +272,50 @@ __device__ __forceinline__ void xor3_into(uint32_t (&acc)[4], const u32x4 &a, co
 // turns both into one SDWA op each (v_and_b32_sdwa / v_lshlrev_b32_sdwa with a byte select).
 // HB = bytes of the input dword per group (4: 8 reads per group, 16 in flight; 2: 4 reads per group,
 // 8 in flight and half the result registers — for kernels that need the VGPRs for occupancy).
-template <int G, int DW, uint32_t TB, int HB = 4>
-__device__ __forceinline__ void lds_issue(u32x4 (&r)[2 * HB], uint32_t xw) {
+// The row addresses of byte P of an input dword: lo nibble * 16, hi nibble * 16. SDWA: one op per
+// address by inline asm, byte P picked by the SDWA source select (hipcc emits a shift + and pair for
+// most of them): 8 % fewer VALU instructions, −1.4…−1.9 % fused ChunkSet::new time (issue-bound),
+// +0.3…+0.9 % encode / decode time (not issue-bound; r05za) — so the fused kernel only.
+template <int P, bool SDWA>
+__device__ __forceinline__ void nibble_addr(uint32_t xw, uint32_t lo4, uint32_t &alo, uint32_t &ahi) {
+    if constexpr (SDWA) {
+        // one op per address, byte P picked by the SDWA source select: (lo4.byte P) << 4 and
+        // (xw.byte P) & 0xF0 (byte 0's high nibble a plain full-rate v_and)
+        asm("v_lshlrev_b32_sdwa %0, 4, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_%c2"
+            : "=v"(alo)
+            : "v"(lo4), "i"(P));
+        if constexpr (P == 0)
+            ahi = xw & 0xF0u;
+        else
+            asm("v_and_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_%c3 src1_sel:DWORD"
+                : "=v"(ahi)
+                : "v"(xw), "v"(0xF0u), "i"(P));
+    } else {
+        alo = ((lo4 >> (8 * P)) & 0xFFu) << 4;
+        ahi = (xw >> (8 * P)) & 0xF0u;
+    }
+}
+
+template <int G, int DW, uint32_t TB, int HB, bool SDWA, int Q>
+__device__ __forceinline__ void lds_issue_q(u32x4 (&r)[2 * HB], uint32_t xw, uint32_t lo4) {
     constexpr int PARTS = 4 / HB, g2 = G / PARTS, part = G % PARTS;
     constexpr int i = g2 / DW;
     constexpr uint32_t tlo = TB + (2 * i) * TABLE_BYTES, thi = TB + (2 * i + 1) * TABLE_BYTES;
+    uint32_t alo, ahi;
+    nibble_addr<part * HB + Q, SDWA>(xw, lo4, alo, ahi);
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r[2 * Q]) : "v"(alo), "i"(tlo));
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r[2 * Q + 1]) : "v"(ahi), "i"(thi));
+}
+
+template <int G, int DW, uint32_t TB, int HB, bool SDWA, int... Qs>
+__device__ __forceinline__ void lds_issue_qs(std::integer_sequence<int, Qs...>, u32x4 (&r)[2 * HB], uint32_t xw) {
     const uint32_t lo4 = xw & 0x0F0F0F0Fu;
-#pragma unroll
-    for (int q = 0; q < HB; q++) {
-        const int p = part * HB + q;
-        const uint32_t alo = ((lo4 >> (8 * p)) & 0xFFu) << 4;
-        const uint32_t ahi = (xw >> (8 * p)) & 0xF0u;
-        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r[2 * q]) : "v"(alo), "i"(tlo));
-        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r[2 * q + 1]) : "v"(ahi), "i"(thi));
-    }
+    (lds_issue_q<G, DW, TB, HB, SDWA, Qs>(r, xw, lo4), ...);
+}
+
+template <int G, int DW, uint32_t TB, int HB = 4, bool SDWA = false>
+__device__ __forceinline__ void lds_issue(u32x4 (&r)[2 * HB], uint32_t xw) {
+    lds_issue_qs<G, DW, TB, HB, SDWA>(std::make_integer_sequence<int, HB>{}, r, xw);
 }
 
 template <int CNT>
@@ -307,7 +337,7 @@ __device__ __forceinline__ void lds_wait(u32x4 (&r)[4]) {
 // Group G of the lookups; input i's register takes the next block's bytes (ncol0) as soon as that
 // input's lookups are all issued — before this block's stores: gfx9's vmcnt counts stores too, so
 // a load issued behind the stores would also wait for them.
-template <int NIN, int DW, uint32_t TB, int G, int HB = 4>
+template <int NIN, int DW, uint32_t TB, int G, int HB = 4, bool SDWA = false>
 __device__ __forceinline__ void lds_step(uint32_t (&acc)[4 * DW][4], u32x4 (&ra)[2 * HB], u32x4 (&rb)[2 * HB],
                                          Vec<DW> (&x)[NIN], const uint8_t *ibase, const uint32_t (&ioff)[NIN],
                                          uint32_t ncol0) {
@@ -316,7 +346,7 @@ __device__ __forceinline__ void lds_step(uint32_t (&acc)[4 * DW][4], u32x4 (&ra)
     u32x4(&nxt)[2 * HB] = (G & 1) ? ra : rb;
     if constexpr (G + 1 < NG) {
         constexpr int H = G + 1, hi = H / NGI, hw = (H / PARTS) % DW;
-        lds_issue<H, DW, TB, HB>(nxt, x[hi][hw]);
+        lds_issue<H, DW, TB, HB, SDWA>(nxt, x[hi][hw]);
         if constexpr ((H % NGI) == NGI - 1) x[hi] = ldrow<DW>(ibase, ioff[hi], ncol0);
         lds_wait<2 * HB>(cur);
     } else {
@@ -327,13 +357,13 @@ __device__ __forceinline__ void lds_step(uint32_t (&acc)[4 * DW][4], u32x4 (&ra)
     for (int q = 0; q < HB; q++) xor3_into(acc[4 * w + part * HB + q], cur[2 * q], cur[2 * q + 1]);
 }
 
-template <int NIN, int DW, uint32_t TB, int HB, int... Gs>
+template <int NIN, int DW, uint32_t TB, int HB, bool SDWA, int... Gs>
 __device__ __forceinline__ void lookups(std::integer_sequence<int, Gs...>, uint32_t (&acc)[4 * DW][4],
                                         Vec<DW> (&x)[NIN], const uint8_t *ibase, const uint32_t (&ioff)[NIN],
                                         uint32_t ncol0) {
     u32x4 ra[2 * HB], rb[2 * HB];
-    lds_issue<0, DW, TB, HB>(ra, x[0][0]);
-    (lds_step<NIN, DW, TB, Gs, HB>(acc, ra, rb, x, ibase, ioff, ncol0), ...);
+    lds_issue<0, DW, TB, HB, SDWA>(ra, x[0][0]);
+    (lds_step<NIN, DW, TB, Gs, HB, SDWA>(acc, ra, rb, x, ibase, ioff, ncol0), ...);
 }
 
 // One lane block of 4*DW columns: out_j[col0 ..) = sum_i M[j][i] * in_i[col0 ..), tables at LDS
@@ -345,7 +375,7 @@ struct NoSink {
     __device__ void operator()(int, const V &) const {}
 };
 template <int NIN, int NOUT, int DW, uint32_t TB = 0, typename Sink = NoSink, int SAUX = 0, bool GSTORE = true,
-          int HB = 4>
+          int HB = 4, bool SDWA = false>
 __device__ __forceinline__ void combine_block(Vec<DW> (&x)[NIN], uint8_t *obase, const uint32_t (&ooff)[NOUT],
                                               uint32_t col0, const uint8_t *ibase, const uint32_t (&ioff)[NIN],
                                               uint32_t ncol0, Sink sink = Sink{}) {
@@ -354,7 +384,7 @@ __device__ __forceinline__ void combine_block(Vec<DW> (&x)[NIN], uint8_t *obase,
     for (int c = 0; c < 4 * DW; c++)
 #pragma unroll
         for (int q = 0; q < 4; q++) acc[c][q] = 0;
-    lookups<NIN, DW, TB, HB>(std::make_integer_sequence<int, DW * NIN * (4 / HB)>{}, acc, x, ibase, ioff, ncol0);
+    lookups<NIN, DW, TB, HB, SDWA>(std::make_integer_sequence<int, DW * NIN * (4 / HB)>{}, acc, x, ibase, ioff, ncol0);
     // columns x outputs -> outputs x columns
 #pragma unroll
     for (int q = 0; q < 4; q++) {
@@ -584,7 +614,7 @@ void rlnc_encode_hash_kernel(const uint8_t *__restrict__ src, size_t n, const ui
     uint32_t st = 0;
 #pragma unroll 1
     do {
-        combine_block<K, N, DW, 0, decltype(sink), FH_STORE_AUX, true, FH_HB>(x, obase, ooff, col(st), ibase, ioff,
+        combine_block<K, N, DW, 0, decltype(sink), FH_STORE_AUX, true, FH_HB, true>(x, obase, ooff, col(st), ibase, ioff,
                                                                              col(st + 1), sink);
         // one wave: its LDS accesses complete in order, no barrier between the slot writes and reads
 #pragma unroll
