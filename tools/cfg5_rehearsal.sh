@@ -6,5 +6,5 @@
 out=${1:-gpurun_out/cfg5_rehearsal.jsonl}; steps=${2:-10}
 mkdir -p "$(dirname "$out")"
 for r in 0 1 2 3 4 5 6 7; do
-  timeout -k 10 300 python bench.py --config cfg3 --rehearse-shard $r/8 --steps $steps --warmup 3 >> "$out" || exit 1
+  timeout -k 10 300 python bench.py --config cfg3 --rehearse-shard $r/8 --steps $steps --warmup 3 --no-cpu-baseline --no-sweep >> "$out" || exit 1
 done
