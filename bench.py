@@ -147,6 +147,44 @@ def cpu_baseline(n_sample, seed, repeats=3):
             "other_variants": {k: rnd(v) for k, v in rows.items()}}
 
 
+def init_group(dist, backend, device, rank, world, timeout_s=300):
+    """The process group for N > 1 (RCCL; DECDS_BENCH_BACKEND=gloo rehearses the path with ranks
+    sharing devices). A failed or stuck rendezvous ends the process with a clear message and a
+    non-zero exit instead of hanging the driver's run."""
+    import datetime
+    try:
+        if backend == "gloo":
+            dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=timeout_s))
+        else:
+            dist.init_process_group("nccl", device_id=device, timeout=datetime.timedelta(seconds=timeout_s))
+        dist.barrier()  # the first collective: fails here, not inside the timed region
+    except Exception as e:  # noqa: BLE001 - any init failure ends the bench
+        sys.stderr.write("bench.py: rank %d/%d: %s process group init failed: %s: %s\n"
+                         % (rank, world, "RCCL" if backend == "nccl" else backend, type(e).__name__, e))
+        sys.stderr.flush()
+        os._exit(3)
+
+
+def rank_record(torch, rank, local, world, lo, hi, shard_bytes, enc_ms, plan_ms, dec_ms, enc_bytes, dec_bytes,
+                n_ready, checked, rep_len, elapsed, steps):
+    """one rank's per-GPU figures for the N > 1 line's per_rank (gathered with all_gather_object)"""
+    import socket
+    props = torch.cuda.get_device_properties(local)
+    uuid = getattr(props, "uuid", None)
+    enc_gbs = enc_bytes / (enc_ms * 1e-3) / 1e9
+    dec_gbs = dec_bytes / (dec_ms * 1e-3) / 1e9 if dec_ms > 0 else 0.0
+    return {"rank": rank, "local_rank": local, "host": socket.gethostname(), "device": local,
+            "device_uuid": str(uuid) if uuid is not None else None,
+            "pci_bus_id": getattr(props, "pci_bus_id", None), "device_name": props.name,
+            "chunksets": [lo, hi], "shard_bytes": shard_bytes,
+            "encode_ms": round(enc_ms, 4), "plan_ms": round(plan_ms, 4), "decode_ms": round(dec_ms, 4),
+            "encode_frac": round(enc_gbs / HBM_PEAK_GBS, 4), "decode_frac": round(dec_gbs / HBM_PEAK_GBS, 4),
+            "ready_chunksets": n_ready, "not_ready_chunksets": hi - lo - n_ready,
+            "repaired_checked": checked, "repaired_blob_bytes": rep_len,
+            "elapsed_s": round(elapsed, 6),
+            "gpu_GiBps": round((shard_bytes + rep_len) / 2 * steps / GIB / elapsed, 2)}
+
+
 def main():
     args = parse()
     import numpy as np
@@ -177,10 +215,7 @@ def main():
         local = local % torch.cuda.device_count()
     torch.cuda.set_device(local)
     if dist_on:
-        if backend == "gloo":
-            dist.init_process_group("gloo")
-        else:
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        init_group(dist, backend, torch.device("cuda", local), rank, world)
 
     blob_per_gpu, desc = CONFIGS[args.config]
     n_total = -(-(blob_per_gpu * world) // CS)
@@ -261,6 +296,7 @@ def main():
     for c in np.nonzero(st == 0)[0].tolist():
         assert torch.equal(out[c * CS:(c + 1) * CS], src[c * CS:(c + 1) * CS]), "repaired chunkset %d differs" % c
     n_ready = int((st == 0).sum())
+    checked = n_ready  # every ready chunkset's repaired bytes were compared with its source above
     if args.spot_out:
         spots = sorted({0, n // 2, n - 1})
         rows = coded.as_strided((n * N, F), (pitch, 1))
@@ -370,11 +406,16 @@ def main():
     # value: blob bytes encoded plus blob bytes repaired (only the chunksets that were ready; the
     # decode kernel skips the rest), halved — encode+repair GiB/s of blob, whole job
     rep_len = sum(min(CS, blob_len_rank - c * CS) for c in np.nonzero(st == 0)[0].tolist())
+    # this rank's figures: with N > 1 every rank's are gathered into the line's per_rank (BASELINE
+    # configs[4]: per-GPU and whole-node GiB/s), with the device each rank ran on
+    mine = rank_record(torch, rank, local, world, lo, hi, blob_len_rank, enc_ms, plan_ms, dec_ms, enc_bytes, dec_bytes,
+                       n_ready, checked, rep_len, elapsed, args.steps)
     if dist_on:
-        rt = torch.tensor([float(rep_len)], dtype=torch.float64, device="cpu" if backend == "gloo" else dev)
-        dist.all_reduce(rt, op=dist.ReduceOp.SUM)
-        rep_total = float(rt.item())
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, mine)
+        rep_total = float(sum(r["repaired_blob_bytes"] for r in per_rank))
     else:
+        per_rank = [mine]
         rep_total = float(rep_len)
     if rank == 0 or rehearse:
         # whole-job blob bytes (a rehearsal: this shard's bytes only)
@@ -410,6 +451,15 @@ def main():
             "commitment": commit,
             "encode_batch_sweep": sweep,
         }
+        if dist_on:
+            line["world_size"] = dist.get_world_size()
+            line["backend"] = "rccl" if backend == "nccl" else backend
+            line["per_rank"] = per_rank
+            devs = [r["device_uuid"] or "%s/%d" % (r["host"], r["local_rank"]) for r in per_rank]
+            line["scaling_point"] = len(set(devs)) == world
+            if not line["scaling_point"]:
+                line["scaling_note"] = ("ranks share devices (%d ranks on %d devices): a rehearsal of the N-rank "
+                                        "path, not a scaling measurement" % (world, len(set(devs))))
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args.cpu_sample, 0xDEC05002)
         else:

@@ -86,8 +86,8 @@ def _declare(L):
         "decds_device_count": (c.c_int, []),
         "decds_encode_batch": (c.c_int, [P, VP, SZ, VP, VP, SZ, VP]),
         "decds_repair_plan_batch": (c.c_int, [P, VP, SZ, SZ, VP, VP, I8P, I32P, VP]),
-        "decds_decode_batch": (c.c_int, [P, VP, SZ, SZ, VP, VP, I32P, VP]),
-        "decds_repair_batch": (c.c_int, [P, VP, SZ, SZ, VP, VP, I8P, VP, I32P, VP]),
+        "decds_decode_batch": (c.c_int, [P, VP, SZ, SZ, VP, VP, I32P, VP, VP]),
+        "decds_repair_batch": (c.c_int, [P, VP, SZ, SZ, VP, VP, I8P, VP, I32P, VP, VP]),
         "decds_fill_random_device": (c.c_int, [P, c.c_uint64, c.c_uint64, VP, SZ, VP]),
         "decds_fill_random_host": (None, [c.c_uint64, c.c_uint64, VP, SZ]),
         "decds_rank_push": (c.c_int, [VP, VP, c.POINTER(c.c_uint32), VP, c.c_uint32]),
@@ -102,7 +102,7 @@ def _declare(L):
         "decds_repairing_chunkset_add_chunk": (c.c_int, [P, SZ, SZ, VP, SZ, VP, SZ]),
         "decds_repairing_chunkset_add_chunk_unvalidated": (c.c_int, [P, SZ, VP, SZ]),
         "decds_repairing_chunkset_is_ready_to_repair": (c.c_int, [P]),
-        "decds_repairing_chunkset_repair": (c.c_int, [P, VP, SZ]),
+        "decds_repairing_chunkset_repair": (c.c_int, [P, VP, SZ, c.POINTER(SZ)]),
         "decds_repairing_chunkset_free": (None, [P]),
         "decds_blob_encode_host": (c.c_int, [P, VP, SZ, VP, VP, SZ]),
         "decds_blob_repair_host": (c.c_int, [P, VP, SZ, VP, SZ, VP, VP, SZ]),

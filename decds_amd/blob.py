@@ -90,6 +90,7 @@ class Blob:
         check(lib().decds_blob_new(arr, n_ctx, ctypes.c_void_p(buf.ctypes.data if buf.size else 0), buf.size,
                                    None if cv is None else ctypes.c_void_p(cv.ctypes.data), ctypes.byref(h)))
         self._h = h
+        self._ctxs = ctxs  # the contexts stay alive while this object uses them (close() still frees it first)
         _adopt_by(ctxs, self)
 
     def get_blob_header(self):
@@ -151,6 +152,7 @@ class RepairingBlob:
                                                    header.get_root_commitment(), roots, ctypes.byref(h)))
         self._h = h
         self.header = header
+        self._ctxs = ctxs  # the contexts stay alive while this object uses them (close() still frees it first)
         _adopt_by(ctxs, self)
         if device_budget is not None:
             check(lib().decds_repairing_blob_set_device_budget(h, int(device_budget)))

@@ -167,6 +167,9 @@ class RepairingChunkSet:
         cm = None if commitment is None else bytes(commitment)
         check(lib().decds_repairing_chunkset_new(ctx.handle, chunkset_id, cm, ctypes.byref(h)))
         self._h = h
+        self._ctx = ctx  # repair() runs on the context's device: keep it alive
+        if hasattr(ctx, "_adopt"):
+            ctx._adopt(self)  # ... and an explicit ctx.close() releases this object first
         self.chunkset_id = chunkset_id
 
     def add_chunk(self, chunk):
@@ -187,16 +190,23 @@ class RepairingChunkSet:
         return bool(lib().decds_repairing_chunkset_is_ready_to_repair(self._h))
 
     def repair(self):
-        """chunkset.rs:200-208; raises DecdsError(ChunksetNotYetReadyToRepair | ChunksetRepairingFailed)."""
-        out = ctypes.create_string_buffer(CHUNKSET_BYTES)
-        check(lib().decds_repairing_chunkset_repair(self._h, out, CHUNKSET_BYTES))
-        return out.raw
+        """chunkset.rs:200-208; raises DecdsError(ChunksetNotYetReadyToRepair | ChunksetRepairingFailed).
+        Returns get_decoded_data's vector: the decoded pieces cut at the last boundary marker — the 10 MiB
+        chunkset for validated chunks, shorter or up to 9 bytes longer for corrupted unvalidated ones."""
+        cap = CHUNKSET_BYTES + K - 1  # DECDS_DECODED_MAX_BYTES
+        out = ctypes.create_string_buffer(cap)
+        n = ctypes.c_size_t()
+        check(lib().decds_repairing_chunkset_repair(self._h, out, cap, ctypes.byref(n)))
+        return out.raw[:n.value]
+
+    def free(self):
+        if self._h:
+            lib().decds_repairing_chunkset_free(self._h)
+            self._h = None
 
     def __del__(self):
         try:
-            if self._h:
-                lib().decds_repairing_chunkset_free(self._h)
-                self._h = None
+            self.free()
         except Exception:
             pass
 

@@ -63,18 +63,42 @@ def repair_plan_batch(ctx, coded, n, cand, plan, verdicts, status, pitch=CODED_P
                                         _ptr(verdicts), _ptr(status), _stream(stream)))
 
 
-def decode_batch(ctx, coded, n, plan, dst, status, pitch=CODED_PIECE_BYTES, stream=None):
+REPAIR_INFO_BYTES = 16  # decds_repair_info: u32 decoded_len, 10 tail bytes, 2 reserved
+
+
+def decode_batch(ctx, coded, n, plan, dst, status, pitch=CODED_PIECE_BYTES, stream=None, info=None):
+    """chunkset.rs:200-208 for n chunksets. info (optional, n*16 bytes, 4-byte aligned device tensor):
+    per chunkset rlnc get_decoded_data's length (cut at the last boundary marker) and the 10 decoded
+    tail bytes past the chunkset; read it with repair_info()."""
     _need(coded, (n * N - 1) * pitch + CODED_PIECE_BYTES, "coded")
     _need(plan, n * REPAIR_PLAN_BYTES, "plan")
     _need(dst, n * CHUNKSET_BYTES, "dst")
     _need(status, n * 4, "status")
+    if info is not None:
+        _need(info, n * REPAIR_INFO_BYTES, "info")
     check(lib().decds_decode_batch(ctx.handle, _ptr(coded), pitch, n, _ptr(plan), _ptr(dst), _ptr(status),
-                                   _stream(stream)))
+                                   None if info is None else _ptr(info), _stream(stream)))
 
 
-def repair_batch(ctx, coded, n, cand, plan, verdicts, dst, status, pitch=CODED_PIECE_BYTES, stream=None):
+def repair_batch(ctx, coded, n, cand, plan, verdicts, dst, status, pitch=CODED_PIECE_BYTES, stream=None, info=None):
     repair_plan_batch(ctx, coded, n, cand, plan, verdicts, status, pitch, stream)
-    decode_batch(ctx, coded, n, plan, dst, status, pitch, stream)
+    decode_batch(ctx, coded, n, plan, dst, status, pitch, stream, info)
+
+
+def repair_info(info, n):
+    """(decoded_len int64[n], tail uint8[n, 10]) from an info tensor/array filled by decode_batch"""
+    a = np.ascontiguousarray(info.cpu().numpy() if hasattr(info, "cpu") else info).view(np.uint8)[:n * REPAIR_INFO_BYTES]
+    a = a.reshape(n, REPAIR_INFO_BYTES)
+    return a[:, :4].copy().view("<u4").reshape(n).astype(np.int64), a[:, 4:14].copy()
+
+
+def decoded_bytes(dst_chunkset, decoded_len, tail):
+    """get_decoded_data's vector of one chunkset from its CS bytes in dst and its repair info"""
+    from ._capi import CHUNKSET_BYTES as CS
+    d = dst_chunkset.cpu().numpy() if hasattr(dst_chunkset, "cpu") else np.asarray(dst_chunkset)
+    if decoded_len <= CS:
+        return d[:decoded_len].tobytes()
+    return d[:CS].tobytes() + bytes(tail[:decoded_len - CS])
 
 
 def commit_batch(ctx, coded, n, digests, roots, proofs, first_chunkset_id=0, pitch=CODED_PIECE_BYTES, stream=None):
@@ -211,7 +235,8 @@ def host_unregister(arr):
     check(lib().decds_host_unregister(ctypes.c_void_p(arr.ctypes.data)))
 
 
-__all__ = ["coded_buffer", "commit_batch", "encode_batch", "repair_plan_batch", "decode_batch", "repair_batch", "fill_random_device",
+__all__ = ["coded_buffer", "commit_batch", "encode_batch", "repair_plan_batch", "decode_batch", "repair_batch", "repair_info",
+           "decoded_bytes", "REPAIR_INFO_BYTES", "fill_random_device",
            "fill_random_host", "blob_encode_host", "blob_repair_host", "blob_encode_host_multi",
            "blob_repair_host_multi", "host_register", "host_unregister",
            "NO_CANDIDATE"]

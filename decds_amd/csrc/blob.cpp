@@ -190,46 +190,56 @@ int repair_range(decds_ctx *ctx, const uint8_t *coded_host, size_t n, const uint
         }
     } pin;
     {
-        hipError_t pe = hipHostMalloc(&pin.p, SLOTS * batch * (N + sizeof(int32_t)), DECDS_HOST_MALLOC_FLAGS);
+        hipError_t pe = hipHostMalloc(&pin.p, SLOTS * batch * (sizeof(decds_repair_info) + sizeof(int32_t) + N),
+                                      DECDS_HOST_MALLOC_FLAGS);
         if (pe) return decds_hip_error(pe, "hipHostMalloc");
     }
     uint8_t *cand_h[SLOTS];
     int32_t *stat_h[SLOTS];
+    decds_repair_info *info_h[SLOTS];
     for (int i = 0; i < SLOTS; i++) {
-        stat_h[i] = reinterpret_cast<int32_t *>(pin.p) + i * batch;
-        cand_h[i] = reinterpret_cast<uint8_t *>(pin.p) + SLOTS * batch * sizeof(int32_t) + i * batch * N;
+        info_h[i] = reinterpret_cast<decds_repair_info *>(pin.p) + i * batch;
+        stat_h[i] = reinterpret_cast<int32_t *>(reinterpret_cast<uint8_t *>(pin.p) + SLOTS * batch * sizeof(decds_repair_info)) +
+                    i * batch;
+        cand_h[i] = reinterpret_cast<uint8_t *>(pin.p) + SLOTS * batch * (sizeof(decds_repair_info) + sizeof(int32_t)) +
+                    i * batch * N;
     }
     HostUse uout(out, blob_len), uin(coded_host, n * N * F);
     std::lock_guard<std::mutex> lock(ctx->host_mu);
-    uint8_t *dcoded[SLOTS], *dcand[SLOTS], *dplan[SLOTS], *dverd[SLOTS], *dstat[SLOTS], *ddst[SLOTS];
-    const size_t sz[6] = {align256(batch * N * F), align256(batch * N), align256(batch * DECDS_REPAIR_PLAN_BYTES),
-                          align256(batch * N), align256(batch * sizeof(int32_t)), align256(batch * CS)};
-    const size_t per = sz[0] + sz[1] + sz[2] + sz[3] + sz[4] + sz[5];
+    uint8_t *dcoded[SLOTS], *dcand[SLOTS], *dplan[SLOTS], *dverd[SLOTS], *dstat[SLOTS], *ddst[SLOTS], *dinfo[SLOTS];
+    const size_t sz[7] = {align256(batch * N * F), align256(batch * N), align256(batch * DECDS_REPAIR_PLAN_BYTES),
+                          align256(batch * N), align256(batch * sizeof(int32_t)), align256(batch * CS),
+                          align256(batch * sizeof(decds_repair_info))};
+    const size_t per = sz[0] + sz[1] + sz[2] + sz[3] + sz[4] + sz[5] + sz[6];
     uint8_t *base;
     hipError_t e;
     if ((e = decds_ctx_scratch(ctx, SLOTS * per, &base))) return decds_hip_error(e, "hipMalloc");
     for (int i = 0; i < SLOTS; i++) {
-        uint8_t **dst[6] = {&dcoded[i], &dcand[i], &dplan[i], &dverd[i], &dstat[i], &ddst[i]};
-        for (int j = 0; j < 6; j++) *dst[j] = base, base += sz[j];
+        uint8_t **dst[7] = {&dcoded[i], &dcand[i], &dplan[i], &dverd[i], &dstat[i], &ddst[i], &dinfo[i]};
+        for (int j = 0; j < 7; j++) *dst[j] = base, base += sz[j];
     }
     Pipe pp;
     if ((e = pp.init())) return decds_hip_error(e, "stream/event setup");
     int rc = DECDS_OK;
     size_t pending_b0[SLOTS], pending_nb[SLOTS] = {};
     for (int i = 0; i < SLOTS; i++) pending_b0[i] = (size_t)-1;
-    // host side of slot k once its D2H is done: a ready chunkset whose decoded tail is not marker
-    // || zeros is ChunksetRepairingFailed and gets no data (its region was written: clear it)
+    // host side of slot k once its D2H is done: a ready chunkset whose decoded data holds no boundary
+    // marker is ChunksetRepairingFailed and gets no data (its region was written: clear it); one whose
+    // cut (get_decoded_data, rows accepted unvalidated) falls inside the chunkset is zero past the cut
+    // (blob.rs:464 truncates only: a cut past the chunkset changes nothing)
     auto finish = [&](int k) -> int {
         if (pending_b0[k] == (size_t)-1) return DECDS_OK;
         hipError_t ee = hipEventSynchronize(pp.out_done[k]);
         if (ee) return decds_hip_error(ee, "hipEventSynchronize");
         for (size_t c = 0; c < pending_nb[k]; c++) {
             const size_t cs = pending_b0[k] + c;
-            if (status_host[cs] == DECDS_OK && stat_h[k][c] != DECDS_OK) {
-                status_host[cs] = DECDS_ERR_CHUNKSET_REPAIRING_FAILED;
+            if (status_host[cs] != DECDS_OK) continue;
+            const size_t off = cs * CS, size = std::min(blob_len - off, (size_t)CS);
+            const size_t keep = stat_h[k][c] != DECDS_OK ? 0 : std::min<size_t>(info_h[k][c].decoded_len, size);
+            if (stat_h[k][c] != DECDS_OK) status_host[cs] = DECDS_ERR_CHUNKSET_REPAIRING_FAILED;
+            if (keep < size) {
                 if (!uout.pinned() && (ee = ctx->out_ring.flush())) return decds_hip_error(ee, "D2H (staged)");
-                const size_t off = cs * CS;
-                std::memset(out + off, 0, std::min(blob_len - off, (size_t)CS));
+                std::memset(out + off + keep, 0, size - keep);
             }
         }
         pending_b0[k] = (size_t)-1;
@@ -269,10 +279,12 @@ int repair_range(decds_ctx *ctx, const uint8_t *coded_host, size_t n, const uint
             break;
         }
         if ((rc = decds_repair_batch(ctx, dcoded[k], F, nb, dcand[k], dplan[k], reinterpret_cast<int8_t *>(dverd[k]),
-                                     ddst[k], reinterpret_cast<int32_t *>(dstat[k]), pp.comp)))
+                                     ddst[k], reinterpret_cast<int32_t *>(dstat[k]),
+                                     reinterpret_cast<decds_repair_info *>(dinfo[k]), pp.comp)))
             break;
         if ((e = hipEventRecord(pp.k_done[k], pp.comp)) || (e = hipStreamWaitEvent(pp.d2h, pp.k_done[k], 0)) ||
-            (e = hipMemcpyAsync(stat_h[k], dstat[k], nb * sizeof(int32_t), hipMemcpyDeviceToHost, pp.d2h))) {
+            (e = hipMemcpyAsync(stat_h[k], dstat[k], nb * sizeof(int32_t), hipMemcpyDeviceToHost, pp.d2h)) ||
+            (e = hipMemcpyAsync(info_h[k], dinfo[k], nb * sizeof(decds_repair_info), hipMemcpyDeviceToHost, pp.d2h))) {
             rc = decds_hip_error(e, "D2H");
             break;
         }
@@ -371,6 +383,7 @@ struct RbChunkset {
     bool repaired = false;  // get_repaired_chunkset took it (blob.rs:458-462: even if repair fails)
     bool decoded = false;   // decoded on the device into decode area `area`
     int32_t dec_status = DECDS_OK;
+    uint32_t dec_len = 0;  // get_decoded_data's cut (decds_repair_info::decoded_len)
     int32_t slot = -1;   // device row slot
     int32_t hslot = -1;  // page-locked host spill slot
     int32_t area = -1;   // decode area holding its decoded bytes
@@ -384,8 +397,8 @@ constexpr size_t RB_AREA_BYTES = RB_ROWS_BYTES + RB_OUT_BYTES;
 constexpr size_t RB_SLAB_BYTES = RB_SLAB_SLOTS * RB_ROWS_BYTES;
 // small device / pinned areas: plans, bases, statuses, valid flags
 constexpr size_t RB_SM_PLAN = 0, RB_SM_INB = RB_SM_PLAN + RB_MAX_DECODE * 128, RB_SM_OUTB = RB_SM_INB + RB_MAX_DECODE * 8,
-                 RB_SM_STAT = RB_SM_OUTB + RB_MAX_DECODE * 8, RB_SM_VALID = RB_SM_STAT + RB_MAX_DECODE * 4,
-                 RB_SM_BYTES = RB_SM_VALID + RB_MAX_ROWS;
+                 RB_SM_STAT = RB_SM_OUTB + RB_MAX_DECODE * 8, RB_SM_INFO = RB_SM_STAT + RB_MAX_DECODE * 4,
+                 RB_SM_VALID = RB_SM_INFO + RB_MAX_DECODE * sizeof(decds_repair_info), RB_SM_BYTES = RB_SM_VALID + RB_MAX_ROWS;
 
 struct RbShard {
     decds_ctx *ctx = nullptr;
@@ -531,10 +544,12 @@ struct RbShard {
         uint64_t *inb = reinterpret_cast<uint64_t *>(h_small + RB_SM_INB), *outb = reinterpret_cast<uint64_t *>(h_small + RB_SM_OUTB);
         hipError_t e;
         int st = DECDS_OK;
+        for (size_t i = 0; i < m; i++) {  // every area taken is owned before anything can fail
+            cs[todo[i]].area = area[i];
+            area_owner[area[i]] = (int64_t)todo[i];
+        }
         for (size_t i = 0; i < m && st == DECDS_OK; i++) {
             RbChunkset &c = cs[todo[i]];
-            c.area = area[i];
-            area_owner[area[i]] = (int64_t)todo[i];
             std::memset(&plans[i], 0, sizeof(RepairPlan));
             for (uint32_t k = 0; k < K; k++) plans[i].sel[k] = (uint8_t)k;
             plans[i].rank = K;
@@ -562,10 +577,11 @@ struct RbShard {
         if (st == DECDS_OK &&
             (e = launch_decode(ctx->geom, nullptr, F, m, d_small + RB_SM_PLAN, nullptr,
                                reinterpret_cast<int32_t *>(d_small + RB_SM_STAT), reinterpret_cast<const uint64_t *>(d_small + RB_SM_INB),
-                               reinterpret_cast<const uint64_t *>(d_small + RB_SM_OUTB), ctx->poly, ctx->marker, s)))
+                               reinterpret_cast<const uint64_t *>(d_small + RB_SM_OUTB), ctx->poly, ctx->marker,
+                               d_small + RB_SM_INFO, s)))
             st = decds_hip_error(e, "rlnc_decode_kernel launch");
         if (st == DECDS_OK &&
-            ((e = hipMemcpyAsync(h_small + RB_SM_STAT, d_small + RB_SM_STAT, m * 4, hipMemcpyDeviceToHost, s)) ||
+            ((e = hipMemcpyAsync(h_small + RB_SM_STAT, d_small + RB_SM_STAT, RB_SM_VALID - RB_SM_STAT, hipMemcpyDeviceToHost, s)) ||
              (e = hipStreamSynchronize(s))))
             st = decds_hip_error(e, "D2H (statuses)");
         if (st != DECDS_OK) {
@@ -573,9 +589,11 @@ struct RbShard {
             return st;
         }
         const int32_t *stat = reinterpret_cast<const int32_t *>(h_small + RB_SM_STAT);
+        const decds_repair_info *info = reinterpret_cast<const decds_repair_info *>(h_small + RB_SM_INFO);
         for (size_t i = 0; i < m; i++) {
             cs[todo[i]].decoded = true;
             cs[todo[i]].dec_status = stat[i];
+            cs[todo[i]].dec_len = info[i].decoded_len;
         }
         return DECDS_OK;
     }
@@ -1088,16 +1106,19 @@ int decds_repairing_blob_get_repaired_chunkset(decds_repairing_blob *rb, size_t 
         return decds_set_error(DECDS_ERR_CHUNKSET_REPAIRING_FAILED, "chunkset %zu repairing failed: RLNC Decoding error: %s",
                                chunkset_id, "invalid decoded data format");
     }
-    HostUse uo(out, size);
+    // get_decoded_data's vector (cut at the last boundary marker: CS for any validated chunk set,
+    // rlnc_tail_scan_kernel) truncated to the chunkset's real size (blob.rs:464 truncates only)
+    const size_t len = std::min<size_t>(size, c.dec_len);
+    HostUse uo(out, len);
     hipError_t e;
-    if ((e = copy_d2h(out, sh.area_out(c.area), size, uo.pinned(), sh.out_ring, sh.s)) || (e = sh.out_ring.flush()) ||
+    if ((e = copy_d2h(out, sh.area_out(c.area), len, uo.pinned(), sh.out_ring, sh.s)) || (e = sh.out_ring.flush()) ||
         (e = hipStreamSynchronize(sh.s))) {
         sh.out_ring.abandon();
         return decds_hip_error(e, "D2H (repaired chunkset)");
     }
     sh.drop_area(c);
     sh.drop_slot(c);
-    if (out_len) *out_len = size;  // blob.rs:464 truncate to the chunkset's real size
+    if (out_len) *out_len = len;
     return DECDS_OK;
 }
 

@@ -37,7 +37,7 @@ namespace decds {
 // Device and pinned buffers of one in-flight chunkset-mirror call. Small-area offsets (device and
 // host mirror alike):
 constexpr size_t SM_CV = 0, SM_CAND = 256, SM_STATUS = 288, SM_VERD = 320, SM_PLAN = 384, SM_ROOT = 512,
-                 SM_DIG = 1024, SM_PRF = 2048, SM_BYTES = 4096;
+                 SM_INFO = 768, SM_DIG = 1024, SM_PRF = 2048, SM_BYTES = 4096;
 static_assert(SM_PRF + N * PROOF_SIZE * 32 <= SM_BYTES && SM_DIG + N * 32 <= SM_PRF, "lane small-area layout");
 
 struct Lane {
@@ -535,12 +535,12 @@ int decds_repairing_chunkset_is_ready_to_repair(const decds_repairing_chunkset *
     return r && !r->repaired && r->rank == K;
 }
 
-int decds_repairing_chunkset_repair(decds_repairing_chunkset *r, uint8_t *out, size_t out_len) {
+int decds_repairing_chunkset_repair(decds_repairing_chunkset *r, uint8_t *out, size_t out_cap, size_t *out_len) {
     if (!r) return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "null repairing chunkset");
     if (r->repaired) return decds_set_error(DECDS_ERR_CHUNKSET_ALREADY_REPAIRED, "chunkset %zu is already repaired", r->id);
     // chunkset.rs:201,206
     if (r->rank != K) return decds_set_error(DECDS_ERR_CHUNKSET_NOT_YET_READY, "chunkset %zu is not ready to repair", r->id);
-    if (!out || out_len < CS) return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "out buffer < %llu", (unsigned long long)CS);
+    if (!out) return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "null out buffer");
     decds_ctx *ctx = r->ctx;
     int s = decds_ctx_bind(ctx);
     if (s) return s;
@@ -557,18 +557,27 @@ int decds_repairing_chunkset_repair(decds_repairing_chunkset *r, uint8_t *out, s
         return decds_hip_error(e, "H2D");
     if ((s = decds_repair_batch(ctx, L.d_coded, F, 1, L.d_small + SM_CAND, L.d_small + SM_PLAN,
                                 reinterpret_cast<int8_t *>(L.d_small + SM_VERD), L.d_cs,
-                                reinterpret_cast<int32_t *>(L.d_small + SM_STATUS), L.s)))
+                                reinterpret_cast<int32_t *>(L.d_small + SM_STATUS),
+                                reinterpret_cast<decds_repair_info *>(L.d_small + SM_INFO), L.s)))
         return s;
     if ((e = hipMemcpyAsync(L.h_big, L.d_cs, CS, hipMemcpyDeviceToHost, L.s)) ||
         (e = hipMemcpyAsync(L.h_small + SM_STATUS, L.d_small + SM_STATUS, 4, hipMemcpyDeviceToHost, L.s)) ||
+        (e = hipMemcpyAsync(L.h_small + SM_INFO, L.d_small + SM_INFO, sizeof(decds_repair_info), hipMemcpyDeviceToHost, L.s)) ||
         (e = hipStreamSynchronize(L.s)))
         return decds_hip_error(e, "D2H");
     int32_t st;
     std::memcpy(&st, L.h_small + SM_STATUS, 4);
-    if (st != DECDS_OK)
+    if (st != DECDS_OK)  // chunkset.rs:202-204: no boundary marker in the decoded data
         return decds_set_error(DECDS_ERR_CHUNKSET_REPAIRING_FAILED, "chunkset %zu repairing failed: RLNC Decoding error: %s",
                                r->id, st == DECDS_ERR_CHUNKSET_REPAIRING_FAILED ? "invalid decoded data format" : decds_status_string(st));
-    par_memcpy(out, L.h_big, CS);
+    decds_repair_info info;
+    std::memcpy(&info, L.h_small + SM_INFO, sizeof info);
+    const size_t len = info.decoded_len;  // get_decoded_data's cut at the last marker (CS when intact)
+    if (out_len) *out_len = len;
+    if (out_cap < len)  // the decoder is not consumed: the caller may retry with a larger buffer
+        return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "out buffer %zu < decoded length %zu", out_cap, len);
+    par_memcpy(out, L.h_big, std::min<size_t>(len, CS));
+    if (len > CS) std::memcpy(out + CS, info.tail, len - CS);
     r->repaired = true;  // repair(self) consumes the decoder (chunkset.rs:200)
     r->rows.clear();
     r->rows.shrink_to_fit();

@@ -34,10 +34,13 @@ hipError_t launch_repair_plan(const uint8_t *coded, size_t pitch, size_t n, cons
                               uint8_t *plan, int8_t *verdicts, int32_t *status, uint32_t poly,
                               uint32_t gen, hipStream_t stream);
 // in_bases / out_bases (device arrays of n addresses, or NULL): the gather form — chunkset c's
-// accepted rows at in_bases[c] + plan.sel[k]*pitch, its output at out_bases[c]
+// accepted rows at in_bases[c] + plan.sel[k]*pitch, its output at out_bases[c]. info (n x 16 B,
+// decds_repair_info, or NULL): get_decoded_data's length and the 10 decoded tail bytes of every
+// chunkset that decodes; the decode kernel is followed by rlnc_tail_scan_kernel on the same stream.
 hipError_t launch_decode(const LaunchGeom &g, const uint8_t *coded, size_t pitch, size_t n,
                          const uint8_t *plan, uint8_t *dst, int32_t *status, const uint64_t *in_bases,
-                         const uint64_t *out_bases, uint32_t poly, uint32_t marker, hipStream_t stream);
+                         const uint64_t *out_bases, uint32_t poly, uint32_t marker, uint8_t *info,
+                         hipStream_t stream);
 hipError_t launch_fill_random(uint64_t seed, uint64_t byte_offset, uint8_t *dst, size_t nbytes,
                               hipStream_t stream);
 const char *encode_kernel_name(size_t n);  // the kernel launch_encode runs for n chunksets

@@ -40,7 +40,11 @@ constexpr uint32_t TILE_BLOCKS = WG;                          // one 16-col bloc
 constexpr uint32_t ROW_BYTES = 16;                            // one nibble row: 16 outputs' products
 constexpr uint32_t TABLE_BYTES = 16 * ROW_BYTES;              // 16 nibble rows = 256 B = the 64 banks once
 constexpr uint32_t LDS_BYTES = K * 2 * TABLE_BYTES;           // 5 KiB
-constexpr uint32_t SWEEP_LDS = 2 * LDS_BYTES + 16;             // two table buffers + the next-tile slot
+constexpr uint32_t SWEEP_LDS = 2 * LDS_BYTES + 32;             // two table buffers + the next-tile slot + TailLds
+constexpr uint32_t DEC_LDS = LDS_BYTES + 16;                   // one-tile decode: tables + TailLds
+// (the tables sit at LDS address 0 of the dynamic area: the inline-asm ds_read_b128 lookups address
+// them absolutely, so a kernel holding them must not declare static __shared__ variables — those
+// would be placed first and move the dynamic area)
 
 #ifndef DECDS_BUILD_XOR
 #define DECDS_BUILD_XOR 1  // table builds in a bank-conflict-free row order (build_tables)
@@ -765,6 +769,75 @@ void rlnc_encode_sweep_kernel(const uint8_t *__restrict__ src, size_t n, const u
     }
 }
 
+// rlnc Decoder::get_decoded_data (chunkset.rs:202-204, restated in oracle/rlnc_oracle.c
+// orc_decoder_get_decoded_data) cuts the concatenated decoded pieces (CS + 10 bytes) at the LAST
+// boundary marker; no marker at all is an error (-> ChunksetRepairingFailed). An intact chunkset ends
+// in marker || 9 zeros, so its cut is at CS. The edge pass decodes the 10 tail bytes [CS, CS + 10)
+// (piece 9's last columns) and notes each and the highest marker among them in LDS (tail_note);
+// after a barrier tail_finish writes the repair info (decoded length, tail bytes) and, when no tail
+// byte is the marker, hands the chunkset to rlnc_tail_scan_kernel, which looks for the last marker
+// in the decoded bytes already in dst (only corrupted rows, accepted unvalidated, get there).
+struct TailLds {
+    uint32_t cut;       // 1 + index of the last marker among the tail bytes, 0: none
+    uint32_t bytes[3];  // the 10 tail bytes
+};
+__device__ __forceinline__ void tail_reset(TailLds &t) {
+    if (threadIdx.x < 4) reinterpret_cast<uint32_t *>(&t)[threadIdx.x] = 0;
+}
+__device__ __forceinline__ void tail_note(TailLds &t, uint64_t p, uint32_t z, uint32_t marker) {
+    const uint32_t j = (uint32_t)(p - CS);
+    reinterpret_cast<uint8_t *>(t.bytes)[j] = (uint8_t)z;
+    if (z == marker) atomicMax(&t.cut, j + 1);
+}
+// after a barrier behind every tail_note; info: 4 dwords per chunkset (decds_repair_info)
+__device__ __forceinline__ void tail_finish(const TailLds &t, uint32_t c, int32_t *status, uint32_t *info) {
+    if (threadIdx.x != 0) return;
+    if (info) {
+        uint32_t *o = info + 4 * (size_t)c;
+        o[0] = t.cut ? (uint32_t)CS + t.cut - 1 : 0u;
+        o[1] = t.bytes[0];
+        o[2] = t.bytes[1];
+        o[3] = t.bytes[2];
+    }
+    if (!t.cut) status[c] = (int32_t)TAIL_SCAN_STATUS;
+}
+
+// The backward marker scan for the chunksets tail_finish left at TAIL_SCAN_STATUS: one workgroup
+// per chunkset, 4 KiB of decoded bytes per step from the end of the chunkset down; the highest
+// marker position found is the decoded length, none anywhere is ChunksetRepairingFailed. Every other
+// workgroup reads one status word and leaves.
+__global__ __launch_bounds__(WG) void rlnc_tail_scan_kernel(size_t n, const uint8_t *__restrict__ dst,
+                                                            int32_t *__restrict__ status,
+                                                            const uint64_t *__restrict__ out_bases,
+                                                            uint32_t *__restrict__ info, uint32_t marker) {
+    const uint32_t c = blockIdx.x;
+    if (c >= n || __builtin_amdgcn_readfirstlane(status[c]) != (int32_t)TAIL_SCAN_STATUS) return;
+    const uint8_t *obase = out_bases ? reinterpret_cast<const uint8_t *>(uniform_u64(out_bases[c])) : dst + (size_t)c * CS;
+    __shared__ uint32_t s_hit;
+    if (threadIdx.x == 0) s_hit = 0;
+    __syncthreads();
+    constexpr uint32_t STEP = WG * 16;
+    static_assert(CS % STEP == 0, "whole steps");
+    uint32_t hit = 0;
+    for (uint32_t blk = (uint32_t)CS; blk > 0;) {
+        blk -= STEP;
+        const uint32_t b0 = blk + threadIdx.x * 16;
+        uint32_t h = 0;
+        for (int b = 15; b >= 0 && !h; b--)
+            if (obase[b0 + b] == marker) h = b0 + b + 1;
+        if (__syncthreads_or(h != 0)) {
+            if (h) atomicMax(&s_hit, h);
+            __syncthreads();
+            hit = s_hit;
+            break;
+        }
+    }
+    if (threadIdx.x == 0) {
+        status[c] = hit ? 0 : 6;  // DECDS_OK / DECDS_ERR_CHUNKSET_REPAIRING_FAILED
+        if (info) info[4 * (size_t)c] = hit ? hit - 1 : 0u;
+    }
+}
+
 // Decode: workgroup = UNIT consecutive tiles of one chunkset. The accepted rows of chunkset cs are
 // rows plan.sel[k] of its 16-row group at coded + cs*16*pitch, or — gather form, in_bases != NULL —
 // rows plan.sel[k] at in_bases[cs] + sel*pitch, written to out_bases[cs] (the incremental
@@ -786,8 +859,10 @@ template <uint32_t UNIT>
 __global__ __launch_bounds__(WG, DECDS_DEC_WAVES) __attribute__((amdgpu_waves_per_eu(DECDS_DEC_WAVES, DECDS_DEC_WAVES)))
 void rlnc_decode_kernel(const uint8_t *__restrict__ coded, size_t pitch, size_t n, const RepairPlan *__restrict__ plan,
                         uint8_t *__restrict__ dst, int32_t *__restrict__ status, const uint64_t *__restrict__ in_bases,
-                        const uint64_t *__restrict__ out_bases, uint32_t poly, uint32_t marker) {
+                        const uint64_t *__restrict__ out_bases, uint32_t poly, uint32_t marker,
+                        uint32_t *__restrict__ info) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    TailLds &s_tail = *reinterpret_cast<TailLds *>(lds + LDS_BYTES);
     constexpr int DW = DECDS_DEC_DW;
     constexpr uint32_t T = TILES<DW>;
     static_assert(T % UNIT == 0, "a workgroup's tiles stay in one chunkset");
@@ -829,12 +904,12 @@ void rlnc_decode_kernel(const uint8_t *__restrict__ coded, size_t pitch, size_t 
     }
     Vec<DW> x[K];
     if constexpr (DECDS_PREFETCH_FIRST) load_block<K, DW>(x, ibase, ioff, tile_col<DW, false>(tile0, tile0 + UNIT, phase));
+    if (tile0 == 0) tail_reset(s_tail);
     build_tables<K, K>(lds, cw, poly);
     lds_barrier();
     if (tile0 == 0) {  // the whole workgroup: one pass over the edge columns
-        // piece 9's must decode to marker || zeros (rlnc get_decoded_data strips them; a mismatch
-        // is a repairing failure, chunkset.rs:202-204)
-        bool ok = true;
+        // the 10 bytes past the chunkset (piece 9's marker || zeros when intact) decide where
+        // get_decoded_data cuts (tail_note, chunkset.rs:202-204)
         for (uint32_t idx = threadIdx.x; idx < edge_cols<DW, false>(phase) * K; idx += WG) {
             const uint32_t i = idx % K, col = edge_col<DW, false>(idx / K, phase);
             uint32_t z = 0;
@@ -844,9 +919,10 @@ void rlnc_decode_kernel(const uint8_t *__restrict__ coded, size_t pitch, size_t 
             if (p < CS)
                 obase[p] = (uint8_t)z;
             else
-                ok &= z == (p == CS ? marker : 0u);
+                tail_note(s_tail, p, z, marker);
         }
-        if (__any(!ok) && (threadIdx.x & 63u) == 0) status[cs] = 6;  // DECDS_ERR_CHUNKSET_REPAIRING_FAILED
+        lds_barrier();
+        tail_finish(s_tail, cs, status, info);
     }
     // (realigning the piece stores — pieces start i bytes past alignment — through LDS staging or a DPP
     // wave shift measured 4-5 % slower / spilled: r02v/w)
@@ -917,8 +993,9 @@ void rlnc_decode_sweep_kernel(const uint8_t *__restrict__ coded, size_t pitch, s
                               const RepairPlan *__restrict__ plan, uint8_t *__restrict__ dst,
                               int32_t *__restrict__ status, const uint64_t *__restrict__ in_bases,
                               const uint64_t *__restrict__ out_bases, uint32_t poly, uint32_t marker,
-                              uint32_t *__restrict__ counter) {
+                              uint32_t *__restrict__ counter, uint32_t *__restrict__ info) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    TailLds &s_tail = *reinterpret_cast<TailLds *>(lds + 2 * LDS_BYTES + 16);
     constexpr uint32_t T = TILES<DW>;
     constexpr uint32_t phase = 0;
     uint32_t ooff[K];
@@ -931,11 +1008,11 @@ void rlnc_decode_sweep_kernel(const uint8_t *__restrict__ coded, size_t pitch, s
         d.resolve(coded, dst, pitch, in_bases, c);
         if (!d.ready) continue;
         const uint32_t cw = table_coeffs<K, K>(plan[c].inv, 1, K);  // input-major inverse
-        lds_barrier();
+        lds_barrier();  // also: the previous chunkset's tail_finish has read s_tail
+        tail_reset(s_tail);
         build_tables<K, K>(lds + LDS_BYTES, cw, poly);
         lds_barrier();
-        // piece 9's must decode to marker || zeros (chunkset.rs:202-204, as rlnc_decode_kernel)
-        bool ok = true;
+        // the tail bytes decide where get_decoded_data cuts (chunkset.rs:202-204, as rlnc_decode_kernel)
         for (uint32_t idx = threadIdx.x; idx < edge_cols<DW, false>(phase) * K; idx += WG) {
             const uint32_t i = idx % K, col = edge_col<DW, false>(idx / K, phase);
             uint32_t z = 0;
@@ -945,9 +1022,10 @@ void rlnc_decode_sweep_kernel(const uint8_t *__restrict__ coded, size_t pitch, s
             if (p < CS)
                 d.obase[p] = (uint8_t)z;
             else
-                ok &= z == (p == CS ? marker : 0u);
+                tail_note(s_tail, p, z, marker);
         }
-        if (__any(!ok) && (threadIdx.x & 63u) == 0) status[c] = 6;  // DECDS_ERR_CHUNKSET_REPAIRING_FAILED
+        lds_barrier();
+        tail_finish(s_tail, c, status, info);
     }
     // 2. the sweep (tiles in runs per XCD, each XCD with its own counter — rlnc_decode_kernel's
     // DEC_XCD_RUN — measured 1-2 % slower here at runs of 4, 8 and 16, r05q)
@@ -1318,10 +1396,10 @@ hipError_t launch_repair_plan(const uint8_t *coded, size_t pitch, size_t n, cons
     return hipGetLastError();
 }
 
-hipError_t launch_decode(const LaunchGeom &geom, const uint8_t *coded, size_t pitch, size_t n, const uint8_t *plan,
-                         uint8_t *dst, int32_t *status, const uint64_t *in_bases, const uint64_t *out_bases,
-                         uint32_t poly, uint32_t marker, hipStream_t stream) {
-    if (n == 0) return hipSuccess;
+static hipError_t launch_decode_kernel(const LaunchGeom &geom, const uint8_t *coded, size_t pitch, size_t n,
+                                       const uint8_t *plan, uint8_t *dst, int32_t *status, const uint64_t *in_bases,
+                                       const uint64_t *out_bases, uint32_t poly, uint32_t marker, uint32_t *info,
+                                       hipStream_t stream) {
     const RepairPlan *pl = reinterpret_cast<const RepairPlan *>(plan);
     if (decode_sweeps(n)) {
         static uint32_t resident = 0;
@@ -1340,14 +1418,26 @@ hipError_t launch_decode(const LaunchGeom &geom, const uint8_t *coded, size_t pi
             if (!geom.counters) return hipErrorInvalidValue;
             counter = geom.counters + (geom.counter_next.fetch_add(1) % LaunchGeom::N_COUNTERS) * LaunchGeom::COUNTER_STRIDE;
         }
-        void *args[] = {&coded, &pitch, &n, &pl, &dst, &status, &in_bases, &out_bases, &poly, &marker, &counter};
+        void *args[] = {&coded, &pitch, &n, &pl, &dst, &status, &in_bases, &out_bases, &poly, &marker, &counter, &info};
         (void)hipGetLastError();  // only this launch's status below
         return hipLaunchKernel(reinterpret_cast<const void *>(DEC_SWEEP), dim3(grid), dim3(WG), args, SWEEP_LDS, stream);
     }
     constexpr uint32_t U = DEC_UNIT;
     (void)hipGetLastError();  // only this launch's status below
-    hipLaunchKernelGGL(rlnc_decode_kernel<U>, dim3((uint32_t)(n * (TILES<DECDS_DEC_DW> / U))), dim3(WG), LDS_BYTES, stream, coded,
-                       pitch, n, pl, dst, status, in_bases, out_bases, poly, marker);
+    hipLaunchKernelGGL(rlnc_decode_kernel<U>, dim3((uint32_t)(n * (TILES<DECDS_DEC_DW> / U))), dim3(WG), DEC_LDS, stream, coded,
+                       pitch, n, pl, dst, status, in_bases, out_bases, poly, marker, info);
+    return hipGetLastError();
+}
+
+hipError_t launch_decode(const LaunchGeom &geom, const uint8_t *coded, size_t pitch, size_t n, const uint8_t *plan,
+                         uint8_t *dst, int32_t *status, const uint64_t *in_bases, const uint64_t *out_bases,
+                         uint32_t poly, uint32_t marker, uint8_t *info, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    uint32_t *inf = reinterpret_cast<uint32_t *>(info);
+    hipError_t e = launch_decode_kernel(geom, coded, pitch, n, plan, dst, status, in_bases, out_bases, poly, marker, inf, stream);
+    if (e != hipSuccess) return e;
+    // get_decoded_data's cut for the chunksets whose tail bytes hold no marker (rlnc_tail_scan_kernel)
+    hipLaunchKernelGGL(rlnc_tail_scan_kernel, dim3((uint32_t)n), dim3(WG), 0, stream, n, dst, status, out_bases, inf, marker);
     return hipGetLastError();
 }
 

@@ -116,12 +116,27 @@ int decds_repair_plan_batch(decds_ctx *ctx, const uint8_t *coded, size_t coded_p
                             size_t n_chunksets, const uint8_t *cand, uint8_t *plan,
                             int8_t *verdicts, int32_t *status, void *stream);
 
+/* What rlnc's Decoder::get_decoded_data returns for one chunkset (chunkset.rs:202-204): the 10
+ * decoded pieces concatenated (CS + 10 bytes) cut at the LAST boundary marker. An intact chunkset
+ * (any set of validated chunks) ends in marker || 9 zeros, so decoded_len == DECDS_CHUNKSET_BYTES;
+ * rows accepted unvalidated (add_chunk_unvalidated) can move the cut: below CS (the vector is the
+ * first decoded_len bytes of dst) or up to CS + 9 (dst's CS bytes, then tail[0 .. decoded_len - CS)).
+ * No marker anywhere is DECDS_ERR_CHUNKSET_REPAIRING_FAILED. */
+typedef struct decds_repair_info {
+    uint32_t decoded_len;  /* length of get_decoded_data's vector, <= DECDS_DECODED_MAX_BYTES */
+    uint8_t tail[10];      /* decoded bytes [CS, CS + 10): marker || zeros when intact */
+    uint8_t reserved[2];
+} decds_repair_info;
+#define DECDS_DECODED_MAX_BYTES (DECDS_CHUNKSET_BYTES + DECDS_NUM_ORIGINAL_CHUNKS - 1ull)
+
 /* Replaces RepairingChunkSet::repair -> Decoder::get_decoded_data (chunkset.rs:200-208):
- * dst = n x DECDS_CHUNKSET_BYTES; chunksets whose status is not DECDS_OK are skipped; a decoded
- * tail that is not marker || zeros sets DECDS_ERR_CHUNKSET_REPAIRING_FAILED. */
+ * dst = n x DECDS_CHUNKSET_BYTES (the first CS decoded bytes of chunkset c at dst + c*CS);
+ * chunksets whose status is not DECDS_OK are skipped. info (n x decds_repair_info, 4-byte aligned,
+ * or NULL) receives each decoded chunkset's cut; status becomes DECDS_ERR_CHUNKSET_REPAIRING_FAILED
+ * when the decoded data holds no marker. */
 int decds_decode_batch(decds_ctx *ctx, const uint8_t *coded, size_t coded_pitch,
                        size_t n_chunksets, const uint8_t *plan, uint8_t *dst, int32_t *status,
-                       void *stream);
+                       decds_repair_info *info, void *stream);
 
 /* name of the gfx950 kernel decds_decode_batch launches for n chunksets (for profiles and traces):
  * rlnc_decode_sweep_kernel from DECDS_DEC_SWEEP_MIN_N chunksets on (environment variable, read per
@@ -132,7 +147,7 @@ const char *decds_decode_kernel_name(size_t n_chunksets);
  * blob.rs:373-394, 451-473, for candidates already resident on the device) */
 int decds_repair_batch(decds_ctx *ctx, const uint8_t *coded, size_t coded_pitch,
                        size_t n_chunksets, const uint8_t *cand, uint8_t *plan, int8_t *verdicts,
-                       uint8_t *dst, int32_t *status, void *stream);
+                       uint8_t *dst, int32_t *status, decds_repair_info *info, void *stream);
 
 /* Counter-based SplitMix64 byte stream (seeded, reproducible on host and device) for synthetic
  * blobs and coding vectors; byte p = byte (p%8) of mix64(seed + (p/8 + 1) * 0x9E3779B97F4A7C15). */
@@ -192,9 +207,13 @@ int decds_repairing_chunkset_add_chunk_unvalidated(decds_repairing_chunkset *rcs
                                                    size_t len);
 /* RepairingChunkSet::is_ready_to_repair (chunkset.rs:187-189) */
 int decds_repairing_chunkset_is_ready_to_repair(const decds_repairing_chunkset *rcs);
-/* RepairingChunkSet::repair (chunkset.rs:200-208): out receives 10 MiB. Consumes the decoder
- * state on success (a second call returns DECDS_ERR_CHUNKSET_ALREADY_REPAIRED). */
-int decds_repairing_chunkset_repair(decds_repairing_chunkset *rcs, uint8_t *out, size_t out_len);
+/* RepairingChunkSet::repair (chunkset.rs:200-208): out receives get_decoded_data's vector, *out_len
+ * its length — 10 MiB for any validated chunk set; rows accepted unvalidated can move rlnc's cut at
+ * the last boundary marker (decds_repair_info), up to DECDS_DECODED_MAX_BYTES. No marker ->
+ * DECDS_ERR_CHUNKSET_REPAIRING_FAILED. out_cap below the decoded length -> DECDS_ERR_INVALID_ARGUMENT
+ * with *out_len set and the decoder kept. Consumes the decoder state on success (a second call
+ * returns DECDS_ERR_CHUNKSET_ALREADY_REPAIRED). */
+int decds_repairing_chunkset_repair(decds_repairing_chunkset *rcs, uint8_t *out, size_t out_cap, size_t *out_len);
 void decds_repairing_chunkset_free(decds_repairing_chunkset *rcs);
 
 /* ---- blob-level batching (decds-lib/src/blob.rs), host buffers ----------------------------- */

@@ -14,7 +14,7 @@
  *   - repair as rlnc's outcome, computed directly: the incremental rank test over the candidates'
  *     coding vectors in arrival order (chunkset.rs:173-184), the inverse of the accepted 10x10
  *     block, then one blocked pass piece_i = sum_k inv[i][k] * payload_k over the accepted rows,
- *     with the marker || zeros tail check of get_decoded_data (chunkset.rs:200-208);
+ *     cut at the last boundary marker as get_decoded_data (chunkset.rs:200-208);
  *   - chunkset-parallel over POSIX threads, as Blob::new's rayon loop (blob.rs:256-264).
  */
 #include <immintrin.h>
@@ -109,27 +109,13 @@ static void fast_encode_chunkset(const uint8_t *data, size_t have, const uint8_t
     }
 }
 
-/* RepairingChunkSet add_chunk_unvalidated x candidates + repair (chunkset.rs:173-208), keep = real size */
-static int fast_repair_chunkset(const uint8_t *coded, const uint8_t *cand, uint8_t *out, size_t keep, uint32_t poly,
-                                uint8_t marker) {
-    uint8_t basis[ORC_K * ORC_K], piv[ORC_K], sel[ORC_K], m[ORC_K * ORC_K], inv[ORC_K * ORC_K];
-    size_t rank = 0;
-    for (unsigned a = 0; a < ORC_N && rank < ORC_K; a++) {
-        const uint8_t r = cand[a];
-        if (r >= ORC_N) break;
-        const size_t before = rank;
-        if (orc_rank_push(basis, piv, &rank, coded + (size_t)r * ORC_F, ORC_K, poly) && rank > before)
-            sel[before] = r;
-    }
-    if (rank < ORC_K) return ORC_ERR_NOT_ALL_PIECES_RECEIVED;
-    for (unsigned k = 0; k < ORC_K; k++) memcpy(m + k * ORC_K, coded + (size_t)sel[k] * ORC_F, ORC_K);
-    if (orc_matrix_inverse(m, inv, ORC_K, poly)) return ORC_ERR_NOT_ALL_PIECES_RECEIVED;
-    mat512 A[ORC_K * ORC_K];
-    broadcast_matrices(A, inv, ORC_K * ORC_K, poly);
+/* the blocked pass piece_i = sum_k inv[i][k] * payload_k over the accepted rows: decoded bytes below
+ * `keep` into out, the 10 bytes past the chunkset ([CS, CS + 10): marker || zeros when intact) into tail */
+static void fast_decode_pass(const uint8_t *coded, const uint8_t *sel, const mat512 *A, uint8_t *out, size_t keep,
+                             uint8_t tail[ORC_K]) {
     const uint8_t *in[ORC_K];
     uint8_t *o[ORC_K];
     uint8_t tin[ORC_K][BLK], tout[ORC_K][BLK];
-    int ok = 1;
     for (size_t c = 0; c < ORC_L; c += BLK) {
         const int full = c + BLK <= ORC_L;
         for (unsigned k = 0; k < ORC_K; k++) {
@@ -152,10 +138,53 @@ static int fast_repair_chunkset(const uint8_t *coded, const uint8_t *cand, uint8
                 if (p < keep)
                     out[p] = tout[i][b];
                 else if (p >= ORC_CS)
-                    ok &= tout[i][b] == (p == ORC_CS ? marker : 0u);
+                    tail[p - ORC_CS] = tout[i][b];
             }
     }
-    return ok ? ORC_OK : ORC_ERR_INVALID_DECODED_DATA;
+}
+
+/* RepairingChunkSet add_chunk_unvalidated x candidates + repair (chunkset.rs:173-208), keep = real size.
+ * get_decoded_data's cut at the last boundary marker as orc_decoder_get_decoded_data: *cut = decoded
+ * length; out holds its first min(cut, keep) bytes and zeros up to keep (the blob paths' layout). */
+static int fast_repair_chunkset(const uint8_t *coded, const uint8_t *cand, uint8_t *out, size_t keep, uint32_t poly,
+                                uint8_t marker, size_t *cut) {
+    uint8_t basis[ORC_K * ORC_K], piv[ORC_K], sel[ORC_K], m[ORC_K * ORC_K], inv[ORC_K * ORC_K], tail[ORC_K];
+    size_t rank = 0;
+    for (unsigned a = 0; a < ORC_N && rank < ORC_K; a++) {
+        const uint8_t r = cand[a];
+        if (r >= ORC_N) break;
+        const size_t before = rank;
+        if (orc_rank_push(basis, piv, &rank, coded + (size_t)r * ORC_F, ORC_K, poly) && rank > before)
+            sel[before] = r;
+    }
+    if (rank < ORC_K) return ORC_ERR_NOT_ALL_PIECES_RECEIVED;
+    for (unsigned k = 0; k < ORC_K; k++) memcpy(m + k * ORC_K, coded + (size_t)sel[k] * ORC_F, ORC_K);
+    if (orc_matrix_inverse(m, inv, ORC_K, poly)) return ORC_ERR_NOT_ALL_PIECES_RECEIVED;
+    mat512 A[ORC_K * ORC_K];
+    broadcast_matrices(A, inv, ORC_K * ORC_K, poly);
+    fast_decode_pass(coded, sel, A, out, keep, tail);
+    size_t len = 0;
+    for (unsigned j = ORC_K; j-- > 0;)
+        if (tail[j] == marker) {
+            len = ORC_CS + j;
+            break;
+        }
+    if (!len) { /* no marker past the chunkset (corrupted rows only): search the decoded chunkset */
+        uint8_t *full = (uint8_t *)malloc(ORC_CS);
+        if (!full) return ORC_ERR_ARGS;
+        fast_decode_pass(coded, sel, A, full, ORC_CS, tail);
+        size_t p = ORC_CS;
+        while (p > 0 && full[p - 1] != marker) p--;
+        free(full);
+        if (p == 0) { /* an error gets no data (as the blob drivers leave it) */
+            memset(out, 0, keep);
+            return ORC_ERR_INVALID_DECODED_DATA;
+        }
+        len = p - 1;
+    }
+    if (len < keep) memset(out + len, 0, keep - len);
+    if (cut) *cut = len;
+    return ORC_OK;
 }
 
 struct fast_job {
@@ -191,7 +220,7 @@ static void *fast_repair_worker(void *arg) {
         const size_t off = c * (size_t)ORC_CS;
         const size_t keep = j->blob_len - off < ORC_CS ? j->blob_len - off : ORC_CS;
         j->status[c] = fast_repair_chunkset(j->coded + c * (size_t)ORC_N * ORC_F, j->cand + c * ORC_N,
-                                            j->out + off, keep, j->poly, j->marker);
+                                            j->out + off, keep, j->poly, j->marker, NULL);
     }
     return NULL;
 }

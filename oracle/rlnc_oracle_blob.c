@@ -5,8 +5,8 @@
  *   orc_blob_encode  follows decds-lib/src/blob.rs:244-264 (zero-pad to a multiple of CS, then
  *                    ChunkSet::new per chunkset on a thread pool — rayon's into_par_iter there).
  *   orc_blob_repair  follows blob.rs:373-394 + 451-473 and chunkset.rs:173-208: feed candidate
- *                    chunks in arrival order to a per-chunkset decoder, stop at rank k, extract,
- *                    truncate to the chunkset's real size.
+ *                    chunks in arrival order to a per-chunkset decoder, stop at rank k, extract
+ *                    (cut at the last boundary marker), truncate to the chunkset's real size.
  */
 #include <pthread.h>
 #include <stdatomic.h>
@@ -92,12 +92,13 @@ static void *repair_worker(void *arg) {
         size_t len = 0;
         int st = orc_decoder_is_decoded(d) ? orc_decoder_get_decoded_data(d, tmp, (size_t)ORC_K * ORC_L, &len)
                                            : ORC_ERR_NOT_ALL_PIECES_RECEIVED;
-        if (st == ORC_OK && len != ORC_CS) st = ORC_ERR_INVALID_DECODED_DATA;
         if (st == ORC_OK) {
-            /* blob.rs:464 truncates to the chunkset's real size (blob.rs:84-94) */
+            /* blob.rs:464 truncates get_decoded_data's vector to the chunkset's real size (blob.rs:84-94);
+             * a vector cut short (rows accepted unvalidated) leaves zeros up to it in this contiguous layout */
             size_t off = c * (size_t)ORC_CS, keep = j->blob_len - off;
             if (keep > ORC_CS) keep = ORC_CS;
-            memcpy(j->out + off, tmp, keep);
+            memcpy(j->out + off, tmp, len < keep ? len : keep);
+            if (len < keep) memset(j->out + off + len, 0, keep - len);
         }
         j->status[c] = st;
         orc_decoder_free(d);

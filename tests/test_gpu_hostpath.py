@@ -22,19 +22,20 @@ def _as(buf, src):
     return buf
 
 
-def _cand_with_failures(coded, n, rng, not_ready, broken):
-    """random arrival orders; chunkset `not_ready` gets 9 candidates; chunkset `broken` gets one accepted
-    row corrupted in its last byte so piece 9's tail no longer decodes to marker || zeros"""
+def _cand_with_failures(coded, coeffs, n, rng, not_ready, broken, short):
+    """random arrival orders; chunkset `not_ready` gets 9 candidates; chunksets `broken` and `short`
+    get piece 9's boundary marker flipped in every row (row r's payload byte changes by c[r][9] * 0x81:
+    linearity), so rlnc's get_decoded_data cuts at the last marker inside the data — none in
+    `broken`'s data (the caller removed them): ChunksetRepairingFailed"""
     cand = np.full((n, N), 0xFF, np.uint8)
     for c in range(n):
         cand[c, :] = rng.permutation(N)
     cand[not_ready, 9:] = 0xFF
-    sel = [int(x) for x in cand[broken, :K]]  # independent with overwhelming probability: checked below
-    inv = o.matrix_inverse(coded[[broken * N + r for r in sel], :K])
-    assert inv is not None
-    k = next(k for k in range(K) if inv[9, k])
     coded = coded.copy()
-    coded[broken * N + sel[k], F - 1] ^= 0x5A
+    cv = np.asarray(coeffs, np.uint8).reshape(n, N, K)
+    for c in (broken, short):
+        for r in range(N):
+            coded[c * N + r, F - K] ^= o.gf_mul(int(cv[c, r, 9]), o.MARKER)
     return cand, coded
 
 
@@ -44,7 +45,9 @@ def test_blob_host_paths_reuse_every_slot(ctx, batch, pinned):
     # unready chunkset (4) and the repair-failed one (5) sit in reused slots; last chunkset ragged
     n = 7
     blob_len = (n - 1) * CS + 12345
-    blob = o.fill_random(0xA5A5 + batch, blob_len)
+    blob = o.fill_random(0xA5A5 + batch, blob_len).copy()
+    part = blob[5 * CS:6 * CS]
+    part[part == o.MARKER] ^= 1  # chunkset 5 holds no marker byte
     coeffs = o.fill_random(0xC5C5 + batch, n * N * K)
     hb = []
     if pinned:  # registered caller memory: DMA'd directly
@@ -54,15 +57,23 @@ def test_blob_host_paths_reuse_every_slot(ctx, batch, pinned):
         blob_in, coded_out, rep_out = blob, None, None
     coded = codec.blob_encode_host(ctx, blob_in, coeffs, batch=batch, out=coded_out)
     assert np.array_equal(coded, o.blob_encode(blob, coeffs, nthreads=8))
-    cand, coded_bad = _cand_with_failures(coded, n, np.random.default_rng(batch), not_ready=4, broken=5)
+    cand, coded_bad = _cand_with_failures(coded, coeffs, n, np.random.default_rng(batch), not_ready=4, broken=5,
+                                          short=2)
+    ref_out, ref_st = o.blob_repair(coded_bad, cand, blob_len, nthreads=8)
     if pinned:
         coded_bad = _as(coded_out, coded_bad)
     out, status = codec.blob_repair_host(ctx, coded_bad, cand, blob_len, batch=batch, out=rep_out)
     assert status.tolist() == [0, 0, 0, 0, 5, 6, 0]
+    assert ref_st.tolist() == [o.OK, o.OK, o.OK, o.OK, o.NOT_ALL, o.INVALID_DATA, o.OK]
+    cut = int(np.nonzero(blob[2 * CS:3 * CS] == o.MARKER)[0][-1])
     for c in range(n):
         lo, hi = c * CS, min(blob_len, (c + 1) * CS)
         if status[c] == 0:
-            assert np.array_equal(out[lo:hi], blob[lo:hi]), c
+            assert np.array_equal(out[lo:hi], ref_out[lo:hi]), c
+            want = blob[lo:hi].copy()
+            if c == 2:
+                want[cut:] = 0  # cut at the last marker of the data, zeros past it
+            assert np.array_equal(out[lo:hi], want), c
         else:
             assert not out[lo:hi].any(), c  # no data for a chunkset that could not be repaired
     for b in hb:

@@ -278,29 +278,120 @@ def test_repair_plan_fuzz_low_rank_and_repeats(ctx):
     assert len(ranks) >= 8  # the draws cover most ranks
 
 
+MARKER = 0x81
+
+
+def _tail_cases():
+    """Chunksets whose decoded data (the 10 pieces concatenated, CS + 10 bytes) ends other than in
+    marker || 9 zeros — reachable through the public add_chunk_unvalidated (lib.rs:138,
+    chunkset.rs:173-184). rlnc's get_decoded_data cuts at the LAST marker (oracle/rlnc_oracle.c
+    orc_decoder_get_decoded_data). Each case: (name, data, {tail position: xor value})."""
+    rng = np.random.default_rng(0x7A11)
+    cases = []
+    d = o.fill_random(41, CS)
+    cases.append(("padding byte flipped", d, {3: 0x5A}))             # cut stays at CS
+    cases.append(("padding byte set to the marker", o.fill_random(42, CS), {6: MARKER}))  # cut at CS + 6
+    cases.append(("marker flipped", o.fill_random(43, CS), {0: MARKER}))  # cut at the data's last marker
+    d = o.fill_random(44, CS).copy()
+    p0 = CS - 3 * 4096 - 77                                          # marker moved earlier
+    d[p0 + 1:][d[p0 + 1:] == MARKER] ^= 1
+    d[p0] = MARKER
+    cases.append(("marker moved earlier", d, {0: MARKER, 1: 0x33}))
+    d = o.fill_random(45, CS).copy()
+    d[d == MARKER] ^= 1                                              # no marker anywhere: an error
+    cases.append(("no marker anywhere", d, {0: MARKER}))
+    d = np.zeros(CS, np.uint8)
+    d[:4 << 20] = o.fill_random(46, 4 << 20)                         # a blob's zero-padded last chunkset
+    cases.append(("zero-padded chunkset, marker flipped", d, {0: MARKER}))
+    cases.append(("intact", o.fill_random(47, CS), {}))
+    cases.append(("several tail markers", o.fill_random(48, CS), {2: MARKER, 9: MARKER, 4: 7}))
+    return cases, rng
+
+
+def _corrupt_tail(coded, coeffs, flips):
+    """coded rows of the padded pieces with piece 9's tail byte j (decoded position CS + j) xor'ed
+    by v: multiplication by a coefficient is linear, so row r's payload byte changes by c[r][9] * v"""
+    coded = coded.copy()
+    for j, v in flips.items():
+        col = K + L - K + j
+        for r in range(N):
+            coded[r, col] ^= o.gf_mul(int(coeffs[r, 9]), v)
+    return coded
+
+
 @pytest.mark.usefixtures("decode_form")
-def test_decode_tail_corruption_is_repairing_failed(ctx):
-    data = o.fill_random(41, CS)
-    coeffs = o.fill_random(42, N * K)
-    src, cv = dev(data), dev(coeffs)
-    coded_d = torch.empty(N * F, dtype=torch.uint8, device="cuda")
-    codec.encode_batch(ctx, src, 1, cv, coded_d)
-    coded = host(coded_d).reshape(N, F).copy()
-    sel = list(range(K))
-    inv = o.matrix_inverse(coded[sel, :K])
-    assert inv is not None
-    t = o.mul_table()
-    # flip the last payload byte of row k where inv[9][k] != 0: piece 9's padding stops being zero
-    k = next(k for k in range(K) if inv[9, k])
-    coded[k, F - 1] ^= 0x5A
-    cand = np.array(sel + [0xFF] * 6, np.uint8)
-    plan = torch.empty(128, dtype=torch.uint8, device="cuda")
-    verd = torch.empty(N, dtype=torch.int8, device="cuda")
-    status = torch.empty(1, dtype=torch.int32, device="cuda")
-    out = torch.zeros(CS, dtype=torch.uint8, device="cuda")
-    codec.repair_batch(ctx, dev(coded.reshape(-1)), 1, dev(cand), plan, verd, out, status)
-    assert host(status)[0] == 6
-    assert int(t[inv[9, k], 0x5A]) != 0
+def test_decoded_data_cut_at_last_marker_matches_oracle(ctx):
+    """get_decoded_data (chunkset.rs:200-208) on corrupted tails: the device batch decode (status,
+    repair info, bytes), the chunkset mirror (add_chunk_unvalidated + repair), the host blob path and
+    both CPU restatements (scalar decoder, blocked GFNI) give the same status and the same bytes."""
+    cases, rng = _tail_cases()
+    n = len(cases)
+    data = np.concatenate([c[1] for c in cases])
+    coeffs = o.fill_random(0xC0EF7A11, n * N * K).reshape(n, N, K)
+    coded_d = torch.empty(n * N * F, dtype=torch.uint8, device="cuda")
+    codec.encode_batch(ctx, dev(data), n, dev(coeffs), coded_d)
+    coded = host(coded_d).reshape(n, N, F)
+    coded = np.stack([_corrupt_tail(coded[c], coeffs[c], cases[c][2]) for c in range(n)])
+    cand = np.full((n, N), 0xFF, np.uint8)
+    for c in range(n):
+        m = 10 if c % 2 else N
+        cand[c, :m] = rng.permutation(N)[:m]
+    plan = torch.empty(n * 128, dtype=torch.uint8, device="cuda")
+    verd = torch.empty(n * N, dtype=torch.int8, device="cuda")
+    status = torch.full((n,), -7, dtype=torch.int32, device="cuda")
+    info = torch.zeros(n * codec.REPAIR_INFO_BYTES, dtype=torch.uint8, device="cuda")
+    out = torch.zeros(n * CS, dtype=torch.uint8, device="cuda")
+    codec.repair_batch(ctx, dev(coded.reshape(-1)), n, dev(cand), plan, verd, out, status, info=info)
+    st, res = host(status), host(out)
+    lens, tails = codec.repair_info(info, n)
+    fast_out, fast_st = (o.fast_blob_repair(coded.reshape(n * N, F), cand, n * CS, nthreads=8)
+                         if o.fast_supported() else (None, None))
+    blob_out, blob_st = o.blob_repair(coded.reshape(n * N, F), cand, n * CS, nthreads=8)
+    host_out, host_st = codec.blob_repair_host(ctx, coded.reshape(n * N, F), cand, n * CS)
+    seen = set()
+    for c, (name, d, flips) in enumerate(cases):
+        dec = o.Decoder()
+        for r in cand[c]:
+            if r == 0xFF or dec.is_already_decoded():
+                break
+            dec.decode(coded[c, r])
+        assert dec.is_already_decoded(), name
+        ost, obytes = dec.get_decoded_data()
+        # the mirror: add_chunk_unvalidated in arrival order, then repair()
+        rcs = decds_amd.RepairingChunkSet(ctx, c)
+        for r in cand[c]:
+            if r == 0xFF or rcs.is_ready_to_repair():
+                break
+            try:
+                rcs.add_chunk_unvalidated(decds_amd.Chunk(c, c * N + int(r), coded[c, r].tobytes()))
+            except decds_amd.DecdsError as e:
+                assert e.kind == "ChunkDecodingFailed"
+        sl = slice(c * CS, (c + 1) * CS)
+        if ost == o.INVALID_DATA:
+            seen.add("error")
+            assert st[c] == 6, name
+            with pytest.raises(decds_amd.DecdsError) as e:
+                rcs.repair()
+            assert e.value.kind == "ChunksetRepairingFailed", name
+            assert blob_st[c] == o.INVALID_DATA and host_st[c] == 6, name
+            assert fast_st is None or fast_st[c] == o.INVALID_DATA, name
+            continue
+        assert ost == o.OK and st[c] == 0, (name, ost, st[c])
+        ln = len(obytes)
+        seen.add("short" if ln < CS else "long" if ln > CS else "cs")
+        assert lens[c] == ln, (name, lens[c], ln)
+        assert codec.decoded_bytes(res[sl], lens[c], tails[c]) == obytes.tobytes(), name
+        assert rcs.repair() == obytes.tobytes(), name
+        # blob layout: the vector truncated to the chunkset (blob.rs:464), zeros past a short cut
+        want = np.zeros(CS, np.uint8)
+        want[:min(ln, CS)] = obytes[:CS]
+        assert blob_st[c] == o.OK and np.array_equal(blob_out[sl], want), name
+        assert host_st[c] == 0 and np.array_equal(host_out[sl], want), name
+        if fast_st is not None:
+            assert fast_st[c] == o.OK and np.array_equal(fast_out[sl], want), name
+        if not flips:
+            assert ln == CS and np.array_equal(res[sl], d), name
+    assert seen == {"error", "short", "long", "cs"}
 
 
 @pytest.mark.usefixtures("decode_form")

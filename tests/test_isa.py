@@ -109,3 +109,47 @@ def test_checker_flags_an_early_read():
             "s_waitcnt vmcnt(1)", "v_mov_b32_e32 v12, v7"]
     ranged = ["global_atomic_add v7, v[0:1], v2, off sc0", "scratch_store_dwordx2 off, v[6:7], off offset:4"]
     assert _unsafe_uses(early) and not _unsafe_uses(late) and _unsafe_uses(ranged)
+
+
+def _kernel_notes(tmp_path):
+    """{kernel symbol: {metadata key: value}} from the gfx950 code objects' AMDGPU notes"""
+    from decds_amd import build
+
+    lib = os.environ.get("DECDS_LIB") or build.build(verbose=False)
+    work = tmp_path / "notes"
+    work.mkdir()
+    shutil.copy(lib, work / "lib.so")
+    subprocess.run([OBJDUMP, "--offloading", "lib.so"], cwd=work, check=True, capture_output=True)
+    readelf = os.path.join(os.path.dirname(OBJDUMP), "llvm-readelf")
+    kernels = {}
+    for f in sorted(os.listdir(work)):
+        if "amdgcn" not in f or "gfx950" not in f:
+            continue
+        r = subprocess.run([readelf, "--notes", f], cwd=work, check=True, capture_output=True, text=True)
+        entry = None
+        for line in r.stdout.splitlines():
+            if re.match(r"^  - \.", line):  # a kernel entry of amdhsa.kernels starts (its keys sorted)
+                entry = {}
+            m = re.match(r"^  [- ] \.(\w+):\s+(\S+)", line)  # the entry's own keys, not its args'
+            if entry is not None and m:
+                entry[m.group(1)] = m.group(2)
+                if m.group(1) == "name":
+                    kernels[m.group(2)] = entry
+    return kernels
+
+
+def test_table_kernels_have_no_static_lds(tmp_path):
+    # The streaming kernels' lookups are inline-asm ds_read_b128 with absolute LDS offsets: their
+    # tables must start at LDS address 0, i.e. the dynamic area must come first. A static __shared__
+    # variable in such a kernel is placed before the dynamic area and shifts every table (round 4's
+    # first TailLds build did that: repaired bytes wrong). Their group segment must be 0.
+    if not os.path.exists(OBJDUMP):
+        pytest.skip("llvm-objdump not in this image")
+    notes = _kernel_notes(tmp_path)
+    table = {k: v for k, v in notes.items()
+             if any(s in k for s in ("encode_sweep_kernel", "decode_sweep_kernel", "rlnc_decode_kernel",
+                                     "encode_hash_kernel"))}
+    assert len(table) >= 5, sorted(notes)
+    for name, md in table.items():
+        assert md.get("group_segment_fixed_size") == "0", (name, md.get("group_segment_fixed_size"))
+        assert md.get("private_segment_fixed_size") == "0", (name, "spills to scratch")

@@ -233,3 +233,52 @@ def test_gf_affine_matrix_is_multiplication():
                 row = (a >> (8 * (7 - i))) & 0xFF
                 y |= (bin(row & x).count("1") & 1) << i
             assert y == t[c, x]
+
+
+def test_decoded_data_cut_at_last_marker_restatements_agree():
+    # rlnc get_decoded_data (chunkset.rs:200-208) cuts the decoded pieces at the LAST boundary marker:
+    # the scalar decoder, the scalar blob driver and the blocked GFNI codec agree on corrupted tails
+    # (rows accepted unvalidated): padding flipped (cut stays at CS), padding turned into the marker
+    # (cut past CS, truncated to the chunkset), marker flipped (cut inside the data; in a blob's last,
+    # zero-padded chunkset below its real size: zeros past the cut) and no marker at all (an error)
+    K, N, CS, L, M = o.K, o.N, o.CS, o.L, o.MARKER
+    d_nomark = o.fill_random(0x7A13, CS).copy()
+    d_nomark[d_nomark == M] ^= 1
+    d_last = np.zeros(CS, np.uint8)
+    d_last[:3 << 20] = o.fill_random(0x7A14, 3 << 20)
+    cases = [(o.fill_random(0x7A10, CS), {}), (o.fill_random(0x7A11, CS), {4: 0x5A}),
+             (o.fill_random(0x7A12, CS), {6: M}), (o.fill_random(0x7A15, CS), {0: M}),
+             (d_nomark, {0: M}), (d_last, {0: M})]
+    n = len(cases)
+    blob_len = (n - 1) * CS + (4 << 20)                   # the last chunkset holds 4 MiB of the blob
+    data = np.concatenate([c[0] for c in cases])
+    coeffs = o.fill_random(0x7A16, n * N * K).reshape(n, N, K)
+    coded = o.blob_encode(data, coeffs, nthreads=8).reshape(n, N, o.F)
+    for c, (_, flips) in enumerate(cases):               # piece 9's tail byte j changes by v (linearity)
+        for j, v in flips.items():
+            for r in range(N):
+                coded[c, r, K + L - K + j] ^= o.gf_mul(int(coeffs[c, r, 9]), v)
+    cand = np.tile(np.arange(N, dtype=np.uint8), (n, 1))
+    ref_out, ref_st = o.blob_repair(coded.reshape(n * N, o.F), cand, blob_len, nthreads=8)
+    if o.fast_supported():
+        out, st = o.fast_blob_repair(coded.reshape(n * N, o.F), cand, blob_len, nthreads=8)
+        assert np.array_equal(st, ref_st) and np.array_equal(out, ref_out)
+    lens = []
+    for c in range(n):
+        dec = o.Decoder()
+        for r in range(K):
+            assert dec.decode(coded[c, r]) == o.OK
+        st, got = dec.get_decoded_data()
+        assert st == ref_st[c]
+        if st != o.OK:
+            lens.append(None)
+            continue
+        lens.append(len(got))
+        keep = min(CS, blob_len - c * CS)
+        want = np.zeros(keep, np.uint8)
+        want[:min(len(got), keep)] = got[:keep]
+        assert np.array_equal(ref_out[c * CS:c * CS + keep], want), c
+    last = int(np.nonzero(cases[3][0] == M)[0][-1])
+    last5 = int(np.nonzero(d_last == M)[0][-1])
+    assert lens == [CS, CS, CS + 6, last, None, last5]
+    assert list(ref_st) == [o.OK] * 4 + [o.INVALID_DATA, o.OK]

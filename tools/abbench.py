@@ -79,7 +79,7 @@ def main():
         if ev:
             ev[2].record(st)
         assert L.decds_decode_batch(h, vp(coded.data_ptr()), p, n, vp(plan.data_ptr()), vp(out.data_ptr()),
-                                    vp(status.data_ptr()), sp) == 0
+                                    vp(status.data_ptr()), None, sp) == 0
         if ev:
             ev[3].record(st)
 

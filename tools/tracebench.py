@@ -77,7 +77,7 @@ def main():
         assert L.decds_repair_plan_batch(h, vp(coded.data_ptr()), F, n, vp(cand.data_ptr()), vp(plan.data_ptr()),
                                          vp(verd.data_ptr()), vp(status.data_ptr()), sp) == 0
         assert L.decds_decode_batch(h, vp(coded.data_ptr()), F, n, vp(plan.data_ptr()), vp(out.data_ptr()),
-                                    vp(status.data_ptr()), sp) == 0
+                                    vp(status.data_ptr()), None, sp) == 0
         st.synchronize()
         dec = np.zeros(2 * TRACE_WAVES, np.uint64)
         assert L.decds_debug_trace(1, dec.ctypes.data) == 0
