@@ -86,66 +86,103 @@ def cpu_threads():
     return max(1, min(16, avail))
 
 
-def cpu_baseline(n_sample, seed, repeats=3):
+def host_cpu():
+    """the host's CPU model and the CPU counts this process sees"""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = None
+    return {"model": model, "cpus_online": os.cpu_count(), "cpus_usable": affinity}
+
+
+def cpu_baseline(n_sample, seed, repeats=3, cfg2_chunksets=103):
     """The CPU restatement (oracle/, "port") on the host cores: chunkset-parallel encode
     (blob.rs:256-264) + per-chunkset repair from 10 survivors (chunkset.rs:173-208).
 
     Headline = the strongest restatement: column-blocked GFNI affine multiplies on AVX-512
     (oracle/rlnc_cpu_fast.c; coefficient-only rank + inverse, then one blocked pass for the repair),
-    the median of `repeats` runs with their spread. Beside it, one run each of the row-pass forms:
-    AVX2 nibble tables, and the scalar table-driven loop rlnc 0.4.0 is recalled to use. All produce
-    the same bytes (tests/test_oracle.py)."""
+    the median of `repeats` runs with their spread. Beside it (BASELINE.md's plan): the same codec on
+    1 thread, and on config 2's sample (the 1 GiB blob's 103 chunksets) with all threads; one run
+    each of the row-pass forms (AVX2 nibble tables; the scalar table-driven loop rlnc 0.4.0 is
+    recalled to use). All produce the same bytes (tests/test_oracle.py)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import numpy as np
     import oracle as o
     threads = cpu_threads()
     if n_sample <= 0:
         n_sample = 16 * threads
-    blob = o.fill_random(seed, n_sample * o.CS)
-    coeffs = o.fill_random(seed + 1, n_sample * o.N * o.K)
-    rng = np.random.default_rng(seed)
-    cand = np.full((n_sample, o.N), 0xFF, np.uint8)
-    for c in range(n_sample):
-        cand[c, :o.K] = rng.permutation(o.N)[:o.K]
-    gib = n_sample * o.CS / GIB
 
-    def run(enc, rep):
+    def sample(n, sd):
+        blob = o.fill_random(sd, n * o.CS)
+        coeffs = o.fill_random(sd + 1, n * o.N * o.K)
+        rng = np.random.default_rng(sd)
+        cand = np.full((n, o.N), 0xFF, np.uint8)
+        for c in range(n):
+            cand[c, :o.K] = rng.permutation(o.N)[:o.K]
+        return blob, coeffs, cand
+
+    def run(enc, rep, smp, nthreads):
+        blob, coeffs, cand = smp
+        n = cand.shape[0]
+        gib = n * o.CS / GIB
         t0 = time.perf_counter()
-        coded = enc(blob, coeffs, nthreads=threads)
+        coded = enc(blob, coeffs, nthreads=nthreads)
         t1 = time.perf_counter()
-        out, status = rep(coded, cand, blob.size, nthreads=threads)
+        out, status = rep(coded, cand, blob.size, nthreads=nthreads)
         t2 = time.perf_counter()
         ok = status == 0
-        assert np.array_equal(out.reshape(n_sample, o.CS)[ok], blob.reshape(n_sample, o.CS)[ok])
+        assert np.array_equal(out.reshape(n, o.CS)[ok], blob.reshape(n, o.CS)[ok])
         del coded, out
         # encode + repair GiB/s as the GPU's value: (blob bytes encoded + repaired) / 2 per second
         return {"value": gib / (t2 - t0), "encode_gib_s": gib / (t1 - t0), "repair_gib_s": gib / (t2 - t1)}
 
-    rows = {}
-    o.set_simd(0)
-    rows["scalar tables, row passes"] = run(o.blob_encode, o.blob_repair)
-    if o.set_simd(1):
-        rows["avx2 nibble tables, row passes"] = run(o.blob_encode, o.blob_repair)
-    o.set_simd(0)
-    head_name, head = None, None
-    if o.fast_supported():
-        head_name = "avx512 gfni affine, column-blocked"
-        runs = [run(o.fast_blob_encode, o.fast_blob_repair) for _ in range(max(1, repeats))]
+    rnd = lambda d: {k: (round(v, 2) if isinstance(v, float) else v) for k, v in d.items()}
+
+    def median(runs):
         med = lambda k: float(np.median([r[k] for r in runs]))
-        head = {"value": med("value"), "encode_gib_s": med("encode_gib_s"), "repair_gib_s": med("repair_gib_s"),
+        return {"value": med("value"), "encode_gib_s": med("encode_gib_s"), "repair_gib_s": med("repair_gib_s"),
                 "runs": len(runs), "spread": [round(min(r["value"] for r in runs), 2),
                                               round(max(r["value"] for r in runs), 2)]}
+
+    smp = sample(n_sample, seed)
+    rows = {}
+    o.set_simd(0)
+    rows["scalar tables, row passes"] = run(o.blob_encode, o.blob_repair, smp, threads)
+    if o.set_simd(1):
+        rows["avx2 nibble tables, row passes"] = run(o.blob_encode, o.blob_repair, smp, threads)
+    o.set_simd(0)
+    extra = {}
+    if o.fast_supported():
+        head_name = "avx512 gfni affine, column-blocked"
+        head = median([run(o.fast_blob_encode, o.fast_blob_repair, smp, threads) for _ in range(max(1, repeats))])
+        del smp
+        smp2 = sample(cfg2_chunksets, seed + 2)
+        cfg2_tag = " (config 2: the 1 GiB blob)" if cfg2_chunksets == 103 else ""
+        extra["threads_1"] = dict(rnd(run(o.fast_blob_encode, o.fast_blob_repair, smp2, 1)), cores=1,
+                                  sample="%d chunksets%s, 1 thread" % (cfg2_chunksets, cfg2_tag))
+        extra["cfg2"] = dict(rnd(median([run(o.fast_blob_encode, o.fast_blob_repair, smp2, threads)
+                                         for _ in range(max(1, repeats))])), cores=threads,
+                             sample="%d chunksets%s, %d threads" % (cfg2_chunksets, cfg2_tag, threads))
+        del smp2
     else:
         head_name = max(rows, key=lambda k: rows[k]["value"])
         head = dict(rows[head_name], runs=1, spread=None)
-    rnd = lambda d: {k: (round(v, 2) if isinstance(v, float) else v) for k, v in d.items()}
-    return {"value": round(head["value"], 2), "unit": "GiB/s", "cores": threads, "kind": "port",
-            "variant": head_name, "median_of": head["runs"], "spread": head["spread"],
-            "sample": "%d chunksets (%.0f MiB) encode + repair from 10 survivors, %d threads (chunkset-parallel)"
-                      % (n_sample, n_sample * o.CS / 2 ** 20, threads),
-            "encode_gib_s": round(head["encode_gib_s"], 2), "repair_gib_s": round(head["repair_gib_s"], 2),
-            "other_variants": {k: rnd(v) for k, v in rows.items()}}
-
+    return dict({"value": round(head["value"], 2), "unit": "GiB/s", "cores": threads, "kind": "port",
+                 "variant": head_name, "median_of": head["runs"], "spread": head["spread"],
+                 "sample": "%d chunksets (%.0f MiB) encode + repair from 10 survivors, %d threads (chunkset-parallel)"
+                           % (n_sample, n_sample * o.CS / 2 ** 20, threads),
+                 "encode_gib_s": round(head["encode_gib_s"], 2), "repair_gib_s": round(head["repair_gib_s"], 2),
+                 "host": host_cpu(),
+                 "other_variants": {k: rnd(v) for k, v in rows.items()}}, **extra)
 
 def init_group(dist, backend, device, rank, world, timeout_s=300):
     """The process group for N > 1 (RCCL; DECDS_BENCH_BACKEND=gloo rehearses the path with ranks

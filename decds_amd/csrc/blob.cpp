@@ -60,9 +60,9 @@ struct Pipe {
         (void)drain();
         for (int i = 0; i < SLOTS; i++)
             for (hipEvent_t ev : {in_done[i], k_done[i], out_done[i]})
-                if (ev) (void)hipEventDestroy(ev);
+                if (ev) hip_tolerate(hipEventDestroy(ev), "hipEventDestroy");
         for (hipStream_t st : {h2d, comp, d2h})
-            if (st) (void)hipStreamDestroy(st);
+            if (st) hip_tolerate(hipStreamDestroy(st), "hipStreamDestroy");
     }
 };
 
@@ -186,7 +186,7 @@ int repair_range(decds_ctx *ctx, const uint8_t *coded_host, size_t n, const uint
     struct Pinned {
         void *p = nullptr;
         ~Pinned() {
-            if (p) (void)hipHostFree(p);
+            if (p) hip_tolerate(hipHostFree(p), "hipHostFree");
         }
     } pin;
     {
@@ -417,17 +417,17 @@ struct RbShard {
     uint64_t batch_bytes = 0;
 
     ~RbShard() {
-        if (ctx) (void)hipSetDevice(ctx->device);
-        if (s) (void)hipStreamSynchronize(s);
+        if (ctx) hip_tolerate(hipSetDevice(ctx->device), "hipSetDevice");
+        if (s) hip_tolerate(hipStreamSynchronize(s), "hipStreamSynchronize");
         in_ring.abandon();
         out_ring.abandon();
-        for (uint8_t *p : slabs) (void)hipFree(p);
-        for (uint8_t *p : areas) (void)hipFree(p);
+        for (uint8_t *p : slabs) hip_tolerate(hipFree(p), "hipFree");
+        for (uint8_t *p : areas) hip_tolerate(hipFree(p), "hipFree");
         for (uint8_t *p : hslabs) host_pinned_free(p, RB_SLAB_BYTES);
         for (uint8_t *p : {d_small, d_hdr, d_batch})
-            if (p) (void)hipFree(p);
-        if (h_small) (void)hipHostFree(h_small);
-        if (s) (void)hipStreamDestroy(s);
+            if (p) hip_tolerate(hipFree(p), "hipFree");
+        if (h_small) hip_tolerate(hipHostFree(h_small), "hipHostFree");
+        if (s) hip_tolerate(hipStreamDestroy(s), "hipStreamDestroy");
     }
     // device budget per context: a quarter for decode areas (at least one), the rest for row slots
     void set_budget(uint64_t bytes) {
@@ -449,11 +449,12 @@ struct RbShard {
         if (c.slot >= 0 || c.hslot >= 0) return DECDS_OK;
         if (free_slots.empty() && slabs.size() < max_slabs) {
             uint8_t *p = nullptr;
-            if (hipMalloc(reinterpret_cast<void **>(&p), RB_SLAB_BYTES) == hipSuccess) {
+            const hipError_t me = hipMalloc(reinterpret_cast<void **>(&p), RB_SLAB_BYTES);
+            if (me == hipSuccess) {
                 slabs.push_back(p);
                 for (size_t i = RB_SLAB_SLOTS; i-- > 0;) free_slots.push_back((int32_t)((slabs.size() - 1) * RB_SLAB_SLOTS + i));
-            } else {
-                (void)hipGetLastError();  // device memory ran out below the budget: spill from here on
+            } else {  // device memory ran out below the budget: spill from here on
+                hip_tolerate(me, "hipMalloc (RepairingBlob row slab; spilling to host memory)");
                 max_slabs = slabs.size();
             }
         }
@@ -496,12 +497,13 @@ struct RbShard {
         }
         if (areas.size() < max_areas) {
             uint8_t *p = nullptr;
-            if (hipMalloc(reinterpret_cast<void **>(&p), RB_AREA_BYTES) == hipSuccess) {
+            const hipError_t me = hipMalloc(reinterpret_cast<void **>(&p), RB_AREA_BYTES);
+            if (me == hipSuccess) {
                 areas.push_back(p);
                 area_owner.push_back(-1);
                 return (int32_t)(areas.size() - 1);
             }
-            (void)hipGetLastError();
+            hip_tolerate(me, "hipMalloc (RepairingBlob decode area; reusing the areas held)");
             max_areas = std::max<size_t>(1, areas.size());
             if (areas.empty()) {
                 *err = decds_set_error(DECDS_ERR_OUT_OF_DEVICE_MEMORY,
@@ -816,8 +818,8 @@ static uint64_t rb_default_budget(decds_ctx *const *ctxs, size_t n_ctx, size_t g
     // DECDS_RB_DEVICE_MB, else half the device's free memory shared by the shards on that device
     if (const char *env = getenv("DECDS_RB_DEVICE_MB")) return (uint64_t)strtoull(env, nullptr, 10) << 20;
     size_t fr = 0, total = 0;
-    if (hipMemGetInfo(&fr, &total) != hipSuccess) {
-        (void)hipGetLastError();
+    if (const hipError_t me = hipMemGetInfo(&fr, &total)) {
+        hip_tolerate(me, "hipMemGetInfo (RepairingBlob default budget: 4 GiB)");
         return (uint64_t)4 << 30;
     }
     size_t same = 0;
@@ -965,8 +967,8 @@ static int rb_add_rows_shard(decds_repairing_blob *rb, RbShard &sh, const std::v
     hipError_t e;
     if (!sh.d_batch || sh.batch_plen < proof_len) {
         if (sh.d_batch) {
-            (void)hipStreamSynchronize(sh.s);
-            (void)hipFree(sh.d_batch);
+            hip_tolerate(hipStreamSynchronize(sh.s), "hipStreamSynchronize");
+            hip_tolerate(hipFree(sh.d_batch), "hipFree");
             sh.d_batch = nullptr;
             sh.batch_bytes = 0;
         }

@@ -21,6 +21,28 @@ using namespace decds;
 
 static thread_local std::string g_last_error;
 static std::atomic<int> g_live_ctx{0};  // contexts created and not yet destroyed
+// hip_status.h: the library's last tolerated HIP failure on this thread, and whether the error being
+// reported was found pending before a launch (then it is an earlier call's, named by g_tolerated)
+static thread_local std::string g_tolerated;
+static thread_local std::string g_pending_before;
+
+namespace decds {
+void hip_tolerate(hipError_t e, const char *what) {
+    if (e == hipSuccess) return;
+    (void)hipGetLastError();  // consumed here: the failure is tolerated, never a later launch's
+    g_tolerated = std::string(what) + ": " + hipGetErrorString(e);
+}
+
+hipError_t hip_launch_begin(const char *kernel) {
+    const hipError_t p = hipPeekAtLastError();
+    if (p == hipSuccess) return hipSuccess;
+    (void)hipGetLastError();
+    g_pending_before = std::string("before launching ") + kernel + ", an error was left pending by an earlier HIP call on "
+                       "this thread (" + (g_tolerated.empty() ? "a call outside the library" :
+                                          "the library's last tolerated failure: " + g_tolerated) + ")";
+    return p;
+}
+}  // namespace decds
 
 int decds_set_error(int code, const char *fmt, ...) {
     char buf[512];
@@ -33,6 +55,11 @@ int decds_set_error(int code, const char *fmt, ...) {
 }
 
 int decds_hip_error(hipError_t e, const char *what) {
+    if (!g_pending_before.empty()) {  // not this call's failure (hip_launch_begin)
+        std::string note;
+        note.swap(g_pending_before);
+        return decds_set_error(DECDS_ERR_HIP, "%s: %s (%d) %s", what, hipGetErrorString(e), (int)e, note.c_str());
+    }
     return decds_set_error(DECDS_ERR_HIP, "%s: %s (%d)", what, hipGetErrorString(e), (int)e);
 }
 
@@ -44,7 +71,7 @@ int decds_ctx_bind(const decds_ctx *ctx) {
 
 hipError_t decds_ctx_scratch(decds_ctx *ctx, size_t bytes, uint8_t **out) {
     if (ctx->host_scratch_cap < bytes) {
-        if (ctx->host_scratch) (void)hipFree(ctx->host_scratch);
+        if (ctx->host_scratch) hip_tolerate(hipFree(ctx->host_scratch), "hipFree");
         ctx->host_scratch = nullptr;
         ctx->host_scratch_cap = 0;
         hipError_t e = hipMalloc(reinterpret_cast<void **>(&ctx->host_scratch), bytes);
@@ -116,6 +143,7 @@ int decds_ctx_create(int device, decds_ctx **out) {
     c->marker = (uint8_t)MARKER_DEFAULT;
     c->gen = host_gf_generator(POLY_DEFAULT);
     c->geom.num_cus = prop.multiProcessorCount;
+    configure_geom(c->geom);
     if ((e = hipMalloc(reinterpret_cast<void **>(&c->geom.counters),
                        LaunchGeom::N_COUNTERS * LaunchGeom::COUNTER_STRIDE * sizeof(uint32_t))) != hipSuccess) {
         delete c;
@@ -123,7 +151,7 @@ int decds_ctx_create(int device, decds_ctx **out) {
     }
     if ((e = hipMemset(c->geom.counters, 0, LaunchGeom::N_COUNTERS * LaunchGeom::COUNTER_STRIDE * sizeof(uint32_t))) !=
         hipSuccess) {
-        (void)hipFree(c->geom.counters);
+        hip_tolerate(hipFree(c->geom.counters), "hipFree");
         delete c;
         return decds_hip_error(e, "hipMemset (tile counters)");
     }
@@ -134,14 +162,14 @@ int decds_ctx_create(int device, decds_ctx **out) {
 
 int decds_ctx_destroy(decds_ctx *ctx) {
     if (!ctx) return DECDS_OK;
-    (void)hipSetDevice(ctx->device);
+    hip_tolerate(hipSetDevice(ctx->device), "hipSetDevice");
     decds_lanes_destroy(ctx);
-    if (ctx->host_scratch) (void)hipFree(ctx->host_scratch);
+    if (ctx->host_scratch) hip_tolerate(hipFree(ctx->host_scratch), "hipFree");
     // the last context out returns the cached page-locked blocks (no idle pinned memory)
     if (g_live_ctx.fetch_sub(1) == 1) (void)host_cache_trim();
     if (ctx->geom.counters) {
-        (void)hipDeviceSynchronize();  // no launch may still count on them
-        (void)hipFree(ctx->geom.counters);
+        hip_tolerate(hipDeviceSynchronize(), "hipDeviceSynchronize");  // no launch may still count on them
+        hip_tolerate(hipFree(ctx->geom.counters), "hipFree");
     }
     delete ctx;
     return DECDS_OK;
@@ -202,6 +230,10 @@ int decds_encode_batch(decds_ctx *ctx, const uint8_t *src, size_t n, const uint8
 
 const char *decds_encode_kernel_name(size_t n_chunksets) { return encode_kernel_name(n_chunksets); }
 const char *decds_decode_kernel_name(size_t n_chunksets) { return decode_kernel_name(n_chunksets); }
+uint64_t decds_set_decode_sweep_min_n(uint64_t n_chunksets) {
+    set_decode_sweep_min_n(n_chunksets);
+    return decode_sweep_min_n();
+}
 
 int decds_repair_plan_batch(decds_ctx *ctx, const uint8_t *coded, size_t coded_pitch, size_t n,
                             const uint8_t *cand, uint8_t *plan, int8_t *verdicts, int32_t *status,

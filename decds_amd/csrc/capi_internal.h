@@ -7,6 +7,7 @@
 #include <mutex>
 #include <vector>
 
+#include "hip_status.h"
 #include "host_mem.h"
 #include "rlnc_kernels.h"
 

@@ -48,12 +48,12 @@ struct Lane {
     uint8_t *h_big = nullptr;    // N*F page-locked staging (>= CS, >= K*F)
     uint8_t *h_small = nullptr;  // SM_BYTES page-locked
     ~Lane() {
-        if (s) (void)hipStreamSynchronize(s);
+        if (s) hip_tolerate(hipStreamSynchronize(s), "hipStreamSynchronize");
         for (uint8_t *p : {d_cs, d_coded, d_small})
-            if (p) (void)hipFree(p);
+            if (p) hip_tolerate(hipFree(p), "hipFree");
         host_pinned_free(h_big, N * F);
-        if (h_small) (void)hipHostFree(h_small);
-        if (s) (void)hipStreamDestroy(s);
+        if (h_small) hip_tolerate(hipHostFree(h_small), "hipHostFree");
+        if (s) hip_tolerate(hipStreamDestroy(s), "hipStreamDestroy");
     }
     hipError_t init() {
         hipError_t e;
@@ -213,18 +213,25 @@ struct CoSlot {
             (e = hipMalloc(reinterpret_cast<void **>(&d_packed), CO_MAX * N * F)) ||
             (e = hipMalloc(reinterpret_cast<void **>(&d_small), BYTES)) ||
             (e = hipMalloc(reinterpret_cast<void **>(&d_ws), decds_encode_commit_workspace_bytes(CO_MAX))) ||
-            (e = hipHostMalloc(reinterpret_cast<void **>(&h_small), BYTES, DECDS_HOST_MALLOC_FLAGS)))
+            (e = hipHostMalloc(reinterpret_cast<void **>(&h_small), BYTES, DECDS_HOST_MALLOC_FLAGS))) {
+            release();  // all or nothing: a later call sees s == nullptr and sets the slot up again
             return e;
+        }
         rows = d_rows + (16 - reinterpret_cast<uintptr_t>(d_rows)) % 128;
         return hipSuccess;
     }
-    ~CoSlot() {
-        if (s) (void)hipStreamSynchronize(s);
-        for (uint8_t *p : {d_src, d_rows, d_packed, d_small, d_ws})
-            if (p) (void)hipFree(p);
-        if (h_small) (void)hipHostFree(h_small);
-        if (s) (void)hipStreamDestroy(s);
+    void release() {
+        if (s) hip_tolerate(hipStreamSynchronize(s), "hipStreamSynchronize");
+        for (uint8_t **p : {&d_src, &d_rows, &d_packed, &d_small, &d_ws}) {
+            if (*p) hip_tolerate(hipFree(*p), "hipFree");
+            *p = nullptr;
+        }
+        if (h_small) hip_tolerate(hipHostFree(h_small), "hipHostFree");
+        if (s) hip_tolerate(hipStreamDestroy(s), "hipStreamDestroy");
+        h_small = rows = nullptr;
+        s = nullptr;
     }
+    ~CoSlot() { release(); }
 };
 
 struct Coalescer {

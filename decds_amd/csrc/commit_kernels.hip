@@ -11,6 +11,7 @@
 
 #include "blake3_impl.h"
 #include "commit_kernels.h"
+#include "hip_status.h"
 #include "rlnc_layout.h"
 
 namespace decds {
@@ -309,12 +310,12 @@ hipError_t configure_commit_kernels() {
 hipError_t launch_commit(const uint8_t *coded, size_t pitch, size_t n, uint64_t first_chunkset_id, uint8_t *digests,
                          uint8_t *roots, uint8_t *proofs, hipStream_t stream) {
     if (n == 0) return hipSuccess;
-    (void)hipGetLastError();  // only this launch's status below
+    if (hipError_t p_ = hip_launch_begin("chunk_digest_kernel")) return p_;
     hipLaunchKernelGGL(chunk_digest_kernel, dim3((uint32_t)(n * N)), dim3(DG_WG), 0, stream, coded, pitch,
                        first_chunkset_id, (const uint64_t *)nullptr, digests);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    (void)hipGetLastError();  // only this launch's status below
+    if (hipError_t p_ = hip_launch_begin("chunkset_merkle_kernel")) return p_;
     hipLaunchKernelGGL(chunkset_merkle_kernel, dim3((uint32_t)((n * N + MK_WG - 1) / MK_WG)), dim3(MK_WG), 0, stream,
                        digests, n, roots, proofs);
     return hipGetLastError();
@@ -324,11 +325,11 @@ hipError_t launch_commit_fold(const uint8_t *coded, size_t pitch, size_t n, cons
                               uint8_t *digests, uint8_t *roots, uint8_t *proofs, hipStream_t stream) {
     if (n == 0) return hipSuccess;
     if (per_row != SUB_PER_ROW) return hipErrorInvalidValue;
-    (void)hipGetLastError();  // only this launch's status below
+    if (hipError_t p_ = hip_launch_begin("commit_fold_kernel")) return p_;
     hipLaunchKernelGGL(commit_fold_kernel, dim3((uint32_t)(n * N)), dim3(FOLD_LANES), 0, stream, coded, pitch, sub, digests);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    (void)hipGetLastError();  // only this launch's status below
+    if (hipError_t p_ = hip_launch_begin("chunkset_merkle_kernel")) return p_;
     hipLaunchKernelGGL(chunkset_merkle_kernel, dim3((uint32_t)((n * N + MK_WG - 1) / MK_WG)), dim3(MK_WG), 0, stream,
                        digests, n, roots, proofs);
     return hipGetLastError();
@@ -339,12 +340,12 @@ hipError_t launch_validate(const uint8_t *coded, size_t pitch, size_t n_rows, co
                            size_t num_chunksets, const uint8_t *blob_root, uint8_t *digests, uint8_t *valid,
                            hipStream_t stream) {
     if (n_rows == 0) return hipSuccess;
-    (void)hipGetLastError();  // only this launch's status below
+    if (hipError_t p_ = hip_launch_begin("chunk_digest_kernel")) return p_;
     hipLaunchKernelGGL(chunk_digest_kernel, dim3((uint32_t)n_rows), dim3(DG_WG), 0, stream, coded, pitch, (uint64_t)0,
                        ids, digests);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    (void)hipGetLastError();  // only this launch's status below
+    if (hipError_t p_ = hip_launch_begin("validate_kernel")) return p_;
     hipLaunchKernelGGL(validate_kernel, dim3((uint32_t)((n_rows + 63) / 64)), dim3(64), 0, stream, digests, n_rows,
                        ids, proofs, proof_len, chunkset_roots, num_chunksets, blob_root, valid);
     return hipGetLastError();

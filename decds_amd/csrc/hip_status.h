@@ -1,0 +1,21 @@
+// hip_status.h — a launch's own status under HIP's per-thread last error (not part of the public ABI).
+//
+// HIP keeps the last error per host thread with CUDA's semantics: hipGetLastError() returns the last
+// FAILURE of any earlier call on the thread (successful calls do not reset it), so the
+// hipGetLastError() that reports a hipLaunchKernelGGL can also carry an older call's failure. Round 3
+// cleared that slot unconditionally before every launch, which would also have swallowed such an
+// older error. Now:
+//   * every HIP call the library makes is checked where it is made; the failures it tolerates
+//     (teardown, a device allocation past the budget that makes it spill) go through hip_tolerate,
+//     which consumes the thread's error slot and notes the call;
+//   * hip_launch_begin, right before a launch, peeks at the slot: an error still pending there is an
+//     earlier call's — it is consumed and returned, and decds_hip_error names it as such ("left
+//     pending by an earlier HIP call on this thread": the library's last tolerated call on the thread,
+//     or "a call outside the library") instead of blaming the launch.
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace decds {
+void hip_tolerate(hipError_t e, const char *what);
+hipError_t hip_launch_begin(const char *kernel);
+}  // namespace decds

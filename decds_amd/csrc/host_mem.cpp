@@ -1,6 +1,7 @@
 // host_mem.cpp — registry of page-locked host ranges (decds_host_register / decds_host_alloc),
 // the host thread pool for staging copies, and the pinned bounce rings (host_mem.h).
 #include "host_mem.h"
+#include "hip_status.h"
 
 #include <algorithm>
 #include <atomic>
@@ -40,7 +41,7 @@ void finalize_if_idle(std::map<uintptr_t, Entry>::iterator it) {
     if (it->second.alloc)
         host_pinned_free(p, it->second.len);
     else
-        (void)hipHostUnregister(p);
+        hip_tolerate(hipHostUnregister(p), "hipHostUnregister");
     g_reg.erase(it);
 }
 
@@ -221,7 +222,7 @@ void host_pinned_free(void *p, size_t) {
             g_block.erase(b);
         }
     }
-    (void)hipHostFree(p);
+    hip_tolerate(hipHostFree(p), "hipHostFree");
 }
 
 size_t host_cache_trim() {
@@ -229,7 +230,7 @@ size_t host_cache_trim() {
     const size_t freed = g_cached;
     for (auto &kv : g_cache) {
         g_block.erase(kv.second);
-        (void)hipHostFree(kv.second);
+        hip_tolerate(hipHostFree(kv.second), "hipHostFree");
     }
     g_cache.clear();
     g_cached = 0;
@@ -339,7 +340,7 @@ hipError_t BounceRing::flush() {
 void BounceRing::abandon() {
     for (int i = 0; i < R; i++) {
         pend_dst[i] = nullptr;  // an abandoned call's copy-outs are dropped, never written late
-        if (used[i]) (void)hipEventSynchronize(ev[i]);
+        if (used[i]) hip_tolerate(hipEventSynchronize(ev[i]), "hipEventSynchronize");
         used[i] = false;
     }
 }
@@ -347,7 +348,7 @@ void BounceRing::abandon() {
 BounceRing::~BounceRing() {
     abandon();
     for (int i = 0; i < R; i++) {
-        if (ev[i]) (void)hipEventDestroy(ev[i]);
+        if (ev[i]) hip_tolerate(hipEventDestroy(ev[i]), "hipEventDestroy");
         if (buf[i]) host_pinned_free(buf[i], PIECE);
     }
 }

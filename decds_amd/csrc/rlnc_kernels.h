@@ -16,7 +16,13 @@ struct LaunchGeom {
     uint32_t *counters = nullptr;
     mutable std::atomic<uint32_t> counter_next{0};
     static constexpr uint32_t N_COUNTERS = 256, COUNTER_STRIDE = 32;  // in uint32_t
+    // resident workgroups of the persistent encode / decode sweeps (configure_geom, at context creation)
+    uint32_t enc_grid = 0, dec_grid = 0;
 };
+void configure_geom(LaunchGeom &g);
+// batches of at least this many chunksets decode with the persistent sweep (process-wide; 0 = default)
+void set_decode_sweep_min_n(uint64_t n);
+uint64_t decode_sweep_min_n();
 
 hipError_t launch_encode(const LaunchGeom &g, const uint8_t *src, size_t n, const uint8_t *coeffs,
                          uint8_t *dst, size_t pitch, uint32_t poly, uint32_t marker,

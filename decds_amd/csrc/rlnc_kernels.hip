@@ -24,10 +24,12 @@
 #include <cstdlib>
 
 #include <algorithm>
+#include <atomic>
 #include <utility>
 
 #include "blake3_impl.h"
 #include "commit_kernels.h"
+#include "hip_status.h"
 #include "rlnc_kernels.h"
 #include "rlnc_layout.h"
 
@@ -802,39 +804,44 @@ __device__ __forceinline__ void tail_finish(const TailLds &t, uint32_t c, int32_
     if (!t.cut) status[c] = (int32_t)TAIL_SCAN_STATUS;
 }
 
-// The backward marker scan for the chunksets tail_finish left at TAIL_SCAN_STATUS: one workgroup
-// per chunkset, 4 KiB of decoded bytes per step from the end of the chunkset down; the highest
-// marker position found is the decoded length, none anywhere is ChunksetRepairingFailed. Every other
-// workgroup reads one status word and leaves.
+// The backward marker scan for the chunksets tail_finish left at TAIL_SCAN_STATUS: a workgroup per
+// chunkset in turn (c = blockIdx.x, + gridDim.x, ...: at most one workgroup per CU is launched, so
+// an intact batch costs a launch and one status read per chunkset), 4 KiB of decoded bytes per step
+// from the end of the chunkset down; the highest marker position found is the decoded length, none
+// anywhere is ChunksetRepairingFailed.
+constexpr uint32_t TAIL_SCAN_GRID = 256;
 __global__ __launch_bounds__(WG) void rlnc_tail_scan_kernel(size_t n, const uint8_t *__restrict__ dst,
                                                             int32_t *__restrict__ status,
                                                             const uint64_t *__restrict__ out_bases,
                                                             uint32_t *__restrict__ info, uint32_t marker) {
-    const uint32_t c = blockIdx.x;
-    if (c >= n || __builtin_amdgcn_readfirstlane(status[c]) != (int32_t)TAIL_SCAN_STATUS) return;
-    const uint8_t *obase = out_bases ? reinterpret_cast<const uint8_t *>(uniform_u64(out_bases[c])) : dst + (size_t)c * CS;
     __shared__ uint32_t s_hit;
-    if (threadIdx.x == 0) s_hit = 0;
-    __syncthreads();
     constexpr uint32_t STEP = WG * 16;
     static_assert(CS % STEP == 0, "whole steps");
-    uint32_t hit = 0;
-    for (uint32_t blk = (uint32_t)CS; blk > 0;) {
-        blk -= STEP;
-        const uint32_t b0 = blk + threadIdx.x * 16;
-        uint32_t h = 0;
-        for (int b = 15; b >= 0 && !h; b--)
-            if (obase[b0 + b] == marker) h = b0 + b + 1;
-        if (__syncthreads_or(h != 0)) {
-            if (h) atomicMax(&s_hit, h);
-            __syncthreads();
-            hit = s_hit;
-            break;
+    for (size_t c = blockIdx.x; c < n; c += gridDim.x) {
+        if (__builtin_amdgcn_readfirstlane(status[c]) != (int32_t)TAIL_SCAN_STATUS) continue;
+        const uint8_t *obase =
+            out_bases ? reinterpret_cast<const uint8_t *>(uniform_u64(out_bases[c])) : dst + c * CS;
+        if (threadIdx.x == 0) s_hit = 0;
+        __syncthreads();
+        uint32_t hit = 0;
+        for (uint32_t blk = (uint32_t)CS; blk > 0;) {
+            blk -= STEP;
+            const uint32_t b0 = blk + threadIdx.x * 16;
+            uint32_t h = 0;
+            for (int b = 15; b >= 0 && !h; b--)
+                if (obase[b0 + b] == marker) h = b0 + b + 1;
+            if (__syncthreads_or(h != 0)) {
+                if (h) atomicMax(&s_hit, h);
+                __syncthreads();
+                hit = s_hit;
+                break;
+            }
         }
-    }
-    if (threadIdx.x == 0) {
-        status[c] = hit ? 0 : 6;  // DECDS_OK / DECDS_ERR_CHUNKSET_REPAIRING_FAILED
-        if (info) info[4 * (size_t)c] = hit ? hit - 1 : 0u;
+        if (threadIdx.x == 0) {
+            status[c] = hit ? 0 : 6;  // DECDS_OK / DECDS_ERR_CHUNKSET_REPAIRING_FAILED
+            if (info) info[4 * c] = hit ? hit - 1 : 0u;
+        }
+        __syncthreads();  // every thread has read s_hit before the next chunkset resets it
     }
 }
 
@@ -1303,21 +1310,25 @@ hipError_t configure_kernels() {
     return configure_commit_kernels();
 }
 
-// resident workgroups of the sweep kernel on this device (occupancy x CUs), once per process
-static uint32_t sweep_grid(const LaunchGeom &g) {
-    static uint32_t grid = 0;
-    if (!grid) {
-        int per_cu = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void *>(ENC_SWEEP(false)), WG,
-                                                         SWEEP_LDS) != hipSuccess || per_cu < 1)
-            per_cu = DECDS_ENC_WAVES;
-        grid = (uint32_t)per_cu * (uint32_t)(g.num_cus > 0 ? g.num_cus : 256);
-#ifdef DECDS_SWEEP_GRID_PCT
-        grid = grid * DECDS_SWEEP_GRID_PCT / 100;  // study builds: fewer resident workgroups than fit
-#endif
+// resident workgroups of a persistent kernel on this device (occupancy x CUs)
+static uint32_t resident_grid(const void *fn, uint32_t lds, int fallback_per_cu, int num_cus) {
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, WG, lds) != hipSuccess || per_cu < 1) {
+        hip_tolerate(hipErrorInvalidValue, "hipOccupancyMaxActiveBlocksPerMultiprocessor (fallback occupancy)");
+        per_cu = fallback_per_cu;
     }
-    return grid;
+    return (uint32_t)per_cu * (uint32_t)(num_cus > 0 ? num_cus : 256);
 }
+
+// the persistent sweeps' grids, once per context at creation (not lazily by concurrent launches)
+void configure_geom(LaunchGeom &g) {
+    g.enc_grid = resident_grid(reinterpret_cast<const void *>(ENC_SWEEP(false)), SWEEP_LDS, DECDS_ENC_WAVES, g.num_cus);
+#ifdef DECDS_SWEEP_GRID_PCT
+    g.enc_grid = g.enc_grid * DECDS_SWEEP_GRID_PCT / 100;  // study builds: fewer resident workgroups than fit
+#endif
+    g.dec_grid = resident_grid(reinterpret_cast<const void *>(DEC_SWEEP), SWEEP_LDS, DECDS_DEC_SWEEP_WAVES, g.num_cus);
+}
+static uint32_t sweep_grid(const LaunchGeom &g) { return g.enc_grid; }
 
 hipError_t launch_encode(const LaunchGeom &geom, const uint8_t *src, size_t n, const uint8_t *coeffs, uint8_t *dst,
                          size_t pitch, uint32_t poly, uint32_t marker, hipStream_t stream) {
@@ -1334,6 +1345,7 @@ hipError_t launch_encode(const LaunchGeom &geom, const uint8_t *src, size_t n, c
         counter = geom.counters + (geom.counter_next.fetch_add(1) % LaunchGeom::N_COUNTERS) * LaunchGeom::COUNTER_STRIDE;
     }
     void *args[] = {&src, &n, &coeffs, &dst, &pitch, const_cast<uint32_t *>(&phase), &poly, &marker, &counter};
+    if (hipError_t p_ = hip_launch_begin("rlnc_encode_sweep_kernel")) return p_;
     return hipLaunchKernel(fn, dim3(grid), dim3(WG), args, SWEEP_LDS, stream);
 }
 
@@ -1344,11 +1356,22 @@ hipError_t launch_encode(const LaunchGeom &geom, const uint8_t *src, size_t n, c
 #ifndef DECDS_DEC_SWEEP_MIN_N
 #define DECDS_DEC_SWEEP_MIN_N 256
 #endif
-static bool decode_sweeps(size_t n) {
-    const char *e = std::getenv("DECDS_DEC_SWEEP_MIN_N");
-    const unsigned long long min_n = e && *e ? std::strtoull(e, nullptr, 10) : DECDS_DEC_SWEEP_MIN_N;
-    return n >= min_n;
+// the threshold: environment variable DECDS_DEC_SWEEP_MIN_N read once (first use), else the build's
+// default; decds_set_decode_sweep_min_n changes it for the process (the GPU tests force either form)
+static uint64_t dec_sweep_default() {
+    static const uint64_t d = [] {
+        const char *e = std::getenv("DECDS_DEC_SWEEP_MIN_N");
+        return e && *e ? (uint64_t)std::strtoull(e, nullptr, 10) : (uint64_t)DECDS_DEC_SWEEP_MIN_N;
+    }();
+    return d;
 }
+static std::atomic<uint64_t> &dec_sweep_min_n() {
+    static std::atomic<uint64_t> v{dec_sweep_default()};
+    return v;
+}
+void set_decode_sweep_min_n(uint64_t n) { dec_sweep_min_n().store(n ? n : dec_sweep_default()); }
+uint64_t decode_sweep_min_n() { return dec_sweep_min_n().load(); }
+static bool decode_sweeps(size_t n) { return n >= dec_sweep_min_n().load(std::memory_order_relaxed); }
 const char *decode_kernel_name(size_t n) { return decode_sweeps(n) ? "rlnc_decode_sweep_kernel" : "rlnc_decode_kernel"; }
 
 const char *encode_kernel_name(size_t) { return "rlnc_encode_sweep_kernel"; }
@@ -1363,7 +1386,7 @@ hipError_t launch_encode_commit(const uint8_t *src, size_t n, const uint8_t *coe
                                 hipStream_t stream) {
     if (n == 0) return hipSuccess;
     if (!encode_commit_fusable(dst, pitch)) return hipErrorInvalidValue;
-    (void)hipGetLastError();  // only this launch's status below
+    if (hipError_t p_ = hip_launch_begin("rlnc_encode_hash_kernel")) return p_;
     hipLaunchKernelGGL((ENC_HASH), dim3((uint32_t)(n * FH_WG_UNITS)), dim3(WG), FH_LDS<DECDS_FH_DW>, stream, src, n,
                        coeffs, dst, pitch, poly, marker, first_id, ids, sub);
     return hipGetLastError();
@@ -1390,7 +1413,7 @@ hipError_t launch_repair_plan(const uint8_t *coded, size_t pitch, size_t n, cons
         last_poly = poly;
         last_gen = gen;
     }
-    (void)hipGetLastError();  // only this launch's status below
+    if (hipError_t p_ = hip_launch_begin("rlnc_plan_kernel")) return p_;
     hipLaunchKernelGGL(rlnc_plan_kernel, dim3((uint32_t)n), dim3(64), 0, stream, coded, pitch, n, cand,
                        reinterpret_cast<RepairPlan *>(plan), verdicts, status, tab);
     return hipGetLastError();
@@ -1402,14 +1425,7 @@ static hipError_t launch_decode_kernel(const LaunchGeom &geom, const uint8_t *co
                                        hipStream_t stream) {
     const RepairPlan *pl = reinterpret_cast<const RepairPlan *>(plan);
     if (decode_sweeps(n)) {
-        static uint32_t resident = 0;
-        if (!resident) {
-            int per_cu = 0;
-            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void *>(DEC_SWEEP), WG,
-                                                             SWEEP_LDS) != hipSuccess || per_cu < 1)
-                per_cu = DECDS_DEC_SWEEP_WAVES;
-            resident = (uint32_t)per_cu * (uint32_t)(geom.num_cus > 0 ? geom.num_cus : 256);
-        }
+        const uint32_t resident = geom.dec_grid;
         const uint64_t tiles = (uint64_t)n * TILES<DECDS_DEC_DW>;
         if (tiles >= (1ull << 31)) return hipErrorInvalidValue;  // tile indices are 32-bit
         const uint32_t grid = (uint32_t)std::min<uint64_t>(tiles, resident);
@@ -1419,11 +1435,11 @@ static hipError_t launch_decode_kernel(const LaunchGeom &geom, const uint8_t *co
             counter = geom.counters + (geom.counter_next.fetch_add(1) % LaunchGeom::N_COUNTERS) * LaunchGeom::COUNTER_STRIDE;
         }
         void *args[] = {&coded, &pitch, &n, &pl, &dst, &status, &in_bases, &out_bases, &poly, &marker, &counter, &info};
-        (void)hipGetLastError();  // only this launch's status below
+        if (hipError_t p_ = hip_launch_begin("rlnc_decode_sweep_kernel")) return p_;
         return hipLaunchKernel(reinterpret_cast<const void *>(DEC_SWEEP), dim3(grid), dim3(WG), args, SWEEP_LDS, stream);
     }
     constexpr uint32_t U = DEC_UNIT;
-    (void)hipGetLastError();  // only this launch's status below
+    if (hipError_t p_ = hip_launch_begin("rlnc_decode_kernel")) return p_;
     hipLaunchKernelGGL(rlnc_decode_kernel<U>, dim3((uint32_t)(n * (TILES<DECDS_DEC_DW> / U))), dim3(WG), DEC_LDS, stream, coded,
                        pitch, n, pl, dst, status, in_bases, out_bases, poly, marker, info);
     return hipGetLastError();
@@ -1437,7 +1453,9 @@ hipError_t launch_decode(const LaunchGeom &geom, const uint8_t *coded, size_t pi
     hipError_t e = launch_decode_kernel(geom, coded, pitch, n, plan, dst, status, in_bases, out_bases, poly, marker, inf, stream);
     if (e != hipSuccess) return e;
     // get_decoded_data's cut for the chunksets whose tail bytes hold no marker (rlnc_tail_scan_kernel)
-    hipLaunchKernelGGL(rlnc_tail_scan_kernel, dim3((uint32_t)n), dim3(WG), 0, stream, n, dst, status, out_bases, inf, marker);
+    if (hipError_t p_ = hip_launch_begin("rlnc_tail_scan_kernel")) return p_;
+    hipLaunchKernelGGL(rlnc_tail_scan_kernel, dim3((uint32_t)std::min<size_t>(n, TAIL_SCAN_GRID)), dim3(WG), 0, stream, n,
+                       dst, status, out_bases, inf, marker);
     return hipGetLastError();
 }
 
@@ -1447,12 +1465,12 @@ hipError_t launch_fill_random(uint64_t seed, uint64_t byte_offset, uint8_t *dst,
     if ((byte_offset & 7u) == 0 && (reinterpret_cast<uintptr_t>(dst) & 7u) == 0 && (nbytes & 7u) == 0) {
         const size_t nw = nbytes / 8;
         const uint32_t grid = (uint32_t)((nw + 255) / 256 < 8192 ? (nw + 255) / 256 : 8192);
-        (void)hipGetLastError();  // only this launch's status below
+        if (hipError_t p_ = hip_launch_begin("fill_random_words_kernel")) return p_;
         hipLaunchKernelGGL(fill_random_words_kernel, dim3(grid), dim3(256), 0, stream, seed, byte_offset / 8,
                            reinterpret_cast<uint64_t *>(dst), nw);
     } else {
         const uint32_t grid = (uint32_t)((nbytes + 255) / 256 < 8192 ? (nbytes + 255) / 256 : 8192);
-        (void)hipGetLastError();  // only this launch's status below
+        if (hipError_t p_ = hip_launch_begin("fill_random_bytes_kernel")) return p_;
         hipLaunchKernelGGL(fill_random_bytes_kernel, dim3(grid), dim3(256), 0, stream, seed, byte_offset, dst,
                            nbytes);
     }

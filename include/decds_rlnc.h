@@ -139,9 +139,12 @@ int decds_decode_batch(decds_ctx *ctx, const uint8_t *coded, size_t coded_pitch,
                        decds_repair_info *info, void *stream);
 
 /* name of the gfx950 kernel decds_decode_batch launches for n chunksets (for profiles and traces):
- * rlnc_decode_sweep_kernel from DECDS_DEC_SWEEP_MIN_N chunksets on (environment variable, read per
- * launch; default 256), rlnc_decode_kernel below */
+ * rlnc_decode_sweep_kernel from the sweep threshold on (default 256, or environment variable
+ * DECDS_DEC_SWEEP_MIN_N read once at first use), rlnc_decode_kernel below */
 const char *decds_decode_kernel_name(size_t n_chunksets);
+/* sets the decode sweep threshold for the process (0 = the default again); returns the threshold now
+ * in force. Both decode kernels give identical results; this only picks the faster form per batch. */
+uint64_t decds_set_decode_sweep_min_n(uint64_t n_chunksets);
 
 /* plan + decode in one call (the RepairingBlob::add_chunk loop + get_repaired_chunkset,
  * blob.rs:373-394, 451-473, for candidates already resident on the device) */

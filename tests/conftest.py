@@ -39,9 +39,11 @@ def _device_status_after_gpu_test(request):
 
 
 @pytest.fixture(params=["tiles", "sweep"])
-def decode_form(request, monkeypatch):
+def decode_form(request):
     """Run a decoding test through both decode kernels whatever its batch size: one-tile workgroups
-    (rlnc_decode_kernel) and the persistent sweep (rlnc_decode_sweep_kernel). launch_decode reads
-    DECDS_DEC_SWEEP_MIN_N at every launch (rlnc_kernels.hip decode_sweeps)."""
-    monkeypatch.setenv("DECDS_DEC_SWEEP_MIN_N", "1" if request.param == "sweep" else str(1 << 62))
-    return request.param
+    (rlnc_decode_kernel) and the persistent sweep (rlnc_decode_sweep_kernel), by the process-wide
+    threshold decds_set_decode_sweep_min_n (restored to the default afterwards)."""
+    from decds_amd._capi import lib
+    lib().decds_set_decode_sweep_min_n(1 if request.param == "sweep" else 1 << 62)
+    yield request.param
+    lib().decds_set_decode_sweep_min_n(0)

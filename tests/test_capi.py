@@ -92,15 +92,28 @@ def test_layout_constants():
     assert _capi.CHUNKSET_BYTES == o.CS
 
 
-def test_decode_kernel_by_batch_size(monkeypatch):
+def test_decode_kernel_by_batch_size():
     # launch_decode (rlnc_kernels.hip decode_sweeps): the persistent sweep from 256 chunksets on,
-    # one-tile workgroups below; DECDS_DEC_SWEEP_MIN_N moves the threshold per launch
+    # one-tile workgroups below; decds_set_decode_sweep_min_n moves the threshold for the process
+    # (0 = the default again); DECDS_DEC_SWEEP_MIN_N sets the default, read once at first use
+    import subprocess
+    import sys
     lib = _capi.lib()
-    monkeypatch.delenv("DECDS_DEC_SWEEP_MIN_N", raising=False)
     name = lambda n: lib.decds_decode_kernel_name(n).decode()  # noqa: E731
-    assert name(1) == name(255) == "rlnc_decode_kernel"
-    assert name(256) == name(1639) == "rlnc_decode_sweep_kernel"
-    monkeypatch.setenv("DECDS_DEC_SWEEP_MIN_N", "1")
-    assert name(1) == "rlnc_decode_sweep_kernel"
-    monkeypatch.setenv("DECDS_DEC_SWEEP_MIN_N", str(1 << 40))
-    assert name(1639) == "rlnc_decode_kernel"
+    try:
+        if "DECDS_DEC_SWEEP_MIN_N" not in os.environ:
+            assert lib.decds_set_decode_sweep_min_n(0) == 256
+            assert name(1) == name(255) == "rlnc_decode_kernel"
+            assert name(256) == name(1639) == "rlnc_decode_sweep_kernel"
+        assert lib.decds_set_decode_sweep_min_n(1) == 1 and name(1) == "rlnc_decode_sweep_kernel"
+        lib.decds_set_decode_sweep_min_n(1 << 40)
+        assert name(1639) == "rlnc_decode_kernel"
+    finally:
+        lib.decds_set_decode_sweep_min_n(0)
+    code = ("import sys; sys.path.insert(0, %r); from decds_amd import _capi; L = _capi.lib(); "
+            "n = lambda k: L.decds_decode_kernel_name(k).decode(); "
+            "assert n(6) == 'rlnc_decode_kernel' and n(7) == 'rlnc_decode_sweep_kernel'; "
+            "assert L.decds_set_decode_sweep_min_n(0) == 7" % ROOT)
+    r = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, DECDS_DEC_SWEEP_MIN_N="7"),
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr[-2000:]

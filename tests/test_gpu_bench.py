@@ -82,3 +82,34 @@ def test_bench_cfg5_last_shard_rehearsal_spot_checked(tmp_path):
         ref = o.chunkset_encode(expect, z["coeffs"][k], nthreads=8)
         assert np.array_equal(z["coded"][k], ref), c
     assert (128 << 30) - 13107 * o.CS == 2 << 20
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_torchrun_per_rank_records():
+    # The N > 1 path as the driver launches it (torch.distributed.run, one process per rank), with
+    # DECDS_BENCH_BACKEND=gloo so both ranks can share this box's one GPU: each rank encodes and repairs
+    # its contiguous shard of a 2 GiB blob (cfg2 per GPU) and checks every repaired chunkset; the
+    # line carries every rank's record (per_rank), the group's world size, and marks ranks sharing a
+    # device as not a scaling point.
+    env = dict(os.environ, DECDS_BENCH_BACKEND="gloo", MASTER_ADDR="127.0.0.1")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", "29531", os.path.join(ROOT, "bench.py"),
+                        "--gpus", "2", "--steps", "2", "--warmup", "1", "--settle-s", "0.1", "--config", "cfg2",
+                        "--no-commit"], capture_output=True, text=True, timeout=240, cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]   # rank 0 prints the one line
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["world_size"] == 2 and d["backend"] == "gloo"
+    pr = d["per_rank"]
+    assert [x["rank"] for x in pr] == [0, 1]
+    n_total = -(-(2 << 30) // (10 << 20))          # 205 chunksets, the last one partial
+    assert pr[0]["chunksets"] == [0, 103] and pr[1]["chunksets"] == [103, n_total]
+    assert pr[0]["shard_bytes"] + pr[1]["shard_bytes"] == 2 << 30
+    for x in pr:
+        lo, hi = x["chunksets"]
+        assert x["ready_chunksets"] + x["not_ready_chunksets"] == hi - lo
+        assert x["repaired_checked"] == x["ready_chunksets"] >= hi - lo - 3
+        assert x["encode_ms"] > 0 and x["decode_ms"] > 0 and x["gpu_GiBps"] > 0
+    assert d["scaling_point"] is False and "share" in d["scaling_note"]
+    assert d["cpu_baseline"] is None and d["encode_batch_sweep"] is None
