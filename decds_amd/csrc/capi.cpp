@@ -230,9 +230,8 @@ int decds_encode_batch(decds_ctx *ctx, const uint8_t *src, size_t n, const uint8
 
 const char *decds_encode_kernel_name(size_t n_chunksets) { return encode_kernel_name(n_chunksets); }
 const char *decds_decode_kernel_name(size_t n_chunksets) { return decode_kernel_name(n_chunksets); }
-uint64_t decds_set_decode_sweep_min_n(uint64_t n_chunksets) {
-    set_decode_sweep_min_n(n_chunksets);
-    return decode_sweep_min_n();
+uint64_t decds_tuning(const char *name, uint64_t value, int set) {
+    return name ? set_tuning(name, value, set != 0) : UINT64_MAX;
 }
 
 int decds_repair_plan_batch(decds_ctx *ctx, const uint8_t *coded, size_t coded_pitch, size_t n,

@@ -17,12 +17,12 @@ struct LaunchGeom {
     mutable std::atomic<uint32_t> counter_next{0};
     static constexpr uint32_t N_COUNTERS = 256, COUNTER_STRIDE = 32;  // in uint32_t
     // resident workgroups of the persistent encode / decode sweeps (configure_geom, at context creation)
-    uint32_t enc_grid = 0, dec_grid = 0;
+    uint32_t enc_grid = 0, enc_small_grid = 0, dec_grid = 0;
 };
 void configure_geom(LaunchGeom &g);
-// batches of at least this many chunksets decode with the persistent sweep (process-wide; 0 = default)
-void set_decode_sweep_min_n(uint64_t n);
-uint64_t decode_sweep_min_n();
+// launch-shape thresholds by name (DECDS_DEC_SWEEP_MIN_N, DECDS_ENC_SMALL_MAX_N, with or without the
+// DECDS_ prefix): set (set = true; UINT64_MAX = the default again) and/or read; UINT64_MAX if unknown
+uint64_t set_tuning(const char *name, uint64_t value, bool set);
 
 hipError_t launch_encode(const LaunchGeom &g, const uint8_t *src, size_t n, const uint8_t *coeffs,
                          uint8_t *dst, size_t pitch, uint32_t poly, uint32_t marker,

@@ -22,6 +22,7 @@
 // git history (tools/study/rlnc_kernels_r01_study.hip at a5d9101) with their measurements in DESIGN.md §8.
 #include <hip/hip_runtime.h>
 #include <cstdlib>
+#include <cstring>
 
 #include <algorithm>
 #include <atomic>
@@ -1289,11 +1290,17 @@ constexpr bool MSG_OK = DECDS_ENC_DW == 4;
 #endif
 #define DEC_SWEEP rlnc_decode_sweep_kernel<DECDS_DEC_DW, DECDS_DEC_SWEEP_WAVES, DECDS_DEC_HB>
 #define ENC_SWEEP(MSG) rlnc_encode_sweep_kernel<DECDS_ENC_DW, DECDS_ENC_WAVES, MSG, (DECDS_ENC_QUEUE != 0)>
+// small batches (DECDS_ENC_SMALL_MAX_N): 8-column lane blocks, 512 tiles per chunkset, 3 waves per SIMD —
+// one chunkset fills the resident grid (16-column tiles give 256 workgroups on 512 slots at n = 1)
+#ifndef DECDS_ENC_SMALL_WAVES
+#define DECDS_ENC_SMALL_WAVES 4
+#endif
+#define ENC_SMALL rlnc_encode_sweep_kernel<2, DECDS_ENC_SMALL_WAVES, false, (DECDS_ENC_QUEUE != 0)>
 
 hipError_t configure_kernels() {
     const void *fns[] = {reinterpret_cast<const void *>(ENC_SWEEP(false)), reinterpret_cast<const void *>(ENC_SWEEP(MSG_OK)),
                          reinterpret_cast<const void *>(ENC_HASH), reinterpret_cast<const void *>(rlnc_decode_kernel<DEC_UNIT>),
-                         reinterpret_cast<const void *>(DEC_SWEEP)};
+                         reinterpret_cast<const void *>(DEC_SWEEP), reinterpret_cast<const void *>(ENC_SMALL)};
     for (const void *f : fns) {
         hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, std::max(SWEEP_LDS, FH_LDS<DECDS_FH_DW>));
         if (e != hipSuccess) return e;
@@ -1309,6 +1316,45 @@ hipError_t configure_kernels() {
     }
     return configure_commit_kernels();
 }
+
+#ifndef DECDS_DEC_SWEEP_MIN_N
+#define DECDS_DEC_SWEEP_MIN_N 256
+#endif
+#ifndef DECDS_ENC_SMALL_MAX_N
+#define DECDS_ENC_SMALL_MAX_N 1
+#endif
+// Launch-shape thresholds (process-wide): the environment variable of the same name read once (at
+// first use), else the build's default; decds_set_tuning changes one for the process (tests force
+// either form of a kernel pair, tools A/B them). Every form gives identical bytes.
+struct Tunable {
+    const char *name;
+    uint64_t build_default;
+    uint64_t initial() const {
+        const char *e = std::getenv(name);
+        return e && *e ? (uint64_t)std::strtoull(e, nullptr, 10) : build_default;
+    }
+};
+static const Tunable TUNABLES[] = {{"DECDS_DEC_SWEEP_MIN_N", DECDS_DEC_SWEEP_MIN_N},
+                                   {"DECDS_ENC_SMALL_MAX_N", DECDS_ENC_SMALL_MAX_N}};
+constexpr int TUNE_DEC_SWEEP_MIN_N = 0, TUNE_ENC_SMALL_MAX_N = 1, N_TUNABLES = 2;
+static uint64_t tune_default(int k) {
+    static const uint64_t d[N_TUNABLES] = {TUNABLES[0].initial(), TUNABLES[1].initial()};
+    return d[k];
+}
+static std::atomic<uint64_t> &tune(int k) {
+    static std::atomic<uint64_t> v[N_TUNABLES] = {{tune_default(0)}, {tune_default(1)}};
+    return v[k];
+}
+uint64_t set_tuning(const char *name, uint64_t value, bool set) {
+    for (int k = 0; k < N_TUNABLES; k++) {
+        if (std::strcmp(name, TUNABLES[k].name) != 0 && std::strcmp(name, TUNABLES[k].name + 6) != 0) continue;
+        if (set) tune(k).store(value == UINT64_MAX ? tune_default(k) : value);
+        return tune(k).load();
+    }
+    return UINT64_MAX;
+}
+static bool decode_sweeps(size_t n) { return n >= tune(TUNE_DEC_SWEEP_MIN_N).load(std::memory_order_relaxed); }
+static bool encode_small(size_t n) { return n <= tune(TUNE_ENC_SMALL_MAX_N).load(std::memory_order_relaxed); }
 
 // resident workgroups of a persistent kernel on this device (occupancy x CUs)
 static uint32_t resident_grid(const void *fn, uint32_t lds, int fallback_per_cu, int num_cus) {
@@ -1327,18 +1373,21 @@ void configure_geom(LaunchGeom &g) {
     g.enc_grid = g.enc_grid * DECDS_SWEEP_GRID_PCT / 100;  // study builds: fewer resident workgroups than fit
 #endif
     g.dec_grid = resident_grid(reinterpret_cast<const void *>(DEC_SWEEP), SWEEP_LDS, DECDS_DEC_SWEEP_WAVES, g.num_cus);
+    g.enc_small_grid = resident_grid(reinterpret_cast<const void *>(ENC_SMALL), SWEEP_LDS, DECDS_ENC_SMALL_WAVES, g.num_cus);
 }
 static uint32_t sweep_grid(const LaunchGeom &g) { return g.enc_grid; }
 
 hipError_t launch_encode(const LaunchGeom &geom, const uint8_t *src, size_t n, const uint8_t *coeffs, uint8_t *dst,
                          size_t pitch, uint32_t poly, uint32_t marker, hipStream_t stream) {
     if (n == 0) return hipSuccess;
-    const uint32_t phase = row_phase<DECDS_ENC_DW>(dst, pitch);
-    const bool msg = MSG_OK && phase == MSG_PHASE;
-    constexpr uint32_t T = TILES<DECDS_ENC_DW>;
+    const bool small = encode_small(n);
+    const uint32_t phase = small ? row_phase<2>(dst, pitch) : row_phase<DECDS_ENC_DW>(dst, pitch);
+    const bool msg = !small && MSG_OK && phase == MSG_PHASE;
+    const uint64_t T = small ? TILES<2> : TILES<DECDS_ENC_DW>;
     // small batches too: with fewer tiles than resident slots it is one tile each
-    const uint32_t grid = (uint32_t)std::min<uint64_t>((uint64_t)n * T, sweep_grid(geom));
-    const void *fn = msg ? reinterpret_cast<const void *>(ENC_SWEEP(MSG_OK)) : reinterpret_cast<const void *>(ENC_SWEEP(false));
+    const uint32_t grid = (uint32_t)std::min<uint64_t>((uint64_t)n * T, small ? geom.enc_small_grid : sweep_grid(geom));
+    const void *fn = small ? reinterpret_cast<const void *>(ENC_SMALL)
+                           : msg ? reinterpret_cast<const void *>(ENC_SWEEP(MSG_OK)) : reinterpret_cast<const void *>(ENC_SWEEP(false));
     uint32_t *counter = nullptr;  // none when every workgroup has one tile: no counter reset to launch
     if (DECDS_ENC_QUEUE && (uint64_t)n * T > grid) {
         if (!geom.counters) return hipErrorInvalidValue;
@@ -1353,25 +1402,6 @@ hipError_t launch_encode(const LaunchGeom &geom, const uint8_t *src, size_t n, c
 // persistent sweep (-1.5...-3.3 % decode time at 256-1639 chunksets, r05p-r05s), smaller ones one-tile
 // workgroups (the sweep measured 1.5-2.6 % slower at 103, r05p/r05q). The environment variable of that
 // name overrides the threshold per launch (tests force either form at any size).
-#ifndef DECDS_DEC_SWEEP_MIN_N
-#define DECDS_DEC_SWEEP_MIN_N 256
-#endif
-// the threshold: environment variable DECDS_DEC_SWEEP_MIN_N read once (first use), else the build's
-// default; decds_set_decode_sweep_min_n changes it for the process (the GPU tests force either form)
-static uint64_t dec_sweep_default() {
-    static const uint64_t d = [] {
-        const char *e = std::getenv("DECDS_DEC_SWEEP_MIN_N");
-        return e && *e ? (uint64_t)std::strtoull(e, nullptr, 10) : (uint64_t)DECDS_DEC_SWEEP_MIN_N;
-    }();
-    return d;
-}
-static std::atomic<uint64_t> &dec_sweep_min_n() {
-    static std::atomic<uint64_t> v{dec_sweep_default()};
-    return v;
-}
-void set_decode_sweep_min_n(uint64_t n) { dec_sweep_min_n().store(n ? n : dec_sweep_default()); }
-uint64_t decode_sweep_min_n() { return dec_sweep_min_n().load(); }
-static bool decode_sweeps(size_t n) { return n >= dec_sweep_min_n().load(std::memory_order_relaxed); }
 const char *decode_kernel_name(size_t n) { return decode_sweeps(n) ? "rlnc_decode_sweep_kernel" : "rlnc_decode_kernel"; }
 
 const char *encode_kernel_name(size_t) { return "rlnc_encode_sweep_kernel"; }

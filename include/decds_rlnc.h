@@ -139,12 +139,15 @@ int decds_decode_batch(decds_ctx *ctx, const uint8_t *coded, size_t coded_pitch,
                        decds_repair_info *info, void *stream);
 
 /* name of the gfx950 kernel decds_decode_batch launches for n chunksets (for profiles and traces):
- * rlnc_decode_sweep_kernel from the sweep threshold on (default 256, or environment variable
- * DECDS_DEC_SWEEP_MIN_N read once at first use), rlnc_decode_kernel below */
+ * rlnc_decode_sweep_kernel from DECDS_DEC_SWEEP_MIN_N chunksets on, rlnc_decode_kernel below */
 const char *decds_decode_kernel_name(size_t n_chunksets);
-/* sets the decode sweep threshold for the process (0 = the default again); returns the threshold now
- * in force. Both decode kernels give identical results; this only picks the faster form per batch. */
-uint64_t decds_set_decode_sweep_min_n(uint64_t n_chunksets);
+/* Launch-shape thresholds, process-wide (every form gives identical bytes; these only pick the faster
+ * kernel form per batch size): "DECDS_DEC_SWEEP_MIN_N" (default 256: persistent decode sweep from
+ * that many chunksets on) and "DECDS_ENC_SMALL_MAX_N" (default 1: encode batches up to that many
+ * chunksets run 8-column tiles, twice as many workgroups). Each starts from the environment variable
+ * of its name (read once, at first use) or the default. set != 0 sets it (value UINT64_MAX: back to
+ * that start value). Returns the value in force, UINT64_MAX for an unknown name. */
+uint64_t decds_tuning(const char *name, uint64_t value, int set);
 
 /* plan + decode in one call (the RepairingBlob::add_chunk loop + get_repaired_chunkset,
  * blob.rs:373-394, 451-473, for candidates already resident on the device) */

@@ -38,12 +38,25 @@ def _device_status_after_gpu_test(request):
     check(lib().decds_device_status(request.getfixturevalue("ctx").handle))
 
 
+def _tuning(name, value):
+    from decds_amd._capi import lib
+    return lib().decds_tuning(name.encode(), value, 1)
+
+
 @pytest.fixture(params=["tiles", "sweep"])
 def decode_form(request):
     """Run a decoding test through both decode kernels whatever its batch size: one-tile workgroups
     (rlnc_decode_kernel) and the persistent sweep (rlnc_decode_sweep_kernel), by the process-wide
-    threshold decds_set_decode_sweep_min_n (restored to the default afterwards)."""
-    from decds_amd._capi import lib
-    lib().decds_set_decode_sweep_min_n(1 if request.param == "sweep" else 1 << 62)
+    threshold DECDS_DEC_SWEEP_MIN_N (decds_tuning; back to its start value afterwards)."""
+    _tuning("DECDS_DEC_SWEEP_MIN_N", 1 if request.param == "sweep" else 1 << 62)
     yield request.param
-    lib().decds_set_decode_sweep_min_n(0)
+    _tuning("DECDS_DEC_SWEEP_MIN_N", (1 << 64) - 1)
+
+
+@pytest.fixture(params=["cols16", "cols8"])
+def encode_form(request):
+    """Run an encoding test through both forms of the encode sweep: 16-column lane blocks (batches
+    above DECDS_ENC_SMALL_MAX_N) and the small-batch form's 8-column blocks, whatever the batch size."""
+    _tuning("DECDS_ENC_SMALL_MAX_N", 1 << 62 if request.param == "cols8" else 0)
+    yield request.param
+    _tuning("DECDS_ENC_SMALL_MAX_N", (1 << 64) - 1)

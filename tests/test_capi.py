@@ -94,26 +94,33 @@ def test_layout_constants():
 
 def test_decode_kernel_by_batch_size():
     # launch_decode (rlnc_kernels.hip decode_sweeps): the persistent sweep from 256 chunksets on,
-    # one-tile workgroups below; decds_set_decode_sweep_min_n moves the threshold for the process
-    # (0 = the default again); DECDS_DEC_SWEEP_MIN_N sets the default, read once at first use
+    # one-tile workgroups below; decds_tuning moves the threshold for the process (UINT64_MAX = back
+    # to the start value); the environment variable of the same name sets that start value, read once
     import subprocess
     import sys
     lib = _capi.lib()
     name = lambda n: lib.decds_decode_kernel_name(n).decode()  # noqa: E731
+    tune = lambda k, v, s=1: lib.decds_tuning(k.encode(), v, s)  # noqa: E731
+    reset = (1 << 64) - 1
     try:
         if "DECDS_DEC_SWEEP_MIN_N" not in os.environ:
-            assert lib.decds_set_decode_sweep_min_n(0) == 256
+            assert tune("DECDS_DEC_SWEEP_MIN_N", reset) == 256
             assert name(1) == name(255) == "rlnc_decode_kernel"
             assert name(256) == name(1639) == "rlnc_decode_sweep_kernel"
-        assert lib.decds_set_decode_sweep_min_n(1) == 1 and name(1) == "rlnc_decode_sweep_kernel"
-        lib.decds_set_decode_sweep_min_n(1 << 40)
+        assert tune("DEC_SWEEP_MIN_N", 1) == 1 and name(1) == "rlnc_decode_sweep_kernel"  # prefix optional
+        tune("DECDS_DEC_SWEEP_MIN_N", 1 << 40)
         assert name(1639) == "rlnc_decode_kernel"
+        assert tune("DECDS_DEC_SWEEP_MIN_N", 0, 0) == 1 << 40  # read only
+        if "DECDS_ENC_SMALL_MAX_N" not in os.environ:
+            assert tune("DECDS_ENC_SMALL_MAX_N", 0, 0) == 1
+        assert tune("NO_SUCH_KNOB", 5) == reset
     finally:
-        lib.decds_set_decode_sweep_min_n(0)
+        tune("DECDS_DEC_SWEEP_MIN_N", reset)
+        tune("DECDS_ENC_SMALL_MAX_N", reset)
     code = ("import sys; sys.path.insert(0, %r); from decds_amd import _capi; L = _capi.lib(); "
             "n = lambda k: L.decds_decode_kernel_name(k).decode(); "
             "assert n(6) == 'rlnc_decode_kernel' and n(7) == 'rlnc_decode_sweep_kernel'; "
-            "assert L.decds_set_decode_sweep_min_n(0) == 7" % ROOT)
+            "assert L.decds_tuning(b'DECDS_DEC_SWEEP_MIN_N', (1 << 64) - 1, 1) == 7" % ROOT)
     r = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, DECDS_DEC_SWEEP_MIN_N="7"),
                        capture_output=True, text=True, timeout=60)
     assert r.returncode == 0, r.stderr[-2000:]

@@ -41,6 +41,7 @@ def gpu_encode(ctx, data, coeffs, n, pitch=F, off=0):
     return np.stack([out[r * pitch: r * pitch + F] for r in range(n * N)])
 
 
+@pytest.mark.usefixtures("encode_form")
 def test_encode_cfg1_matches_golden_and_oracle(ctx, kat):
     c = kat["cfg1"]
     data = o.fill_random(c["data_seed"], CS)
@@ -50,6 +51,7 @@ def test_encode_cfg1_matches_golden_and_oracle(ctx, kat):
     assert np.array_equal(coded, o.chunkset_encode(data, coeffs, nthreads=8))
 
 
+@pytest.mark.usefixtures("encode_form")
 def test_encode_batch_bitexact_and_pitch(ctx):
     n = 5
     data = o.fill_random(0xDEC05002, n * CS)
@@ -63,6 +65,7 @@ def test_encode_batch_bitexact_and_pitch(ctx):
             assert np.array_equal(coded[c * N:(c + 1) * N], refs[c]), (pitch, off, c)
 
 
+@pytest.mark.usefixtures("encode_form")
 def test_encode_every_column_phase(ctx):
     # a 16-byte-aligned pitch at each of the 16 base offsets runs the encode blocks at each column
     # phase; above phase 7 the last block becomes edge columns (piece 9 must not read past the
@@ -101,6 +104,7 @@ def test_encode_decode_at_the_largest_pitch(ctx):
     assert e.value.kind == "InvalidArgument"
 
 
+@pytest.mark.usefixtures("encode_form")
 def test_encode_zero_and_edge_coefficients(ctx):
     # zero coding vectors, identity rows (systematic pieces) and 0xFF everywhere
     data = o.fill_random(31, CS)
