@@ -431,14 +431,27 @@ def main():
     dec_kernel = _lib().decds_decode_kernel_name(n).decode()
     dominant = enc_kernel if enc_ms >= dec_ms else dec_kernel
     achieved = enc_gbs if dominant == enc_kernel else dec_gbs
-    traffic = None
+    traffic, fused_valu = None, None
     try:
         with open(args.traffic_json) as f:
             tj = json.load(f)
         if tj.get("config") == args.config and dominant in tj.get("kernels", {}):
             traffic = tj["kernels"][dominant]["hbm_bytes_per_launch"]
+        if tj.get("config") == args.config:
+            fused_valu = tj.get("kernels", {}).get("rlnc_encode_hash_kernel", {}).get("valu")
+            if fused_valu:
+                fused_valu = dict(fused_valu, source=tj.get("source"))
     except (OSError, ValueError):
         pass
+    if commit is not None:
+        # the fused ChunkSet::new kernel's own roofline: vector issue (tools/isa_mix.py; PMC of the same
+        # command, profiles/): VALU instructions x the built mix's cycles each / (1024 SIMDs x cycles)
+        commit["chunkset_new"]["valu_roofline"] = (
+            None if not fused_valu else {"kernel": "rlnc_encode_hash_kernel", "bound": "valu", "frac": fused_valu["frac"],
+                                         "frac_full_rate": fused_valu["frac_full_rate"],
+                                         "cycles_per_valu": fused_valu["cycles_per_valu"],
+                                         "insts_per_launch": fused_valu["insts_per_launch"],
+                                         "source": fused_valu["source"]})
 
     # value: blob bytes encoded plus blob bytes repaired (only the chunksets that were ready; the
     # decode kernel skips the rest), halved — encode+repair GiB/s of blob, whole job

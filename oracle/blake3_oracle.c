@@ -7,7 +7,7 @@
  * BLAKE3 specification in the structure of its reference implementation: a chunk state that
  * compresses 64-byte blocks with CHUNK_START / CHUNK_END flags, and an incremental chaining-value
  * stack that merges completed subtrees (PARENT) and finalises the root with the ROOT flag.
- * Pinned by the specification's published known answers (tests/test_commit_oracle.py).
+ * Pinned by the specification's published known answers (tests/test_commit_cpu.py).
  *
  * decds usage restated:
  *   chunk.rs:40-46        Chunk::digest = BLAKE3(chunkset_id as u64 LE || chunk_id as u64 LE || data)

@@ -2,7 +2,9 @@
 rule 24): every build is loaded with its own ctypes handle; rounds alternate between builds so DVFS
 and device drift hit all of them alike. Prints one JSON line per build (median / min over rounds).
 
-usage: python tools/abbench.py --n 1639 --rounds 12 lib_a.so lib_b.so[:pitch] ...
+usage: python tools/abbench.py --n 1639 --rounds 12 lib_a.so lib_b.so[:pitch[+offset]][@KNOB=V] ...
+  "default" = the in-tree library; @KNOB=V sets a launch-shape threshold (decds_tuning, e.g.
+  @DECDS_ENC_SMALL_MAX_N=64) before each of that build's runs, so forms of one build A/B in-process.
 """
 import argparse
 import ctypes
@@ -34,13 +36,19 @@ def main():
     na = max(a.alloc_n, n + a.at)
     builds = []
     for spec in a.libs:
+        spec, _, knob = spec.partition("@")
         path, _, rest = spec.partition(":")
+        if path == "default":
+            from decds_amd import build as _build
+            path = _build.LIB
         pitch, _, off = rest.partition("+")  # lib.so[:pitch[+offset]]: coded rows start `offset` bytes in
         L = ctypes.CDLL(os.path.abspath(path), mode=ctypes.RTLD_LOCAL)
         _declare(L)
         h = ctypes.c_void_p()
         assert L.decds_ctx_create(0, ctypes.byref(h)) == 0, L.decds_last_error()
-        builds.append({"tag": os.path.basename(path)[:-3] + ("@%s" % rest if rest else ""), "lib": L, "ctx": h,
+        kname, _, kval = knob.partition("=")
+        builds.append({"tag": os.path.basename(path)[:-3] + (":%s" % rest if rest else "") + ("@%s" % knob if knob else ""),
+                       "lib": L, "ctx": h, "knob": (kname.encode(), int(kval)) if knob else None,
                        "pitch": int(pitch) if pitch else F, "off": int(off) if off else 0, "cs": CS,
                        "t": []})
     maxcs = max(b["cs"] for b in builds)
@@ -68,6 +76,8 @@ def main():
 
     def run(b, ev=None, encode=True):
         L, h, p = b["lib"], b["ctx"], b["pitch"]
+        if b["knob"]:
+            L.decds_tuning(b["knob"][0], b["knob"][1], 1)
         coded = coded0[b["off"]:]
         if ev:
             ev[0].record(st)

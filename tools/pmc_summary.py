@@ -57,6 +57,25 @@ def main():
             if line.startswith("{") and '"metric"' in line:
                 with open(os.path.join(prof, "%s_bench_traced.json" % tag), "w") as f:
                     f.write(line)
+    # the VALU issue roofline of the VALU-bound kernels (tools/isa_mix.py: SQ_INSTS_VALU x mean cycles per
+    # VALU instruction of the built kernel's mix / (1024 SIMDs x GRBM_GUI_ACTIVE / 8)), read by bench.py
+    try:
+        sys.path.insert(0, os.path.join(ROOT, "tools"))
+        import isa_mix
+        from decds_amd import build
+        funcs = isa_mix.functions(isa_mix.disassemble(build.build(verbose=False)))
+        for k, c in summary.items():
+            name = k.split("::")[-1]
+            sym = next((s for s in funcs if name in s), None)
+            if sym and "SQ_INSTS_VALU" in c and "GRBM_GUI_ACTIVE" in c:
+                m = isa_mix.mix(funcs[sym])
+                simd_cycles = isa_mix.SIMDS * c["GRBM_GUI_ACTIVE"] / isa_mix.XCDS
+                traffic["kernels"].setdefault(name, {})["valu"] = {
+                    "insts_per_launch": c["SQ_INSTS_VALU"], "cycles_per_valu": m["cycles_per_valu"],
+                    "frac": round(c["SQ_INSTS_VALU"] * m["cycles_per_valu"] / simd_cycles, 4),
+                    "frac_full_rate": round(c["SQ_INSTS_VALU"] * 2 / simd_cycles, 4)}
+    except Exception as e:  # noqa: BLE001 - the traffic figures stand without it
+        print("valu roofline skipped: %s" % e, file=sys.stderr)
     with open(os.path.join(prof, "traffic.json"), "w") as f:
         json.dump(traffic, f, indent=1)
     print(json.dumps(traffic, indent=1))
