@@ -673,7 +673,12 @@ void rlnc_encode_hash_kernel(const uint8_t *__restrict__ src, size_t n, const ui
 // counter == NULL (batches of at most G tiles): one tile per workgroup, no counter. counter[0] is the
 // tile counter, counter[1] the exit count; both start at 0 (zeroed with the context) and the last
 // workgroup to finish zeroes them again.
-template <int DW, int WAVES, bool MSG, bool QUEUE = false>
+// EDGE_SPLIT (the small-batch form): the last min(n, EDGE_WGS) workgroups of the grid do the
+// prefixes and edge columns, one chunkset each in turn, beside the tile workgroups instead of ahead of
+// their first tile (at n = 1 the edge pass — byte-wise loads, a few dependent HBM round trips — sat on
+// the one critical path of a 13 µs launch). The launcher keeps the whole grid co-resident.
+constexpr uint32_t EDGE_WGS = 64;
+template <int DW, int WAVES, bool MSG, bool QUEUE = false, bool EDGE_SPLIT = false>
 __global__ __launch_bounds__(WG, WAVES) __attribute__((amdgpu_waves_per_eu(WAVES, WAVES)))
 void rlnc_encode_sweep_kernel(const uint8_t *__restrict__ src, size_t n, const uint8_t *__restrict__ coeffs,
                               uint8_t *__restrict__ dst, size_t pitch, uint32_t phase, uint32_t poly, uint32_t marker,
@@ -687,8 +692,12 @@ void rlnc_encode_sweep_kernel(const uint8_t *__restrict__ src, size_t n, const u
     for (int i = 0; i < (int)K; i++) ioff[i] = (uint32_t)(i * L);
 #pragma unroll
     for (int j = 0; j < (int)N; j++) ooff[j] = (uint32_t)(j * pitch + K);
-    // 1. coding-vector prefixes and edge columns of chunksets b, b + gridDim, ... (tables in buffer 1)
-    for (size_t cs = blockIdx.x; cs < n; cs += gridDim.x) {
+    // 1. coding-vector prefixes and edge columns of chunksets b, b + G, ... (tables in buffer 1); with
+    // EDGE_SPLIT by the NE edge workgroups at the end of the grid, which then leave
+    const uint32_t NE = EDGE_SPLIT ? (uint32_t)(n < EDGE_WGS ? n : EDGE_WGS) : 0u;
+    const uint32_t G = gridDim.x - NE;  // tile workgroups
+    const bool edge_wg = EDGE_SPLIT && blockIdx.x >= G;
+    for (size_t cs = EDGE_SPLIT ? (edge_wg ? blockIdx.x - G : n) : blockIdx.x; cs < n; cs += EDGE_SPLIT ? NE : G) {
         const uint8_t *M = coeffs + cs * N * K;
         const uint8_t *ibase = src + cs * CS;
         uint8_t *obase = dst + cs * N * pitch;
@@ -711,9 +720,8 @@ void rlnc_encode_sweep_kernel(const uint8_t *__restrict__ src, size_t n, const u
     }
     // 2. the sweep over tiles blockIdx.x, + G, ... (sweeps per XCD eighth measured slower, r02p)
     const uint64_t total = (uint64_t)n * T;
-    const uint32_t G = gridDim.x;
     uint32_t t = blockIdx.x;
-    if (t >= total) return;
+    if (edge_wg || t >= total) return;
     auto col_of = [&](uint32_t tt) { return tile_col<DW, MSG>(tt % T, T, phase); };
     uint32_t cs = t / T;
     // prologue = the loop's memory-counter picture at its head: this tile's coefficient bytes, its
@@ -1295,7 +1303,7 @@ constexpr bool MSG_OK = DECDS_ENC_DW == 4;
 #ifndef DECDS_ENC_SMALL_WAVES
 #define DECDS_ENC_SMALL_WAVES 4
 #endif
-#define ENC_SMALL rlnc_encode_sweep_kernel<2, DECDS_ENC_SMALL_WAVES, false, (DECDS_ENC_QUEUE != 0)>
+#define ENC_SMALL rlnc_encode_sweep_kernel<2, DECDS_ENC_SMALL_WAVES, false, (DECDS_ENC_QUEUE != 0), true>
 
 hipError_t configure_kernels() {
     const void *fns[] = {reinterpret_cast<const void *>(ENC_SWEEP(false)), reinterpret_cast<const void *>(ENC_SWEEP(MSG_OK)),
@@ -1384,12 +1392,16 @@ hipError_t launch_encode(const LaunchGeom &geom, const uint8_t *src, size_t n, c
     const uint32_t phase = small ? row_phase<2>(dst, pitch) : row_phase<DECDS_ENC_DW>(dst, pitch);
     const bool msg = !small && MSG_OK && phase == MSG_PHASE;
     const uint64_t T = small ? TILES<2> : TILES<DECDS_ENC_DW>;
-    // small batches too: with fewer tiles than resident slots it is one tile each
-    const uint32_t grid = (uint32_t)std::min<uint64_t>((uint64_t)n * T, small ? geom.enc_small_grid : sweep_grid(geom));
+    // small batches too: with fewer tiles than resident slots it is one tile each; the small form's edge
+    // workgroups (EDGE_SPLIT) come on top, the whole grid within the resident slots
+    const uint32_t ne = small ? (uint32_t)std::min<size_t>(n, EDGE_WGS) : 0u;
+    const uint32_t tile_grid =
+        (uint32_t)std::min<uint64_t>((uint64_t)n * T, small ? geom.enc_small_grid - ne : sweep_grid(geom));
+    const uint32_t grid = tile_grid + ne;
     const void *fn = small ? reinterpret_cast<const void *>(ENC_SMALL)
                            : msg ? reinterpret_cast<const void *>(ENC_SWEEP(MSG_OK)) : reinterpret_cast<const void *>(ENC_SWEEP(false));
     uint32_t *counter = nullptr;  // none when every workgroup has one tile: no counter reset to launch
-    if (DECDS_ENC_QUEUE && (uint64_t)n * T > grid) {
+    if (DECDS_ENC_QUEUE && (uint64_t)n * T > tile_grid) {
         if (!geom.counters) return hipErrorInvalidValue;
         counter = geom.counters + (geom.counter_next.fetch_add(1) % LaunchGeom::N_COUNTERS) * LaunchGeom::COUNTER_STRIDE;
     }
