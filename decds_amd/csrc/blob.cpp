@@ -488,7 +488,9 @@ struct RbShard {
         c.decoded = false;
     }
     // a decode area: a free one, a new one within the budget, or (evict) one whose decoded chunkset
-    // has not been fetched yet; -1 when none (*err set only when not even one area can be allocated)
+    // has not been fetched yet; -1 when none (*err set only when not even one area can be allocated).
+    // Every get_repaired_chunkset frees the area of the chunkset it returns, so a later call always
+    // finds a free one: the eviction is a guard, not a path the API's call orders reach.
     int32_t take_area(std::vector<RbChunkset> &cs, bool evict, int *err) {
         if (!free_areas.empty()) {
             const int32_t a = free_areas.back();
@@ -1116,6 +1118,8 @@ int decds_repairing_blob_get_repaired_chunkset(decds_repairing_blob *rb, size_t 
     if ((e = copy_d2h(out, sh.area_out(c.area), len, uo.pinned(), sh.out_ring, sh.s)) || (e = sh.out_ring.flush()) ||
         (e = hipStreamSynchronize(sh.s))) {
         sh.out_ring.abandon();
+        sh.drop_area(c);  // consumed either way (blob.rs:458-462): its area and slot go back to the pools
+        sh.drop_slot(c);
         return decds_hip_error(e, "D2H (repaired chunkset)");
     }
     sh.drop_area(c);

@@ -338,3 +338,27 @@ def test_context_close_releases_its_objects_first(ctx):
     ctx2.close()
     assert rep._h is None and b2._h is None
     del rep, b2
+
+
+
+@pytest.mark.usefixtures("decode_form")
+def test_repairing_blob_two_decode_areas_any_fetch_order(ctx):
+    # RbShard's decode-area pool (blob.cpp) at its smallest useful size, two areas: each fetch decodes
+    # the chunkset asked for plus the next ready one into the other area when that is free, and frees
+    # the asked-for one's area, so a later fetch always finds a free area (take_area's eviction branch
+    # is a guard that this API order never reaches). Out-of-order fetches must return
+    # every chunkset's bytes, whether it was decoded as the asked-for one or ahead of time.
+    blob_len = 5 * CS + 777
+    data, _, blob = _blob(ctx, blob_len, 0x8B80)
+    header = blob.get_blob_header()
+    n = header.get_num_chunksets()
+    rep = decds_amd.RepairingBlob(ctx, header, device_budget=8 * _AREA + 8 * _SLAB)  # a quarter: 2 areas
+    for c in _all_chunks(blob):
+        if not rep.is_chunkset_ready_to_repair(c.get_chunkset_id()):
+            rep.add_chunk(c)
+    assert all(rep.is_chunkset_ready_to_repair(c) for c in range(n))
+    want = lambda c: data[c * CS:min(blob_len, (c + 1) * CS)].tobytes()  # noqa: E731
+    for c in (0, 3, 4, 1, 5, 2):  # c1 is decoded ahead with c0 and c2 with c5, the others on demand
+        assert rep.get_repaired_chunkset(c) == want(c), c
+        assert rep.memory()["decode_areas"] == 2
+    assert all(rep.is_chunkset_already_repaired(c) for c in range(n))
