@@ -352,7 +352,7 @@ def test_repairing_blob_two_decode_areas_any_fetch_order(ctx):
     data, _, blob = _blob(ctx, blob_len, 0x8B80)
     header = blob.get_blob_header()
     n = header.get_num_chunksets()
-    rep = decds_amd.RepairingBlob(ctx, header, device_budget=8 * _AREA + 8 * _SLAB)  # a quarter: 2 areas
+    rep = decds_amd.RepairingBlob(ctx, header, device_budget=8 * _AREA + 1)  # a quarter: 2 areas; 1 slab for rows
     for c in _all_chunks(blob):
         if not rep.is_chunkset_ready_to_repair(c.get_chunkset_id()):
             rep.add_chunk(c)
