@@ -1298,8 +1298,9 @@ constexpr bool MSG_OK = DECDS_ENC_DW == 4;
 #endif
 #define DEC_SWEEP rlnc_decode_sweep_kernel<DECDS_DEC_DW, DECDS_DEC_SWEEP_WAVES, DECDS_DEC_HB>
 #define ENC_SWEEP(MSG) rlnc_encode_sweep_kernel<DECDS_ENC_DW, DECDS_ENC_WAVES, MSG, (DECDS_ENC_QUEUE != 0)>
-// small batches (DECDS_ENC_SMALL_MAX_N): 8-column lane blocks, 512 tiles per chunkset, 3 waves per SIMD —
-// one chunkset fills the resident grid (16-column tiles give 256 workgroups on 512 slots at n = 1)
+// small batches (DECDS_ENC_SMALL_MAX_N): 8-column lane blocks, 512 tiles per chunkset, 4 waves per SIMD
+// (118 VGPRs) — one chunkset fills 512 workgroups (16-column tiles give 256 at n = 1); slower per byte
+// from 2 chunksets on (r06c), so the default threshold is 1
 #ifndef DECDS_ENC_SMALL_WAVES
 #define DECDS_ENC_SMALL_WAVES 4
 #endif
@@ -1367,8 +1368,9 @@ static bool encode_small(size_t n) { return n <= tune(TUNE_ENC_SMALL_MAX_N).load
 // resident workgroups of a persistent kernel on this device (occupancy x CUs)
 static uint32_t resident_grid(const void *fn, uint32_t lds, int fallback_per_cu, int num_cus) {
     int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, WG, lds) != hipSuccess || per_cu < 1) {
-        hip_tolerate(hipErrorInvalidValue, "hipOccupancyMaxActiveBlocksPerMultiprocessor (fallback occupancy)");
+    const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, WG, lds);
+    if (e != hipSuccess || per_cu < 1) {
+        hip_tolerate(e, "hipOccupancyMaxActiveBlocksPerMultiprocessor (the kernel's own occupancy used instead)");
         per_cu = fallback_per_cu;
     }
     return (uint32_t)per_cu * (uint32_t)(num_cus > 0 ? num_cus : 256);
