@@ -21,25 +21,24 @@ using namespace decds;
 
 static thread_local std::string g_last_error;
 static std::atomic<int> g_live_ctx{0};  // contexts created and not yet destroyed
-// hip_status.h: the library's last tolerated HIP failure on this thread, and whether the error being
-// reported was found pending before a launch (then it is an earlier call's, named by g_tolerated)
-static thread_local std::string g_tolerated;
+// hip_status.h: set when the error being reported was found pending before a launch (an earlier
+// call's, not the launch's); decds_hip_error names it as such
 static thread_local std::string g_pending_before;
 
 namespace decds {
 void hip_tolerate(hipError_t e, const char *what) {
-    if (e == hipSuccess) return;
-    (void)hipGetLastError();  // consumed here: the failure is tolerated, never a later launch's
-    g_tolerated = std::string(what) + ": " + hipGetErrorString(e);
+    (void)what;  // the call site names the tolerated failure; nothing is reported
+    if (e != hipSuccess) (void)hipGetLastError();  // consumed here, never a later launch's
 }
 
 hipError_t hip_launch_begin(const char *kernel) {
     const hipError_t p = hipPeekAtLastError();
     if (p == hipSuccess) return hipSuccess;
     (void)hipGetLastError();
-    g_pending_before = std::string("before launching ") + kernel + ", an error was left pending by an earlier HIP call on "
-                       "this thread (" + (g_tolerated.empty() ? "a call outside the library" :
-                                          "the library's last tolerated failure: " + g_tolerated) + ")";
+    // the library consumes every failure it reports (decds_hip_error) or tolerates (hip_tolerate), so
+    // an error pending here was left by a HIP call outside the library on this thread
+    g_pending_before = std::string("left pending before launching ") + kernel +
+                       " by an earlier HIP call on this thread, outside the library (not this launch's)";
     return p;
 }
 }  // namespace decds
@@ -55,6 +54,7 @@ int decds_set_error(int code, const char *fmt, ...) {
 }
 
 int decds_hip_error(hipError_t e, const char *what) {
+    (void)hipGetLastError();  // reported here: the thread's error slot is left clean for later launches
     if (!g_pending_before.empty()) {  // not this call's failure (hip_launch_begin)
         std::string note;
         note.swap(g_pending_before);

@@ -249,3 +249,37 @@ def test_chunkset_new_16_concurrent_callers(ctx, coalesce, monkeypatch):
                 root, proofs = o.merkle(leaves)
                 assert cs.get_root_commitment() == root, (t, rd)
                 assert [c.proof for c in chunks] == proofs, (t, rd)
+
+
+def _loaded_hip_runtime():
+    """the libamdhip64 this process already loaded (torch's; the library binds to the same one)"""
+    import ctypes
+    with open("/proc/self/maps") as f:
+        paths = {ln.split()[-1] for ln in f if "libamdhip64.so" in ln}
+    assert paths, "no HIP runtime mapped"
+    return ctypes.CDLL(sorted(paths)[0])  # an already-loaded path: the same handle, no second runtime
+
+
+def test_launch_reports_an_earlier_pending_hip_error_by_name(ctx):
+    # HIP keeps the last error per thread (CUDA semantics): a failed call outside the library leaves
+    # it pending, and the hipGetLastError() that reports a launch would return it. The launchers peek
+    # before launching (hip_launch_begin, decds_amd/csrc/hip_status.h): the pending error is returned
+    # once, named as an earlier call's — round 3's r05b failure read "fused encode + chunk hashing
+    # launch: invalid device ordinal (101)" with nothing saying it was not the launch's — and the
+    # next call is clean.
+    import torch
+    hip = _loaded_hip_runtime()
+    n = 1
+    src = torch.zeros(n * CS, dtype=torch.uint8, device="cuda")
+    cv = torch.ones(n * N * K, dtype=torch.uint8, device="cuda")
+    dst = torch.empty(n * N * F, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    assert hip.hipSetDevice(12345) == 101          # hipErrorInvalidDevice, left pending on this thread
+    with pytest.raises(DecdsError) as e:
+        codec.encode_batch(ctx, src, n, cv, dst)
+    msg = str(e.value)
+    assert e.value.kind == "HipError", msg
+    assert "(101)" in msg and "earlier HIP call on this thread" in msg and "outside the library" in msg, msg
+    codec.encode_batch(ctx, src, n, cv, dst)       # consumed: the next launch runs
+    torch.cuda.synchronize()
+    assert dst.view(n * N, F)[:, :K].cpu().numpy().tolist() == [[1] * K] * (n * N)
