@@ -693,11 +693,13 @@ void rlnc_encode_sweep_kernel(const uint8_t *__restrict__ src, size_t n, const u
 #pragma unroll
     for (int j = 0; j < (int)N; j++) ooff[j] = (uint32_t)(j * pitch + K);
     // 1. coding-vector prefixes and edge columns of chunksets b, b + G, ... (tables in buffer 1); with
-    // EDGE_SPLIT by the NE edge workgroups at the end of the grid, which then leave
-    const uint32_t NE = EDGE_SPLIT ? (uint32_t)(n < EDGE_WGS ? n : EDGE_WGS) : 0u;
+    // EDGE_SPLIT, when the launcher gave one workgroup per tile plus NE more, by those NE edge
+    // workgroups at the end of the grid, which then leave
+    const uint64_t total = (uint64_t)n * T;
+    const uint32_t NE = EDGE_SPLIT && gridDim.x > total ? (uint32_t)(gridDim.x - total) : 0u;
     const uint32_t G = gridDim.x - NE;  // tile workgroups
-    const bool edge_wg = EDGE_SPLIT && blockIdx.x >= G;
-    for (size_t cs = EDGE_SPLIT ? (edge_wg ? blockIdx.x - G : n) : blockIdx.x; cs < n; cs += EDGE_SPLIT ? NE : G) {
+    const bool edge_wg = NE && blockIdx.x >= G;
+    for (size_t cs = NE ? (edge_wg ? blockIdx.x - G : n) : blockIdx.x; cs < n; cs += NE ? NE : G) {
         const uint8_t *M = coeffs + cs * N * K;
         const uint8_t *ibase = src + cs * CS;
         uint8_t *obase = dst + cs * N * pitch;
@@ -719,7 +721,6 @@ void rlnc_encode_sweep_kernel(const uint8_t *__restrict__ src, size_t n, const u
         }
     }
     // 2. the sweep over tiles blockIdx.x, + G, ... (sweeps per XCD eighth measured slower, r02p)
-    const uint64_t total = (uint64_t)n * T;
     uint32_t t = blockIdx.x;
     if (edge_wg || t >= total) return;
     auto col_of = [&](uint32_t tt) { return tile_col<DW, MSG>(tt % T, T, phase); };
@@ -1300,11 +1301,14 @@ constexpr bool MSG_OK = DECDS_ENC_DW == 4;
 #define ENC_SWEEP(MSG) rlnc_encode_sweep_kernel<DECDS_ENC_DW, DECDS_ENC_WAVES, MSG, (DECDS_ENC_QUEUE != 0)>
 // small batches (DECDS_ENC_SMALL_MAX_N): 8-column lane blocks, 512 tiles per chunkset, 4 waves per SIMD
 // (118 VGPRs) — one chunkset fills 512 workgroups (16-column tiles give 256 at n = 1); slower per byte
-// from 2 chunksets on (r06c), so the default threshold is 1
+// from 4 chunksets on, where the 16-column form fills the grid too (r06c / r06j): threshold 2
 #ifndef DECDS_ENC_SMALL_WAVES
 #define DECDS_ENC_SMALL_WAVES 4
 #endif
-#define ENC_SMALL rlnc_encode_sweep_kernel<2, DECDS_ENC_SMALL_WAVES, false, (DECDS_ENC_QUEUE != 0), true>
+#ifndef DECDS_ENC_SMALL_EDGE
+#define DECDS_ENC_SMALL_EDGE 1  // the small form's edge columns on their own workgroups (EDGE_SPLIT)
+#endif
+#define ENC_SMALL rlnc_encode_sweep_kernel<2, DECDS_ENC_SMALL_WAVES, false, (DECDS_ENC_QUEUE != 0), (DECDS_ENC_SMALL_EDGE != 0)>
 
 hipError_t configure_kernels() {
     const void *fns[] = {reinterpret_cast<const void *>(ENC_SWEEP(false)), reinterpret_cast<const void *>(ENC_SWEEP(MSG_OK)),
@@ -1330,7 +1334,7 @@ hipError_t configure_kernels() {
 #define DECDS_DEC_SWEEP_MIN_N 256
 #endif
 #ifndef DECDS_ENC_SMALL_MAX_N
-#define DECDS_ENC_SMALL_MAX_N 1
+#define DECDS_ENC_SMALL_MAX_N 2
 #endif
 // Launch-shape thresholds (process-wide): the environment variable of the same name read once (at
 // first use), else the build's default; decds_set_tuning changes one for the process (tests force
@@ -1394,11 +1398,14 @@ hipError_t launch_encode(const LaunchGeom &geom, const uint8_t *src, size_t n, c
     const uint32_t phase = small ? row_phase<2>(dst, pitch) : row_phase<DECDS_ENC_DW>(dst, pitch);
     const bool msg = !small && MSG_OK && phase == MSG_PHASE;
     const uint64_t T = small ? TILES<2> : TILES<DECDS_ENC_DW>;
-    // small batches too: with fewer tiles than resident slots it is one tile each; the small form's edge
-    // workgroups (EDGE_SPLIT) come on top, the whole grid within the resident slots
-    const uint32_t ne = small ? (uint32_t)std::min<size_t>(n, EDGE_WGS) : 0u;
-    const uint32_t tile_grid =
-        (uint32_t)std::min<uint64_t>((uint64_t)n * T, small ? geom.enc_small_grid - ne : sweep_grid(geom));
+    // small batches too: with fewer tiles than resident slots it is one tile each. The small form's edge
+    // workgroups (EDGE_SPLIT) come on top only when every tile has its own workgroup and the whole grid
+    // stays resident — taking slots from the tiles instead left a straggler round (n = 2: 1024 tiles on
+    // 1022 workgroups, 2.4x the time, r06j)
+    const uint32_t cap = small ? geom.enc_small_grid : sweep_grid(geom);
+    const uint32_t tile_grid = (uint32_t)std::min<uint64_t>((uint64_t)n * T, cap);
+    const uint32_t ne_want = small && DECDS_ENC_SMALL_EDGE ? (uint32_t)std::min<size_t>(n, EDGE_WGS) : 0u;
+    const uint32_t ne = (uint64_t)n * T + ne_want <= cap ? ne_want : 0u;
     const uint32_t grid = tile_grid + ne;
     const void *fn = small ? reinterpret_cast<const void *>(ENC_SMALL)
                            : msg ? reinterpret_cast<const void *>(ENC_SWEEP(MSG_OK)) : reinterpret_cast<const void *>(ENC_SWEEP(false));

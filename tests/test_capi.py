@@ -112,7 +112,7 @@ def test_decode_kernel_by_batch_size():
         assert name(1639) == "rlnc_decode_kernel"
         assert tune("DECDS_DEC_SWEEP_MIN_N", 0, 0) == 1 << 40  # read only
         if "DECDS_ENC_SMALL_MAX_N" not in os.environ:
-            assert tune("DECDS_ENC_SMALL_MAX_N", 0, 0) == 1
+            assert tune("DECDS_ENC_SMALL_MAX_N", 0, 0) == 2
         assert tune("NO_SUCH_KNOB", 5) == reset
     finally:
         tune("DECDS_DEC_SWEEP_MIN_N", reset)
