@@ -111,3 +111,16 @@ def test_rehearse_shard_argument_checked_before_any_device_work():
         assert r.returncode == 2 and msg in r.stderr and "Traceback" not in r.stderr, (bad, r.stderr[-500:])
     assert bench.parse(["--rehearse-shard", "7/8"]).rehearse_shard == (7, 8)
     assert bench.parse([]).config == "cfg3"     # BASELINE's largest single-GPU configuration
+
+
+def test_init_failure_exits_with_a_message_not_a_hang():
+    # bench.init_group: a rendezvous that cannot complete (rank 0 of 2, rank 1 never starts) ends the
+    # process within the timeout with exit status 3 and a one-line reason — the driver's N-GPU run
+    # never hangs on a failed RCCL init (the same path; gloo here, no device)
+    import subprocess
+    code = ("import sys; sys.path.insert(0, %r); import bench, torch.distributed as dist; "
+            "bench.init_group(dist, 'gloo', None, 0, 2, timeout_s=4); print('unreachable')" % ROOT)
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), WORLD_SIZE="2", RANK="0")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 3, (r.returncode, r.stderr[-1500:])
+    assert "rank 0/2: gloo process group init failed" in r.stderr and "unreachable" not in r.stdout
