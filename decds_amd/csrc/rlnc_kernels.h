@@ -20,7 +20,7 @@ struct LaunchGeom {
     uint32_t enc_grid = 0, enc_small_grid = 0, dec_grid = 0;
 };
 void configure_geom(LaunchGeom &g);
-// launch-shape thresholds by name (DECDS_DEC_SWEEP_MIN_N, DECDS_ENC_SMALL_MAX_N, with or without the
+// launch-shape thresholds by name (DECDS_DEC_SWEEP_MIN_N, DECDS_ENC_SMALL_MAX_N, DECDS_ENC_NT_MIN_N, with or without the
 // DECDS_ prefix): set (set = true; UINT64_MAX = the default again) and/or read; UINT64_MAX if unknown
 uint64_t set_tuning(const char *name, uint64_t value, bool set);
 

@@ -471,7 +471,7 @@ __device__ __forceinline__ uint32_t tile_col(uint32_t t, uint32_t tb, uint32_t p
 // merges paths that issued no stores and waits with vmcnt(NIN-1) for the next tile's first input:
 // every tile then waited for the previous tile's stores as well; here it waits for the inputs only.
 // HAVE: x already holds tile ta's inputs (loaded before the workgroup's table build).
-template <int NIN, int NOUT, int DW, bool HAVE, bool MSG = false, int HB = 4>
+template <int NIN, int NOUT, int DW, bool HAVE, bool MSG = false, int HB = 4, int SAUX = 0>
 __device__ __forceinline__ void stream_range(uint32_t ta, uint32_t tb, uint32_t phase, const uint8_t *ibase,
                                              const uint32_t (&ioff)[NIN], uint8_t *obase,
                                              const uint32_t (&ooff)[NOUT], Vec<DW> (&x)[NIN]) {
@@ -485,7 +485,7 @@ __device__ __forceinline__ void stream_range(uint32_t ta, uint32_t tb, uint32_t 
     uint32_t t = ta;
 #pragma unroll 1
     do {
-        combine_block<NIN, NOUT, DW, 0, NoSink, 0, true, HB>(x, obase, ooff, col(t), ibase, ioff, col(t + 1));
+        combine_block<NIN, NOUT, DW, 0, NoSink, SAUX, true, HB>(x, obase, ooff, col(t), ibase, ioff, col(t + 1));
     } while (++t < tb);
 }
 
@@ -678,7 +678,30 @@ void rlnc_encode_hash_kernel(const uint8_t *__restrict__ src, size_t n, const ui
 // their first tile (at n = 1 the edge pass — byte-wise loads, a few dependent HBM round trips — sat on
 // the one critical path of a 13 µs launch). The launcher keeps the whole grid co-resident.
 constexpr uint32_t EDGE_WGS = 64;
-template <int DW, int WAVES, bool MSG, bool QUEUE = false, bool EDGE_SPLIT = false>
+// coded-row store cache policy (SAUX, the buffer stores' aux bits): `sc1` (16, write-through) below
+// DECDS_ENC_NT_MIN_N chunksets, `nt` (2) from there on. A plain store leaves its line dirty in the
+// XCD's L2, so a small batch's coded rows were written back by the end-of-kernel release, after its
+// last wave: write-through moves that into the launch (-12...-16 % at 1-2 chunksets, -3 % at 16,
+// r06p / r06q). From 256 chunksets on `sc1` costs +0.5 % and `nt` gains 0.5-1.5 %.
+constexpr int STORE_SC1 = 16, STORE_NT = 2;
+// Study builds only (DECDS_PHASE_TRACE, tools/phasetrace.py): wave 0 of each workgroup stamps the
+// 100 MHz real-time counter at its phases — entry, edge pass done, first tables ready, last lookups
+// issued, stores drained — plus its tile count (vector stores; decds_debug_phase_trace copies them out).
+#ifdef DECDS_PHASE_TRACE
+constexpr uint32_t PT_WGS = 8192, PT_SLOTS = 8;
+__device__ uint64_t g_phase_trace[PT_WGS * PT_SLOTS];
+#define PT_SET(slot, v)                                                                   \
+    do {                                                                                  \
+        if (threadIdx.x == 0 && blockIdx.x < PT_WGS) g_phase_trace[blockIdx.x * PT_SLOTS + (slot)] = (v); \
+    } while (0)
+#define PT_STAMP(slot) PT_SET(slot, __builtin_amdgcn_s_memrealtime())
+#else
+#define PT_SET(slot, v) \
+    do {                \
+    } while (0)
+#define PT_STAMP(slot) PT_SET(slot, 0)
+#endif
+template <int DW, int WAVES, bool MSG, bool QUEUE = false, bool EDGE_SPLIT = false, int SAUX = 0>
 __global__ __launch_bounds__(WG, WAVES) __attribute__((amdgpu_waves_per_eu(WAVES, WAVES)))
 void rlnc_encode_sweep_kernel(const uint8_t *__restrict__ src, size_t n, const uint8_t *__restrict__ coeffs,
                               uint8_t *__restrict__ dst, size_t pitch, uint32_t phase, uint32_t poly, uint32_t marker,
@@ -686,6 +709,7 @@ void rlnc_encode_sweep_kernel(const uint8_t *__restrict__ src, size_t n, const u
     // no static __shared__ here: the lookups' inline-asm ds_reads address the tables from LDS byte 0,
     // so everything lives in the dynamic allocation (2 table buffers, then the next-tile slot)
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    PT_STAMP(0);
     constexpr uint32_t T = TILES<DW>;
     uint32_t ioff[K], ooff[N];
 #pragma unroll
@@ -721,8 +745,18 @@ void rlnc_encode_sweep_kernel(const uint8_t *__restrict__ src, size_t n, const u
         }
     }
     // 2. the sweep over tiles blockIdx.x, + G, ... (sweeps per XCD eighth measured slower, r02p)
+    PT_STAMP(1);
     uint32_t t = blockIdx.x;
+#ifdef DECDS_PHASE_TRACE
+    if (edge_wg || t >= total) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        PT_STAMP(4);
+        return;
+    }
+    uint32_t pt_tiles = 0;
+#else
     if (edge_wg || t >= total) return;
+#endif
     auto col_of = [&](uint32_t tt) { return tile_col<DW, MSG>(tt % T, T, phase); };
     uint32_t cs = t / T;
     // prologue = the loop's memory-counter picture at its head: this tile's coefficient bytes, its
@@ -760,17 +794,26 @@ void rlnc_encode_sweep_kernel(const uint8_t *__restrict__ src, size_t n, const u
             if (threadIdx.x == 0) s_next = G + grab;
         }
         lds_barrier();
+#ifdef DECDS_PHASE_TRACE
+        if (pt_tiles++ == 0) PT_STAMP(2);
+#endif
         const uint32_t tn = QUEUE ? s_next : t + G;
         grab = grab_next();
         more = tn < total;
         const uint32_t csn = more ? tn / T : cs;
         cw = table_coeffs_all<K, N>(coeffs + (size_t)csn * N * K, K);
-        combine_block<K, N, DW, 0, NoSink, 0, true, DECDS_ENC_HB>(x, dst + (size_t)cs * N * pitch, ooff, col_of(t),
+        combine_block<K, N, DW, 0, NoSink, SAUX, true, DECDS_ENC_HB>(x, dst + (size_t)cs * N * pitch, ooff, col_of(t),
                                                                   src + (size_t)csn * CS, ioff, more ? col_of(tn) : OOB_COL);
         lds_barrier();
         t = tn;
         cs = csn;
     } while (more);
+#ifdef DECDS_PHASE_TRACE
+    PT_STAMP(3);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    PT_STAMP(4);
+    PT_SET(5, pt_tiles);
+#endif
     // the last workgroup out resets the counter pair (tile counter, exit count) for the next launch
     // that takes this slot: no reset launch on the stream (a hipMemsetAsync was ~5 µs per encode)
     if (QUEUE && counter && threadIdx.x == 0) {
@@ -869,6 +912,9 @@ __global__ __launch_bounds__(WG) void rlnc_tail_scan_kernel(size_t n, const uint
 #ifndef DECDS_DEC_HB
 #define DECDS_DEC_HB 2  // decode lookup group size (bytes of an input dword per group)
 #endif
+#ifndef DECDS_DEC_STORE_AUX
+#define DECDS_DEC_STORE_AUX 0
+#endif
 #ifndef DECDS_DEC_DW
 #define DECDS_DEC_DW 4  // decode lane-block width in dwords (4: 16 columns per lane)
 #endif
@@ -943,7 +989,7 @@ void rlnc_decode_kernel(const uint8_t *__restrict__ coded, size_t pitch, size_t 
     }
     // (realigning the piece stores — pieces start i bytes past alignment — through LDS staging or a DPP
     // wave shift measured 4-5 % slower / spilled: r02v/w)
-    stream_range<K, K, DW, DECDS_PREFETCH_FIRST, false, DECDS_DEC_HB>(tile0, tile0 + UNIT, phase, ibase, ioff, obase, ooff, x);
+    stream_range<K, K, DW, DECDS_PREFETCH_FIRST, false, DECDS_DEC_HB, DECDS_DEC_STORE_AUX>(tile0, tile0 + UNIT, phase, ibase, ioff, obase, ooff, x);
 }
 
 // 3 waves/SIMD for the decode sweep: at 4 (128 VGPRs) its loop spills, the tile counter's pending
@@ -1298,7 +1344,7 @@ constexpr bool MSG_OK = DECDS_ENC_DW == 4;
 #define DECDS_ENC_QUEUE 1
 #endif
 #define DEC_SWEEP rlnc_decode_sweep_kernel<DECDS_DEC_DW, DECDS_DEC_SWEEP_WAVES, DECDS_DEC_HB>
-#define ENC_SWEEP(MSG) rlnc_encode_sweep_kernel<DECDS_ENC_DW, DECDS_ENC_WAVES, MSG, (DECDS_ENC_QUEUE != 0)>
+#define ENC_SWEEP(MSG, SAUX) rlnc_encode_sweep_kernel<DECDS_ENC_DW, DECDS_ENC_WAVES, MSG, (DECDS_ENC_QUEUE != 0), false, SAUX>
 // small batches (DECDS_ENC_SMALL_MAX_N): 8-column lane blocks, 512 tiles per chunkset, 4 waves per SIMD
 // (118 VGPRs) — one chunkset fills 512 workgroups (16-column tiles give 256 at n = 1); slower per byte
 // from 4 chunksets on, where the 16-column form fills the grid too (r06c / r06j): threshold 2
@@ -1308,10 +1354,11 @@ constexpr bool MSG_OK = DECDS_ENC_DW == 4;
 #ifndef DECDS_ENC_SMALL_EDGE
 #define DECDS_ENC_SMALL_EDGE 1  // the small form's edge columns on their own workgroups (EDGE_SPLIT)
 #endif
-#define ENC_SMALL rlnc_encode_sweep_kernel<2, DECDS_ENC_SMALL_WAVES, false, (DECDS_ENC_QUEUE != 0), (DECDS_ENC_SMALL_EDGE != 0)>
+#define ENC_SMALL rlnc_encode_sweep_kernel<2, DECDS_ENC_SMALL_WAVES, false, (DECDS_ENC_QUEUE != 0), (DECDS_ENC_SMALL_EDGE != 0), STORE_SC1>
 
 hipError_t configure_kernels() {
-    const void *fns[] = {reinterpret_cast<const void *>(ENC_SWEEP(false)), reinterpret_cast<const void *>(ENC_SWEEP(MSG_OK)),
+    const void *fns[] = {reinterpret_cast<const void *>(ENC_SWEEP(false, STORE_SC1)), reinterpret_cast<const void *>(ENC_SWEEP(MSG_OK, STORE_SC1)),
+                         reinterpret_cast<const void *>(ENC_SWEEP(false, STORE_NT)), reinterpret_cast<const void *>(ENC_SWEEP(MSG_OK, STORE_NT)),
                          reinterpret_cast<const void *>(ENC_HASH), reinterpret_cast<const void *>(rlnc_decode_kernel<DEC_UNIT>),
                          reinterpret_cast<const void *>(DEC_SWEEP), reinterpret_cast<const void *>(ENC_SMALL)};
     for (const void *f : fns) {
@@ -1336,6 +1383,9 @@ hipError_t configure_kernels() {
 #ifndef DECDS_ENC_SMALL_MAX_N
 #define DECDS_ENC_SMALL_MAX_N 2
 #endif
+#ifndef DECDS_ENC_NT_MIN_N
+#define DECDS_ENC_NT_MIN_N 256
+#endif
 // Launch-shape thresholds (process-wide): the environment variable of the same name read once (at
 // first use), else the build's default; decds_set_tuning changes one for the process (tests force
 // either form of a kernel pair, tools A/B them). Every form gives identical bytes.
@@ -1348,14 +1398,15 @@ struct Tunable {
     }
 };
 static const Tunable TUNABLES[] = {{"DECDS_DEC_SWEEP_MIN_N", DECDS_DEC_SWEEP_MIN_N},
-                                   {"DECDS_ENC_SMALL_MAX_N", DECDS_ENC_SMALL_MAX_N}};
-constexpr int TUNE_DEC_SWEEP_MIN_N = 0, TUNE_ENC_SMALL_MAX_N = 1, N_TUNABLES = 2;
+                                   {"DECDS_ENC_SMALL_MAX_N", DECDS_ENC_SMALL_MAX_N},
+                                   {"DECDS_ENC_NT_MIN_N", DECDS_ENC_NT_MIN_N}};
+constexpr int TUNE_DEC_SWEEP_MIN_N = 0, TUNE_ENC_SMALL_MAX_N = 1, TUNE_ENC_NT_MIN_N = 2, N_TUNABLES = 3;
 static uint64_t tune_default(int k) {
-    static const uint64_t d[N_TUNABLES] = {TUNABLES[0].initial(), TUNABLES[1].initial()};
+    static const uint64_t d[N_TUNABLES] = {TUNABLES[0].initial(), TUNABLES[1].initial(), TUNABLES[2].initial()};
     return d[k];
 }
 static std::atomic<uint64_t> &tune(int k) {
-    static std::atomic<uint64_t> v[N_TUNABLES] = {{tune_default(0)}, {tune_default(1)}};
+    static std::atomic<uint64_t> v[N_TUNABLES] = {{tune_default(0)}, {tune_default(1)}, {tune_default(2)}};
     return v[k];
 }
 uint64_t set_tuning(const char *name, uint64_t value, bool set) {
@@ -1368,6 +1419,7 @@ uint64_t set_tuning(const char *name, uint64_t value, bool set) {
 }
 static bool decode_sweeps(size_t n) { return n >= tune(TUNE_DEC_SWEEP_MIN_N).load(std::memory_order_relaxed); }
 static bool encode_small(size_t n) { return n <= tune(TUNE_ENC_SMALL_MAX_N).load(std::memory_order_relaxed); }
+static bool encode_nt(size_t n) { return n >= tune(TUNE_ENC_NT_MIN_N).load(std::memory_order_relaxed); }
 
 // resident workgroups of a persistent kernel on this device (occupancy x CUs)
 static uint32_t resident_grid(const void *fn, uint32_t lds, int fallback_per_cu, int num_cus) {
@@ -1382,7 +1434,7 @@ static uint32_t resident_grid(const void *fn, uint32_t lds, int fallback_per_cu,
 
 // the persistent sweeps' grids, once per context at creation (not lazily by concurrent launches)
 void configure_geom(LaunchGeom &g) {
-    g.enc_grid = resident_grid(reinterpret_cast<const void *>(ENC_SWEEP(false)), SWEEP_LDS, DECDS_ENC_WAVES, g.num_cus);
+    g.enc_grid = resident_grid(reinterpret_cast<const void *>(ENC_SWEEP(false, STORE_NT)), SWEEP_LDS, DECDS_ENC_WAVES, g.num_cus);
 #ifdef DECDS_SWEEP_GRID_PCT
     g.enc_grid = g.enc_grid * DECDS_SWEEP_GRID_PCT / 100;  // study builds: fewer resident workgroups than fit
 #endif
@@ -1407,8 +1459,10 @@ hipError_t launch_encode(const LaunchGeom &geom, const uint8_t *src, size_t n, c
     const uint32_t ne_want = small && DECDS_ENC_SMALL_EDGE ? (uint32_t)std::min<size_t>(n, EDGE_WGS) : 0u;
     const uint32_t ne = (uint64_t)n * T + ne_want <= cap ? ne_want : 0u;
     const uint32_t grid = tile_grid + ne;
+    const bool nt = encode_nt(n);
     const void *fn = small ? reinterpret_cast<const void *>(ENC_SMALL)
-                           : msg ? reinterpret_cast<const void *>(ENC_SWEEP(MSG_OK)) : reinterpret_cast<const void *>(ENC_SWEEP(false));
+                     : msg ? (nt ? reinterpret_cast<const void *>(ENC_SWEEP(MSG_OK, STORE_NT)) : reinterpret_cast<const void *>(ENC_SWEEP(MSG_OK, STORE_SC1)))
+                           : (nt ? reinterpret_cast<const void *>(ENC_SWEEP(false, STORE_NT)) : reinterpret_cast<const void *>(ENC_SWEEP(false, STORE_SC1)));
     uint32_t *counter = nullptr;  // none when every workgroup has one tile: no counter reset to launch
     if (DECDS_ENC_QUEUE && (uint64_t)n * T > tile_grid) {
         if (!geom.counters) return hipErrorInvalidValue;
@@ -1529,3 +1583,17 @@ hipError_t launch_fill_random(uint64_t seed, uint64_t byte_offset, uint8_t *dst,
 }
 
 }  // namespace decds
+
+#ifdef DECDS_PHASE_TRACE
+// study builds: copy out (and clear) the encode sweep's per-workgroup phase stamps
+extern "C" int decds_debug_phase_trace(uint64_t *out, int clear) {
+    using namespace decds;
+    hipError_t e = hipDeviceSynchronize();
+    if (e == hipSuccess && out) e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase_trace), sizeof(g_phase_trace), 0, hipMemcpyDeviceToHost);
+    if (e == hipSuccess && clear) {
+        static uint64_t zero[PT_WGS * PT_SLOTS];
+        e = hipMemcpyToSymbol(HIP_SYMBOL(g_phase_trace), zero, sizeof(zero), 0, hipMemcpyHostToDevice);
+    }
+    return (int)e;
+}
+#endif

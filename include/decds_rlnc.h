@@ -143,8 +143,9 @@ int decds_decode_batch(decds_ctx *ctx, const uint8_t *coded, size_t coded_pitch,
 const char *decds_decode_kernel_name(size_t n_chunksets);
 /* Launch-shape thresholds, process-wide (every form gives identical bytes; these only pick the faster
  * kernel form per batch size): "DECDS_DEC_SWEEP_MIN_N" (default 256: persistent decode sweep from
- * that many chunksets on) and "DECDS_ENC_SMALL_MAX_N" (default 2: encode batches up to that many
- * chunksets run 8-column tiles, twice as many workgroups). Each starts from the environment variable
+ * that many chunksets on), "DECDS_ENC_SMALL_MAX_N" (default 2: encode batches up to that many
+ * chunksets run 8-column tiles, twice as many workgroups) and "DECDS_ENC_NT_MIN_N" (default 256: from
+ * that many chunksets on the encode stores its coded rows non-temporal, below write-through). Each starts from the environment variable
  * of its name (read once, at first use) or the default. set != 0 sets it (value UINT64_MAX: back to
  * that start value). Returns the value in force, UINT64_MAX for an unknown name. */
 uint64_t decds_tuning(const char *name, uint64_t value, int set);

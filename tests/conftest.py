@@ -53,10 +53,13 @@ def decode_form(request):
     _tuning("DECDS_DEC_SWEEP_MIN_N", (1 << 64) - 1)
 
 
-@pytest.fixture(params=["cols16", "cols8"])
+@pytest.fixture(params=["cols16", "cols16_nt", "cols8"])
 def encode_form(request):
-    """Run an encoding test through both forms of the encode sweep: 16-column lane blocks (batches
-    above DECDS_ENC_SMALL_MAX_N) and the small-batch form's 8-column blocks, whatever the batch size."""
+    """Run an encoding test through every instantiation of the encode sweep whatever its batch size:
+    16-column lane blocks (batches above DECDS_ENC_SMALL_MAX_N) with write-through (below
+    DECDS_ENC_NT_MIN_N) or non-temporal coded-row stores, and the small-batch form's 8-column blocks."""
     _tuning("DECDS_ENC_SMALL_MAX_N", 1 << 62 if request.param == "cols8" else 0)
+    _tuning("DECDS_ENC_NT_MIN_N", 0 if request.param == "cols16_nt" else 1 << 62)
     yield request.param
     _tuning("DECDS_ENC_SMALL_MAX_N", (1 << 64) - 1)
+    _tuning("DECDS_ENC_NT_MIN_N", (1 << 64) - 1)

@@ -113,6 +113,9 @@ def test_decode_kernel_by_batch_size():
         assert tune("DECDS_DEC_SWEEP_MIN_N", 0, 0) == 1 << 40  # read only
         if "DECDS_ENC_SMALL_MAX_N" not in os.environ:
             assert tune("DECDS_ENC_SMALL_MAX_N", 0, 0) == 2
+        if "DECDS_ENC_NT_MIN_N" not in os.environ:
+            assert tune("DECDS_ENC_NT_MIN_N", 0, 0) == 256
+        assert tune("ENC_NT_MIN_N", 5) == 5 and tune("DECDS_ENC_NT_MIN_N", reset) != 5
         assert tune("NO_SUCH_KNOB", 5) == reset
     finally:
         tune("DECDS_DEC_SWEEP_MIN_N", reset)
