@@ -688,7 +688,7 @@ constexpr int STORE_SC1 = 16, STORE_NT = 2;
 // 100 MHz real-time counter at its phases — entry, edge pass done, first tables ready, last lookups
 // issued, stores drained — plus its tile count (vector stores; decds_debug_phase_trace copies them out).
 #ifdef DECDS_PHASE_TRACE
-constexpr uint32_t PT_WGS = 8192, PT_SLOTS = 8;
+constexpr uint32_t PT_WGS = 8192, PT_SLOTS = 24;  // slots 8 + k: tile k's tables ready (k < 16)
 __device__ uint64_t g_phase_trace[PT_WGS * PT_SLOTS];
 #define PT_SET(slot, v)                                                                   \
     do {                                                                                  \
@@ -795,6 +795,7 @@ void rlnc_encode_sweep_kernel(const uint8_t *__restrict__ src, size_t n, const u
         }
         lds_barrier();
 #ifdef DECDS_PHASE_TRACE
+        if (pt_tiles < 16) PT_STAMP(8 + pt_tiles);
         if (pt_tiles++ == 0) PT_STAMP(2);
 #endif
         const uint32_t tn = QUEUE ? s_next : t + G;
@@ -912,13 +913,14 @@ __global__ __launch_bounds__(WG) void rlnc_tail_scan_kernel(size_t n, const uint
 #ifndef DECDS_DEC_HB
 #define DECDS_DEC_HB 2  // decode lookup group size (bytes of an input dword per group)
 #endif
-#ifndef DECDS_DEC_STORE_AUX
-#define DECDS_DEC_STORE_AUX 0
-#endif
+// piece stores of the one-tile decode write-through (`sc1`) for batches of up to DEC_WT_MAX_N
+// chunksets: -4 % at 1 and 2 chunksets (end-of-kernel write-back, as the encode's), +1 % at 16,
+// +6 % at 103 and +8 % at 255 (r06r); plain stores above
+constexpr size_t DEC_WT_MAX_N = 2;
 #ifndef DECDS_DEC_DW
 #define DECDS_DEC_DW 4  // decode lane-block width in dwords (4: 16 columns per lane)
 #endif
-template <uint32_t UNIT>
+template <uint32_t UNIT, int SAUX = 0>
 __global__ __launch_bounds__(WG, DECDS_DEC_WAVES) __attribute__((amdgpu_waves_per_eu(DECDS_DEC_WAVES, DECDS_DEC_WAVES)))
 void rlnc_decode_kernel(const uint8_t *__restrict__ coded, size_t pitch, size_t n, const RepairPlan *__restrict__ plan,
                         uint8_t *__restrict__ dst, int32_t *__restrict__ status, const uint64_t *__restrict__ in_bases,
@@ -989,7 +991,7 @@ void rlnc_decode_kernel(const uint8_t *__restrict__ coded, size_t pitch, size_t 
     }
     // (realigning the piece stores — pieces start i bytes past alignment — through LDS staging or a DPP
     // wave shift measured 4-5 % slower / spilled: r02v/w)
-    stream_range<K, K, DW, DECDS_PREFETCH_FIRST, false, DECDS_DEC_HB, DECDS_DEC_STORE_AUX>(tile0, tile0 + UNIT, phase, ibase, ioff, obase, ooff, x);
+    stream_range<K, K, DW, DECDS_PREFETCH_FIRST, false, DECDS_DEC_HB, SAUX>(tile0, tile0 + UNIT, phase, ibase, ioff, obase, ooff, x);
 }
 
 // 3 waves/SIMD for the decode sweep: at 4 (128 VGPRs) its loop spills, the tile counter's pending
@@ -1360,6 +1362,7 @@ hipError_t configure_kernels() {
     const void *fns[] = {reinterpret_cast<const void *>(ENC_SWEEP(false, STORE_SC1)), reinterpret_cast<const void *>(ENC_SWEEP(MSG_OK, STORE_SC1)),
                          reinterpret_cast<const void *>(ENC_SWEEP(false, STORE_NT)), reinterpret_cast<const void *>(ENC_SWEEP(MSG_OK, STORE_NT)),
                          reinterpret_cast<const void *>(ENC_HASH), reinterpret_cast<const void *>(rlnc_decode_kernel<DEC_UNIT>),
+                         reinterpret_cast<const void *>(rlnc_decode_kernel<DEC_UNIT, STORE_SC1>),
                          reinterpret_cast<const void *>(DEC_SWEEP), reinterpret_cast<const void *>(ENC_SMALL)};
     for (const void *f : fns) {
         hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, std::max(SWEEP_LDS, FH_LDS<DECDS_FH_DW>));
@@ -1545,8 +1548,13 @@ static hipError_t launch_decode_kernel(const LaunchGeom &geom, const uint8_t *co
     }
     constexpr uint32_t U = DEC_UNIT;
     if (hipError_t p_ = hip_launch_begin("rlnc_decode_kernel")) return p_;
-    hipLaunchKernelGGL(rlnc_decode_kernel<U>, dim3((uint32_t)(n * (TILES<DECDS_DEC_DW> / U))), dim3(WG), DEC_LDS, stream, coded,
-                       pitch, n, pl, dst, status, in_bases, out_bases, poly, marker, info);
+    const dim3 grid((uint32_t)(n * (TILES<DECDS_DEC_DW> / U)));
+    if (n <= DEC_WT_MAX_N)
+        hipLaunchKernelGGL((rlnc_decode_kernel<U, STORE_SC1>), grid, dim3(WG), DEC_LDS, stream, coded, pitch, n, pl, dst,
+                           status, in_bases, out_bases, poly, marker, info);
+    else
+        hipLaunchKernelGGL(rlnc_decode_kernel<U>, grid, dim3(WG), DEC_LDS, stream, coded, pitch, n, pl, dst, status,
+                           in_bases, out_bases, poly, marker, info);
     return hipGetLastError();
 }
 

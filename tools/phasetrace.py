@@ -15,7 +15,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-PT_WGS, PT_SLOTS = 8192, 8
+PT_WGS, PT_SLOTS = 8192, 24
 
 
 def pct(v, qs=(0, 50, 90, 100)):
@@ -77,6 +77,8 @@ def main():
                    "drained": pct(us(4)[tile]),
                    "edge_wgs_drained": pct(us(4)[edge]),
                    "tiles_min_max": [int(s[tile, 5].min()), int(s[tile, 5].max())] if tile.any() else None,
+                   "round_start_p50": [round(float(np.median(us(8 + k)[tile & (s[:, 8 + k] > 0)])), 2)
+                                       for k in range(16) if (tile & (s[:, 8 + k] > 0)).sum() > len(s) // 2],
                    "span_us": round(float((s[:, 4].max() - t0) / 100.0), 2),
                    "algorithmic_frac_of_span": round(n * (CS + N * F) / ((s[:, 4].max() - t0) * 1e-8) / 8e12, 4)}
             print(json.dumps(rec), flush=True)
