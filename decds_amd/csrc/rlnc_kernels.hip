@@ -119,6 +119,31 @@ __device__ __forceinline__ uint32_t table_coeffs_all(const uint8_t *M, uint32_t 
     return live ? w : 0u;
 }
 
+// table_coeffs_all in two steps for a loop that loads the next tile's coefficients at its top and
+// builds their tables at the next iteration: the bytes (load) and, after the tile's lookups and stores
+// are issued, the word (pack). Packed where they are loaded, the scheduler puts the packing among the
+// first lookups, where waiting for the four byte loads — the latest vector memory operations issued —
+// is vmcnt(0): a wait for the previous tile's 16 stores as well, every tile (and, for a workgroup's
+// only tile, for all ten of its inputs before the first lookup).
+struct CoeffBytes {
+    uint32_t b[4];
+};
+template <int NIN, int NOUT>
+__device__ __forceinline__ CoeffBytes table_coeff_bytes(const uint8_t *M, uint32_t ldm) {
+    static_assert(NOUT == 16, "every coefficient word has 4 live outputs");
+    const uint32_t p = threadIdx.x < NIN * 8 ? threadIdx.x : 0u, q = p & 3u, i = p >> 3;
+    CoeffBytes c;
+#pragma unroll
+    for (uint32_t jj = 0; jj < 4; jj++) c.b[jj] = M[(4 * q + jj) * ldm + i];
+    return c;
+}
+template <int NIN>
+__device__ __forceinline__ uint32_t table_coeff_pack(CoeffBytes &c) {
+    asm volatile("" : "+v"(c.b[0]), "+v"(c.b[1]), "+v"(c.b[2]), "+v"(c.b[3]));
+    const uint32_t w = c.b[0] | (c.b[1] << 8) | (c.b[2] << 16) | (c.b[3] << 24);
+    return threadIdx.x < NIN * 8 ? w : 0u;
+}
+
 // table_coeffs_all for the decode sweep's loop, from the plan's input-major inverse (input i's
 // coefficients for outputs 0..9 are the 10 bytes at i * K): lane quad q's word is those of outputs
 // 4q..4q+3 — one dword load, not four byte loads (fewer registers pending across the lookups). It
@@ -790,7 +815,9 @@ void rlnc_encode_sweep_kernel(const uint8_t *__restrict__ src, size_t n, const u
     do {
         build_tables<K, N>(lds, cw, poly);
         if constexpr (QUEUE) {
-            asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+            // the counter's answer (with no counter — one tile per workgroup — grab is 0 and the
+            // lookups wait for each input as it is consumed, not for all ten ahead of the barrier)
+            if (counter) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
             if (threadIdx.x == 0) s_next = G + grab;
         }
         lds_barrier();
@@ -802,9 +829,10 @@ void rlnc_encode_sweep_kernel(const uint8_t *__restrict__ src, size_t n, const u
         grab = grab_next();
         more = tn < total;
         const uint32_t csn = more ? tn / T : cs;
-        cw = table_coeffs_all<K, N>(coeffs + (size_t)csn * N * K, K);
+        CoeffBytes cb = table_coeff_bytes<K, N>(coeffs + (size_t)csn * N * K, K);
         combine_block<K, N, DW, 0, NoSink, SAUX, true, DECDS_ENC_HB>(x, dst + (size_t)cs * N * pitch, ooff, col_of(t),
                                                                   src + (size_t)csn * CS, ioff, more ? col_of(tn) : OOB_COL);
+        cw = table_coeff_pack<K>(cb);
         lds_barrier();
         t = tn;
         cs = csn;
