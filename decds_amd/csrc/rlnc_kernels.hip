@@ -748,7 +748,11 @@ void rlnc_encode_sweep_kernel(const uint8_t *__restrict__ src, size_t n, const u
     const uint32_t NE = EDGE_SPLIT && gridDim.x > total ? (uint32_t)(gridDim.x - total) : 0u;
     const uint32_t G = gridDim.x - NE;  // tile workgroups
     const bool edge_wg = NE && blockIdx.x >= G;
+#ifdef DECDS_STUDY_NO_EDGE  // timing studies only: no edge pass at all (wrong bytes in the edge columns)
+    for (size_t cs = n; cs < n; cs++) {
+#else
     for (size_t cs = NE ? (edge_wg ? blockIdx.x - G : n) : blockIdx.x; cs < n; cs += NE ? NE : G) {
+#endif
         const uint8_t *M = coeffs + cs * N * K;
         const uint8_t *ibase = src + cs * CS;
         uint8_t *obase = dst + cs * N * pitch;

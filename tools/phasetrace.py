@@ -79,6 +79,11 @@ def main():
                    "tiles_min_max": [int(s[tile, 5].min()), int(s[tile, 5].max())] if tile.any() else None,
                    "round_start_p50": [round(float(np.median(us(8 + k)[tile & (s[:, 8 + k] > 0)])), 2)
                                        for k in range(16) if (tile & (s[:, 8 + k] > 0)).sum() > len(s) // 2],
+                   "by_tiles": {int(k): [int((tile & (s[:, 5] == k)).sum()),
+                                         round(float(np.median(us(3)[tile & (s[:, 5] == k)])), 2)]
+                                for k in sorted(set(s[tile, 5].tolist()))},
+                   "edge_wgs_first_tile_p50": round(float(np.median(us(2)[tile & (s[:, 1] - s[:, 0] > 200)])), 2)
+                   if (tile & (s[:, 1] - s[:, 0] > 200)).any() else None,
                    "span_us": round(float((s[:, 4].max() - t0) / 100.0), 2),
                    "algorithmic_frac_of_span": round(n * (CS + N * F) / ((s[:, 4].max() - t0) * 1e-8) / 8e12, 4)}
             print(json.dumps(rec), flush=True)
