@@ -362,3 +362,29 @@ def test_repairing_blob_two_decode_areas_any_fetch_order(ctx):
         assert rep.get_repaired_chunkset(c) == want(c), c
         assert rep.memory()["decode_areas"] == 2
     assert all(rep.is_chunkset_already_repaired(c) for c in range(n))
+
+
+def test_objects_built_on_temporary_contexts_stay_usable():
+    # Blob, RepairingBlob and RepairingChunkSet keep the contexts they were built on alive:
+    # built on contexts nobody else holds, they still work after a garbage collection
+    import gc
+    blob_len = CS + 12345
+    data = o.fill_random(0x7E4D, blob_len)
+    coeffs = o.fill_random(0x7E4E, 2 * N * K)
+    blob = decds_amd.Blob(decds_amd.Context(0), data, coeffs)
+    gc.collect()
+    header = blob.get_blob_header()
+    chunks = _all_chunks(blob)
+    rep = decds_amd.RepairingBlob([decds_amd.Context(0), decds_amd.Context(0)], header)
+    rcs = decds_amd.RepairingChunkSet(decds_amd.Context(0), 1)
+    gc.collect()
+    for ch in chunks:
+        if ch.get_chunkset_id() == 1 and not rcs.is_ready_to_repair():
+            rcs.add_chunk_unvalidated(ch)
+        for cid in (0, 1):
+            if ch.get_chunkset_id() == cid and not rep.is_chunkset_ready_to_repair(cid):
+                rep.add_chunk(ch)
+    gc.collect()
+    assert rep.get_repaired_chunkset(0) == data[:CS].tobytes()
+    assert rep.get_repaired_chunkset(1) == data[CS:].tobytes()
+    assert rcs.repair()[:blob_len - CS] == data[CS:].tobytes()
