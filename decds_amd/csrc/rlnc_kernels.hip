@@ -981,7 +981,6 @@ void rlnc_decode_kernel(const uint8_t *__restrict__ coded, size_t pitch, size_t 
     const uint32_t w1 = __builtin_amdgcn_readfirstlane(pw[1]);
     const uint32_t w2 = __builtin_amdgcn_readfirstlane(pw[2]);
     if (((w2 >> 16) & 0xFFu) != K) return;  // RepairPlan::rank at byte 10: not ready
-    const uint32_t cw = table_coeffs<K, K>(plan[cs].inv, 1, K);  // input-major inverse
     const uint32_t sel[K] = {w0 & 0xFFu, (w0 >> 8) & 0xFFu, (w0 >> 16) & 0xFFu, w0 >> 24,
                              w1 & 0xFFu, (w1 >> 8) & 0xFFu, (w1 >> 16) & 0xFFu, w1 >> 24,
                              w2 & 0xFFu, (w2 >> 8) & 0xFFu};
@@ -999,31 +998,43 @@ void rlnc_decode_kernel(const uint8_t *__restrict__ coded, size_t pitch, size_t 
         ibase = coded + (size_t)cs * N * pitch;
         obase = dst + (size_t)cs * CS;
     }
+    // the input-major inverse's coefficient words as one dword load each, ahead of the tile's loads so
+    // that the table build waits for it alone (the byte-wise table_coeffs, with a branch per output
+    // past 10, waited for each of its loads in turn: three HBM round trips before the tile's own loads
+    // were issued, r06z4)
+    const uint32_t cw = table_coeffs_imaj<K, K>(plan[cs].inv);
     Vec<DW> x[K];
     if constexpr (DECDS_PREFETCH_FIRST) load_block<K, DW>(x, ibase, ioff, tile_col<DW, false>(tile0, tile0 + UNIT, phase));
     if (tile0 == 0) tail_reset(s_tail);
     build_tables<K, K>(lds, cw, poly);
     lds_barrier();
-    if (tile0 == 0) {  // the whole workgroup: one pass over the edge columns
-        // the 10 bytes past the chunkset (piece 9's marker || zeros when intact) decide where
-        // get_decoded_data cuts (tail_note, chunkset.rs:202-204)
-        for (uint32_t idx = threadIdx.x; idx < edge_cols<DW, false>(phase) * K; idx += WG) {
-            const uint32_t i = idx % K, col = edge_col<DW, false>(idx / K, phase);
-            uint32_t z = 0;
+    auto edge_pass = [&]() {
+        // the workgroup of tile 0 makes one pass over the edge columns — after its tile, so that no
+        // branch ahead of the tile's stream merges memory-counter pictures (which had the lookups wait for
+        // all ten loads, vmcnt(0), instead of each as it is consumed). With the one-dword coefficient
+        // load: -6 / -6 / -2 % decode time at 1 / 16 / 64 chunksets, ±1 % at 103-255 (r06z4, r06z5)
+        if (tile0 == 0) {
+            // the 10 bytes past the chunkset (piece 9's marker || zeros when intact) decide where
+            // get_decoded_data cuts (tail_note, chunkset.rs:202-204)
+            for (uint32_t idx = threadIdx.x; idx < edge_cols<DW, false>(phase) * K; idx += WG) {
+                const uint32_t i = idx % K, col = edge_col<DW, false>(idx / K, phase);
+                uint32_t z = 0;
 #pragma unroll
-            for (uint32_t k = 0; k < K; k++) z ^= tbl_mul(lds, k, i, ibase[ioff[k] + col]);
-            const uint64_t p = (uint64_t)i * L + col;
-            if (p < CS)
-                obase[p] = (uint8_t)z;
-            else
-                tail_note(s_tail, p, z, marker);
+                for (uint32_t k = 0; k < K; k++) z ^= tbl_mul(lds, k, i, ibase[ioff[k] + col]);
+                const uint64_t p = (uint64_t)i * L + col;
+                if (p < CS)
+                    obase[p] = (uint8_t)z;
+                else
+                    tail_note(s_tail, p, z, marker);
+            }
+            lds_barrier();
+            tail_finish(s_tail, cs, status, info);
         }
-        lds_barrier();
-        tail_finish(s_tail, cs, status, info);
-    }
+    };
     // (realigning the piece stores — pieces start i bytes past alignment — through LDS staging or a DPP
     // wave shift measured 4-5 % slower / spilled: r02v/w)
     stream_range<K, K, DW, DECDS_PREFETCH_FIRST, false, DECDS_DEC_HB, SAUX>(tile0, tile0 + UNIT, phase, ibase, ioff, obase, ooff, x);
+    edge_pass();
 }
 
 // 3 waves/SIMD for the decode sweep: at 4 (128 VGPRs) its loop spills, the tile counter's pending
@@ -1104,7 +1115,7 @@ void rlnc_decode_sweep_kernel(const uint8_t *__restrict__ coded, size_t pitch, s
         d.load(plan, in_bases, out_bases, c);
         d.resolve(coded, dst, pitch, in_bases, c);
         if (!d.ready) continue;
-        const uint32_t cw = table_coeffs<K, K>(plan[c].inv, 1, K);  // input-major inverse
+        const uint32_t cw = table_coeffs_imaj<K, K>(plan[c].inv);  // input-major inverse, one dword load
         lds_barrier();  // also: the previous chunkset's tail_finish has read s_tail
         tail_reset(s_tail);
         build_tables<K, K>(lds + LDS_BYTES, cw, poly);
