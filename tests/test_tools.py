@@ -26,3 +26,14 @@ def test_tool_microbenchmarks_compile():
     with concurrent.futures.ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 1)) as ex:
         bad = [(os.path.basename(s), err) for s, rc, err in ex.map(check, srcs) if rc != 0]
     assert not bad, bad
+
+
+def test_study_builds_of_the_kernels_compile():
+    # the timing-study forms DESIGN.md §8 cites (per-workgroup phase trace, no edge pass) stay buildable
+    if not os.path.exists(HIPCC) and not shutil.which("hipcc"):
+        pytest.skip("hipcc not in this image")
+    src = os.path.join(ROOT, "decds_amd", "csrc", "rlnc_kernels.hip")
+    for defs in (["-DDECDS_PHASE_TRACE=1"], ["-DDECDS_PHASE_TRACE=1", "-DDECDS_STUDY_NO_EDGE=1"]):
+        r = subprocess.run([HIPCC, "--offload-arch=gfx950", "-std=c++17", "-I" + os.path.join(ROOT, "include"),
+                            "-fsyntax-only"] + defs + [src], capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, (defs, r.stderr[-1500:])
