@@ -1111,7 +1111,7 @@ int decds_repairing_blob_get_repaired_chunkset(decds_repairing_blob *rb, size_t 
                                chunkset_id, "invalid decoded data format");
     }
     // get_decoded_data's vector (cut at the last boundary marker: CS for any validated chunk set,
-    // rlnc_tail_scan_kernel) truncated to the chunkset's real size (blob.rs:464 truncates only)
+    // the decode kernels' tail_scan_decoded) truncated to the chunkset's real size (blob.rs:464 truncates only)
     const size_t len = std::min<size_t>(size, c.dec_len);
     HostUse uo(out, len);
     hipError_t e;

@@ -42,7 +42,8 @@ hipError_t launch_repair_plan(const uint8_t *coded, size_t pitch, size_t n, cons
 // in_bases / out_bases (device arrays of n addresses, or NULL): the gather form — chunkset c's
 // accepted rows at in_bases[c] + plan.sel[k]*pitch, its output at out_bases[c]. info (n x 16 B,
 // decds_repair_info, or NULL): get_decoded_data's length and the 10 decoded tail bytes of every
-// chunkset that decodes; the decode kernel is followed by rlnc_tail_scan_kernel on the same stream.
+// chunkset that decodes (the decode kernels' edge pass finds the cut, tail_scan_decoded when no tail
+// byte is the marker).
 hipError_t launch_decode(const LaunchGeom &g, const uint8_t *coded, size_t pitch, size_t n,
                          const uint8_t *plan, uint8_t *dst, int32_t *status, const uint64_t *in_bases,
                          const uint64_t *out_bases, uint32_t poly, uint32_t marker, uint8_t *info,

@@ -43,8 +43,8 @@ constexpr uint32_t TILE_BLOCKS = WG;                          // one 16-col bloc
 constexpr uint32_t ROW_BYTES = 16;                            // one nibble row: 16 outputs' products
 constexpr uint32_t TABLE_BYTES = 16 * ROW_BYTES;              // 16 nibble rows = 256 B = the 64 banks once
 constexpr uint32_t LDS_BYTES = K * 2 * TABLE_BYTES;           // 5 KiB
-constexpr uint32_t SWEEP_LDS = 2 * LDS_BYTES + 32;             // two table buffers + the next-tile slot + TailLds
-constexpr uint32_t DEC_LDS = LDS_BYTES + 16;                   // one-tile decode: tables + TailLds
+constexpr uint32_t SWEEP_LDS = 2 * LDS_BYTES + 48;             // two table buffers + the next-tile slot + TailLds
+constexpr uint32_t DEC_LDS = LDS_BYTES + 32;                   // one-tile decode: tables + TailLds
 // (the tables sit at LDS address 0 of the dynamic area: the inline-asm ds_read_b128 lookups address
 // them absolutely, so a kernel holding them must not declare static __shared__ variables — those
 // would be placed first and move the dynamic area)
@@ -862,73 +862,75 @@ void rlnc_encode_sweep_kernel(const uint8_t *__restrict__ src, size_t n, const u
 // boundary marker; no marker at all is an error (-> ChunksetRepairingFailed). An intact chunkset ends
 // in marker || 9 zeros, so its cut is at CS. The edge pass decodes the 10 tail bytes [CS, CS + 10)
 // (piece 9's last columns) and notes each and the highest marker among them in LDS (tail_note);
-// after a barrier tail_finish writes the repair info (decoded length, tail bytes) and, when no tail
-// byte is the marker, hands the chunkset to rlnc_tail_scan_kernel, which looks for the last marker
-// in the decoded bytes already in dst (only corrupted rows, accepted unvalidated, get there).
+// after a barrier, when no tail byte is the marker (only corrupted rows, accepted unvalidated, get
+// there), tail_scan_decoded looks for the last marker among the decoded bytes [0, CS), and
+// tail_finish writes the repair info (decoded length, tail bytes) and the status.
 struct TailLds {
     uint32_t cut;       // 1 + index of the last marker among the tail bytes, 0: none
     uint32_t bytes[3];  // the 10 tail bytes
+    uint32_t scan;      // 1 + position of the last marker in [0, CS) (tail_scan_decoded), 0: none
+    uint32_t pad[3];
 };
+constexpr uint32_t TAIL_LDS = sizeof(TailLds);
+static_assert(TAIL_LDS == 32, "LDS layout");
 __device__ __forceinline__ void tail_reset(TailLds &t) {
-    if (threadIdx.x < 4) reinterpret_cast<uint32_t *>(&t)[threadIdx.x] = 0;
+    if (threadIdx.x < TAIL_LDS / 4) reinterpret_cast<uint32_t *>(&t)[threadIdx.x] = 0;
 }
 __device__ __forceinline__ void tail_note(TailLds &t, uint64_t p, uint32_t z, uint32_t marker) {
     const uint32_t j = (uint32_t)(p - CS);
     reinterpret_cast<uint8_t *>(t.bytes)[j] = (uint8_t)z;
     if (z == marker) atomicMax(&t.cut, j + 1);
 }
-// after a barrier behind every tail_note; info: 4 dwords per chunkset (decds_repair_info)
+// The whole workgroup, after a barrier behind every tail_note; returns at once when a tail byte is
+// the marker. Otherwise the decoded bytes are decoded again here from the accepted rows (the
+// chunkset's tiles are being written by other workgroups at the same time), from the end of the
+// chunkset down, WG x 16 positions per step (4 positions per thread at a time: one round trip for
+// their 40 byte loads), until a step holds a marker. tbl: the decode tables (input k, output i).
+__device__ __forceinline__ void tail_scan_decoded(TailLds &t, const uint8_t *tbl, const uint8_t *ibase, const uint32_t (&ioff)[K],
+                                  uint32_t marker) {
+    if (__builtin_amdgcn_readfirstlane(t.cut)) return;
+    constexpr uint32_t STEP = WG * 16;
+    static_assert(CS % STEP == 0, "whole steps");
+    for (uint32_t blk = (uint32_t)CS; blk > 0;) {
+        blk -= STEP;
+        uint32_t h = 0;
+#pragma unroll 1
+        for (int g = 3; g >= 0; g--) {
+            const uint32_t b0 = blk + threadIdx.x * 16 + 4 * (uint32_t)g;
+            uint32_t xb[4][K];
+#pragma unroll
+            for (uint32_t b = 0; b < 4; b++)
+#pragma unroll
+                for (uint32_t k = 0; k < K; k++) xb[b][k] = ibase[ioff[k] + (b0 + b) % (uint32_t)L];
+#pragma unroll
+            for (uint32_t b = 0; b < 4; b++) {
+                const uint32_t p = b0 + b, i = p / (uint32_t)L;
+                uint32_t z = 0;
+#pragma unroll
+                for (uint32_t k = 0; k < K; k++) z ^= tbl_mul(tbl, k, i, xb[b][k]);
+                if (z == marker) h = h > p + 1 ? h : p + 1;
+            }
+        }
+        // (not __syncthreads_or: HIP's keeps a static __shared__ word, which would move the dynamic
+        // LDS area the tables' inline-asm reads address from byte 0)
+        if (h) atomicMax(&t.scan, h);
+        __syncthreads();
+        const uint32_t found = __builtin_amdgcn_readfirstlane(t.scan);
+        __syncthreads();  // every wave has read t.scan before a later step may raise it
+        if (found) return;
+    }
+}
+// after tail_scan_decoded; info: 4 dwords per chunkset (decds_repair_info)
 __device__ __forceinline__ void tail_finish(const TailLds &t, uint32_t c, int32_t *status, uint32_t *info) {
     if (threadIdx.x != 0) return;
     if (info) {
         uint32_t *o = info + 4 * (size_t)c;
-        o[0] = t.cut ? (uint32_t)CS + t.cut - 1 : 0u;
+        o[0] = t.cut ? (uint32_t)CS + t.cut - 1 : t.scan ? t.scan - 1 : 0u;
         o[1] = t.bytes[0];
         o[2] = t.bytes[1];
         o[3] = t.bytes[2];
     }
-    if (!t.cut) status[c] = (int32_t)TAIL_SCAN_STATUS;
-}
-
-// The backward marker scan for the chunksets tail_finish left at TAIL_SCAN_STATUS: a workgroup per
-// chunkset in turn (c = blockIdx.x, + gridDim.x, ...: at most one workgroup per CU is launched, so
-// an intact batch costs a launch and one status read per chunkset), 4 KiB of decoded bytes per step
-// from the end of the chunkset down; the highest marker position found is the decoded length, none
-// anywhere is ChunksetRepairingFailed.
-constexpr uint32_t TAIL_SCAN_GRID = 256;
-__global__ __launch_bounds__(WG) void rlnc_tail_scan_kernel(size_t n, const uint8_t *__restrict__ dst,
-                                                            int32_t *__restrict__ status,
-                                                            const uint64_t *__restrict__ out_bases,
-                                                            uint32_t *__restrict__ info, uint32_t marker) {
-    __shared__ uint32_t s_hit;
-    constexpr uint32_t STEP = WG * 16;
-    static_assert(CS % STEP == 0, "whole steps");
-    for (size_t c = blockIdx.x; c < n; c += gridDim.x) {
-        if (__builtin_amdgcn_readfirstlane(status[c]) != (int32_t)TAIL_SCAN_STATUS) continue;
-        const uint8_t *obase =
-            out_bases ? reinterpret_cast<const uint8_t *>(uniform_u64(out_bases[c])) : dst + c * CS;
-        if (threadIdx.x == 0) s_hit = 0;
-        __syncthreads();
-        uint32_t hit = 0;
-        for (uint32_t blk = (uint32_t)CS; blk > 0;) {
-            blk -= STEP;
-            const uint32_t b0 = blk + threadIdx.x * 16;
-            uint32_t h = 0;
-            for (int b = 15; b >= 0 && !h; b--)
-                if (obase[b0 + b] == marker) h = b0 + b + 1;
-            if (__syncthreads_or(h != 0)) {
-                if (h) atomicMax(&s_hit, h);
-                __syncthreads();
-                hit = s_hit;
-                break;
-            }
-        }
-        if (threadIdx.x == 0) {
-            status[c] = hit ? 0 : 6;  // DECDS_OK / DECDS_ERR_CHUNKSET_REPAIRING_FAILED
-            if (info) info[4 * c] = hit ? hit - 1 : 0u;
-        }
-        __syncthreads();  // every thread has read s_hit before the next chunkset resets it
-    }
+    if (!t.cut && !t.scan) status[c] = 6;  // DECDS_ERR_CHUNKSET_REPAIRING_FAILED: no marker anywhere
 }
 
 // Decode: workgroup = UNIT consecutive tiles of one chunkset. The accepted rows of chunkset cs are
@@ -1028,6 +1030,7 @@ void rlnc_decode_kernel(const uint8_t *__restrict__ coded, size_t pitch, size_t 
                     tail_note(s_tail, p, z, marker);
             }
             lds_barrier();
+            tail_scan_decoded(s_tail, lds, ibase, ioff, marker);
             tail_finish(s_tail, cs, status, info);
         }
     };
@@ -1133,6 +1136,7 @@ void rlnc_decode_sweep_kernel(const uint8_t *__restrict__ coded, size_t pitch, s
                 tail_note(s_tail, p, z, marker);
         }
         lds_barrier();
+        tail_scan_decoded(s_tail, lds + LDS_BYTES, d.ibase, d.ioff, marker);
         tail_finish(s_tail, c, status, info);
     }
     // 2. the sweep (tiles in runs per XCD, each XCD with its own counter — rlnc_decode_kernel's
@@ -1606,13 +1610,9 @@ hipError_t launch_decode(const LaunchGeom &geom, const uint8_t *coded, size_t pi
                          uint32_t poly, uint32_t marker, uint8_t *info, hipStream_t stream) {
     if (n == 0) return hipSuccess;
     uint32_t *inf = reinterpret_cast<uint32_t *>(info);
-    hipError_t e = launch_decode_kernel(geom, coded, pitch, n, plan, dst, status, in_bases, out_bases, poly, marker, inf, stream);
-    if (e != hipSuccess) return e;
-    // get_decoded_data's cut for the chunksets whose tail bytes hold no marker (rlnc_tail_scan_kernel)
-    if (hipError_t p_ = hip_launch_begin("rlnc_tail_scan_kernel")) return p_;
-    hipLaunchKernelGGL(rlnc_tail_scan_kernel, dim3((uint32_t)std::min<size_t>(n, TAIL_SCAN_GRID)), dim3(WG), 0, stream, n,
-                       dst, status, out_bases, inf, marker);
-    return hipGetLastError();
+    // get_decoded_data's cut, the repair info and the status come from the decode kernels' edge pass
+    // (tail_scan_decoded for the chunksets whose tail bytes hold no marker): one launch
+    return launch_decode_kernel(geom, coded, pitch, n, plan, dst, status, in_bases, out_bases, poly, marker, inf, stream);
 }
 
 hipError_t launch_fill_random(uint64_t seed, uint64_t byte_offset, uint8_t *dst, size_t nbytes,

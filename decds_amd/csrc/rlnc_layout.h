@@ -27,11 +27,6 @@ constexpr uint32_t TAIL_COLS = (uint32_t)L - MAIN_COLS;     // 17
 static_assert(MAIN_COLS + TAIL_COLS == L, "tiling covers the piece");
 static_assert((K - 1) * L + MAIN_COLS <= CS, "main loop never reads piece 9's marker/padding");
 
-// Internal per-chunkset status between the decode kernel's edge pass and rlnc_tail_scan_kernel (no
-// marker among the 10 decoded tail bytes: the cut is searched for in the decoded data); never
-// returned to a caller — launch_decode always runs the scan behind the decode.
-constexpr uint32_t TAIL_SCAN_STATUS = 0x7A115CA9u;
-
 // Decode plan, one per chunkset (written by the plan kernel, read by the decode kernel).
 struct alignas(16) RepairPlan {
     uint8_t sel[K];      // coded-row index (0..15) of the k-th accepted chunk, acceptance order
