@@ -430,9 +430,22 @@ def main():
             stream.synchronize()
             ms = float(np.median([a.elapsed_time(b) for a, b in sev]))
             gbs = ns * (CS + N * F) / (ms * 1e-3) / 1e9
-            sweep.append({"chunksets": ns, "kernel": _lib().decds_encode_kernel_name(ns).decode(),
-                          "encode_ms": round(ms, 4), "launches": reps, "encode_GBps": round(gbs, 1),
-                          "frac": round(gbs / HBM_PEAK_GBS, 4), "blob_GiBps": round(ns * CS / GIB / (ms * 1e-3), 1)})
+            rec = {"chunksets": ns, "kernel": _lib().decds_encode_kernel_name(ns).decode(),
+                   "encode_ms": round(ms, 4), "launches": reps, "encode_GBps": round(gbs, 1),
+                   "frac": round(gbs / HBM_PEAK_GBS, 4), "blob_GiBps": round(ns * CS / GIB / (ms * 1e-3), 1)}
+            if ns <= 64:
+                # beside it (not instead): a stream of back-to-back launches between one event pair, the
+                # shape of many small encode calls in a row (each launch's dispatch behind the previous one)
+                b0, b1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                b0.record(stream)
+                for _ in range(4 * reps):
+                    codec.encode_batch(ctx, big, ns, cbig, obig, bpitch, stream=stream)
+                b1.record(stream)
+                stream.synchronize()
+                sms = b0.elapsed_time(b1) / (4 * reps)
+                rec["stream"] = {"launches": 4 * reps, "encode_ms": round(sms, 4),
+                                 "frac": round(ns * (CS + N * F) / (sms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+            sweep.append(rec)
         del big, cbig, obig
 
     enc_bytes = n * (CS + N * F)            # algorithmic HBM bytes of one encode launch
