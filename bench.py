@@ -111,7 +111,8 @@ def cpu_baseline(n_sample, seed, repeats=5, cfg2_chunksets=103):
     Headline = the strongest restatement: column-blocked GFNI affine multiplies on AVX-512
     (oracle/rlnc_cpu_fast.c; coefficient-only rank + inverse, then one blocked pass for the repair),
     the median of `repeats` runs (each at least 1 s of passes over the sample) with their spread. Beside it (BASELINE.md's plan): the same codec on
-    1 thread, and on config 2's sample (the 1 GiB blob's 103 chunksets) with all threads; one run
+    1 thread, on config 2's sample (the 1 GiB blob's 103 chunksets) with all threads and on config 1's
+    single chunkset (one thread: the work is chunkset-parallel); one run
     each of the row-pass forms (AVX2 nibble tables; the scalar table-driven loop rlnc 0.4.0 is
     recalled to use). All produce the same bytes (tests/test_oracle.py)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -184,6 +185,12 @@ def cpu_baseline(n_sample, seed, repeats=5, cfg2_chunksets=103):
                                          for _ in range(max(1, repeats))])), cores=threads,
                              sample="%d chunksets%s, %d threads" % (cfg2_chunksets, cfg2_tag, threads))
         del smp2
+        # config 1: one chunkset (chunkset-parallel, so one thread does all of it), median of repeats
+        smp1 = sample(1, seed + 3)
+        extra["cfg1"] = dict(rnd(median([run(o.fast_blob_encode, o.fast_blob_repair, smp1, 1, min_s=0.5)
+                                         for _ in range(max(1, repeats))])), cores=1,
+                             sample="1 chunkset (config 1), 1 thread")
+        del smp1
     else:
         head_name = max(rows, key=lambda k: rows[k]["value"])
         head = dict(rows[head_name], runs=1, spread=None)
