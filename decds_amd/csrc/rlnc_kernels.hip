@@ -17,9 +17,12 @@
 // accumulation into a 16x16 byte block (columns x outputs), a v_perm byte transpose, 16 (or 10)
 // 16-B stores. No MFMA: this is byte-wise finite-field work, bounded by HBM bandwidth.
 //
-// Only the shipped configuration lives here. The round-1 study variants (persistent walks, XCD
-// bands, per-half work shares, per-tile barriers, the warp-specialised kernel, timing hooks) are in
-// git history (tools/study/rlnc_kernels_r01_study.hip at a5d9101) with their measurements in DESIGN.md §8.
+// Only the shipped configuration lives here, plus two study hooks that compile to nothing by default
+// (DECDS_PHASE_TRACE: per-workgroup phase stamps of the encode sweep for tools/phasetrace.py;
+// DECDS_STUDY_NO_EDGE: the encode without its edge pass, timing only). The round-1 study variants
+// (persistent walks, XCD bands, per-half work shares, per-tile barriers, the warp-specialised kernel)
+// are in git history (tools/study/rlnc_kernels_r01_study.hip at a5d9101) with their measurements in
+// DESIGN.md §8.
 #include <hip/hip_runtime.h>
 #include <cstdlib>
 #include <cstring>
