@@ -6,9 +6,11 @@ decds_amd/csrc/rlnc_kernels.hip) bump their tile counter with an inline-asm
 still pending; the kernels wait for it themselves, a step later, with `s_waitcnt vmcnt(N)` (N = the
 memory operations issued after it). That is only sound while the compiler neither reads nor copies
 nor spills that VGPR before such a wait — a property of the generated code, so it is checked on the
-generated code: for every returning atomic, scanning forward in program order, the first
-instruction that names its destination register must come after a vmcnt wait that covers the
-atomic (count <= memory operations issued since).
+generated code: for every returning atomic, on every control-flow path from it (branches followed,
+both ways for conditional ones, loops until the counts repeat), the first instruction that names its
+destination register must come after a vmcnt wait that covers the atomic (count <= memory
+operations issued since). (A scan in program order was enough until the compiler placed a loop's
+tail after its atomic: the scan then walked past an `s_branch` into the epilogue.)
 """
 import os
 import re
@@ -41,7 +43,7 @@ def _device_code(tmp_path):
 
 
 def _functions(text):
-    """{symbol: [instruction lines]} of the disassembly."""
+    """{symbol: [(byte address, instruction)]} of the disassembly."""
     funcs, cur = {}, None
     for line in text.splitlines():
         m = re.match(r"^[0-9a-f]+ <(.+)>:$", line)
@@ -49,9 +51,11 @@ def _functions(text):
             cur = funcs.setdefault(m.group(1), [])
             continue
         if cur is not None:
-            ins = line.split("//")[0].strip()
-            if ins and not ins.endswith(":"):
-                cur.append(ins)
+            parts = line.split("//")
+            ins = parts[0].strip()
+            am = re.match(r"\s*([0-9A-Fa-f]+):", parts[1]) if len(parts) > 1 else None
+            if ins and not ins.endswith(":") and am:
+                cur.append((int(am.group(1), 16), ins))
     return funcs
 
 
@@ -64,26 +68,46 @@ def _names_vgpr(ins, reg):
     return False
 
 
-def _unsafe_uses(ins_list):
-    """(atomic index, offending instruction) for every returning atomic read too early."""
+def _successors(fn, idx, at):
+    """instruction indices that can follow fn[idx] (s_branch: its target; s_cbranch_*: both)."""
+    addr, ins = fn[idx]
+    op = ins.split()[0]
+    if op in ("s_endpgm", "s_setpc_b64", "s_swappc_b64"):
+        return []
+    nxt = [idx + 1] if idx + 1 < len(fn) else []
+    if op == "s_branch" or op.startswith("s_cbranch"):
+        simm = int(ins.split()[1], 0) & 0xFFFF
+        simm -= 0x10000 if simm & 0x8000 else 0
+        tgt = at.get(addr + 4 + 4 * simm)
+        tgts = [tgt] if tgt is not None else []
+        return tgts if op == "s_branch" else nxt + tgts
+    return nxt
+
+
+def _unsafe_uses(fn):
+    """(atomic index, offending instruction) for every returning atomic read too early on some path."""
+    at = {a: i for i, (a, _) in enumerate(fn)}
     bad = []
-    for i, ins in enumerate(ins_list):
+    for i, (_, ins) in enumerate(fn):
         m = re.match(r"^global_atomic_add v(\d+), .*\bsc0\b", ins)
         if not m:
             continue
-        reg, issued = int(m.group(1)), 0
-        for nxt in ins_list[i + 1:]:
+        reg = int(m.group(1))
+        seen, stack = set(), [(j, 0) for j in _successors(fn, i, at)]
+        while stack and not bad:
+            j, issued = stack.pop()
+            if (j, issued) in seen:
+                continue
+            seen.add((j, issued))
+            nxt = fn[j][1]
             w = re.search(r"s_waitcnt\b.*\bvmcnt\((\d+)\)", nxt)
             if w and int(w.group(1)) <= issued:
-                break  # the atomic has landed
-            op = nxt.split()[0]
+                continue  # the atomic has landed on this path
             if _names_vgpr(nxt, reg) and not w:
                 bad.append((i, nxt))
                 break
-            if op.startswith(VMEM):
-                issued += 1
-            if op == "s_endpgm":
-                break
+            inc = 1 if nxt.split()[0].startswith(VMEM) else 0
+            stack.extend((k, min(issued + inc, 64)) for k in _successors(fn, j, at))
     return bad
 
 
@@ -95,7 +119,7 @@ def test_counter_atomics_are_waited_for_before_use(tmp_path):
     assert any("encode_sweep" in k for k in sweeps), sorted(funcs)[:20]
     checked = 0
     for name, ins in sweeps.items():
-        checked += sum(1 for x in ins if re.match(r"^global_atomic_add v\d+, .*\bsc0\b", x))
+        checked += sum(1 for _, x in ins if re.match(r"^global_atomic_add v\d+, .*\bsc0\b", x))
         assert not _unsafe_uses(ins), (name, _unsafe_uses(ins))
     assert checked >= 2
 
@@ -108,7 +132,20 @@ def test_checker_flags_an_early_read():
     late = ["global_atomic_add v7, v[0:1], v2, off sc0", "buffer_load_dwordx4 v[8:11], v3, s[0:3], 0 offen",
             "s_waitcnt vmcnt(1)", "v_mov_b32_e32 v12, v7"]
     ranged = ["global_atomic_add v7, v[0:1], v2, off sc0", "scratch_store_dwordx2 off, v[6:7], off offset:4"]
-    assert _unsafe_uses(early) and not _unsafe_uses(late) and _unsafe_uses(ranged)
+    # control flow: an early read jumped over (s_branch) is not on the path; one on either side of a
+    # conditional branch is
+    jumped = ["global_atomic_add v7, v[0:1], v2, off sc0", "s_branch 1", "v_mov_b32_e32 v12, v7", "s_waitcnt vmcnt(0)",
+              "v_mov_b32_e32 v12, v7", "s_endpgm"]
+    either = ["global_atomic_add v7, v[0:1], v2, off sc0", "s_cbranch_scc1 1", "v_mov_b32_e32 v12, v7", "s_waitcnt vmcnt(0)",
+              "s_endpgm"]
+    def fn(xs):  # byte addresses: 8-byte memory instructions, 4-byte others (branch offsets count dwords)
+        out, a = [], 0
+        for x in xs:
+            out.append((a, x))
+            a += 8 if x.startswith(VMEM) else 4
+        return out
+    assert _unsafe_uses(fn(early)) and not _unsafe_uses(fn(late)) and _unsafe_uses(fn(ranged))
+    assert not _unsafe_uses(fn(jumped)) and _unsafe_uses(fn(either))
 
 
 def _kernel_notes(tmp_path):
