@@ -793,9 +793,6 @@ void rlnc_encode_sweep_kernel(const uint8_t *__restrict__ src, size_t n, const u
     uint32_t cs = t / T;
     // prologue = the loop's memory-counter picture at its head: this tile's coefficient bytes, its
     // inputs, then 16 dropped stores
-    uint32_t cw = table_coeffs_all<K, N>(coeffs + (size_t)cs * N * K, K);
-    Vec<DW> x[K];
-    load_block<K, DW>(x, src + (size_t)cs * CS, ioff, col_of(t));
     // The tile counter is bumped by inline asm: a compiler-visible atomic's result becomes a phi at the
     // end of the lane-0 branch, where hipcc waits for it with vmcnt(0) — i.e. for every store in
     // flight. Here it is waited for explicitly, a step later, with vmcnt(16): this step's 16 stores
@@ -807,7 +804,14 @@ void rlnc_encode_sweep_kernel(const uint8_t *__restrict__ src, size_t n, const u
             asm volatile("global_atomic_add %0, %1, %2, off sc0" : "=v"(r) : "v"(counter), "v"(1u) : "memory");
         return r;
     };
+    // the first grab goes ahead of the tile's coefficient and input loads, so that the first loop head
+    // waits for it (and the coefficients) with vmcnt(26) — the ten input loads and 16 dropped stores
+    // still in flight — and the first tile's lookups take each input as it lands
     uint32_t grab = grab_next();  // -> the tile after the next
+    asm volatile("" ::: "memory");
+    uint32_t cw = table_coeffs_all<K, N>(coeffs + (size_t)cs * N * K, K);
+    Vec<DW> x[K];
+    load_block<K, DW>(x, src + (size_t)cs * CS, ioff, col_of(t));
     asm volatile("" ::: "memory");
 #pragma unroll
     for (int j = 0; j < (int)N; j++) strow<DW>(dst, ooff[j], OOB_COL, Vec<DW>{});
@@ -818,15 +822,22 @@ void rlnc_encode_sweep_kernel(const uint8_t *__restrict__ src, size_t n, const u
     lds_barrier();  // the edge pass's table readers are done
     uint32_t &s_next = *reinterpret_cast<uint32_t *>(lds + 2 * LDS_BYTES);
     uint32_t more;
+    bool first = true;
 #pragma unroll 1
     do {
         build_tables<K, N>(lds, cw, poly);
         if constexpr (QUEUE) {
-            // the counter's answer (with no counter — one tile per workgroup — grab is 0 and the
-            // lookups wait for each input as it is consumed, not for all ten ahead of the barrier)
-            if (counter) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+            // the counter's answer: at the first tile everything but its ten input loads and the 16
+            // dropped stores, later everything but the previous tile's 16 stores (waited for whether
+            // or not a counter was passed — with none, one tile per workgroup, grab is 0 — so that on
+            // every path the pending atomic register is read after its wait: tests/test_isa.py)
+            if (first)
+                asm volatile("s_waitcnt vmcnt(26)" ::: "memory");
+            else
+                asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
             if (threadIdx.x == 0) s_next = G + grab;
         }
+        first = false;
         lds_barrier();
 #ifdef DECDS_PHASE_TRACE
         if (pt_tiles < 16) PT_STAMP(8 + pt_tiles);
