@@ -80,6 +80,23 @@ def test_encode_every_column_phase(ctx):
             assert np.array_equal(coded[c * N:(c + 1) * N], refs[c]), (off, c)
 
 
+@pytest.mark.usefixtures("encode_form")
+@pytest.mark.parametrize("n", [1, 16])
+def test_encode_small_batches_match_oracle(ctx, n):
+    # the small-batch sizes of the bench's sweep through every encode form, in the
+    # bench's payload-aligned layout: first, middle and last chunkset against the oracle
+    data = o.fill_random(0xDEC05016 + n, n * CS)
+    coeffs = o.fill_random(0xC0EF0016 + n, n * N * K)
+    src, cv = dev(data), dev(coeffs)
+    dst, pitch = codec.coded_buffer(n)
+    codec.encode_batch(ctx, src, n, cv, dst, pitch)
+    out = host(dst)
+    for c in sorted({0, n // 2, n - 1}):
+        ref = o.chunkset_encode(data[c * CS:(c + 1) * CS], coeffs[c * 160:(c + 1) * 160], nthreads=8)
+        rows = np.stack([out[(c * N + j) * pitch:(c * N + j) * pitch + F] for j in range(N)])
+        assert np.array_equal(rows, ref), c
+
+
 @pytest.mark.usefixtures("decode_form")
 def test_encode_decode_at_the_largest_pitch(ctx):
     # a chunkset's 16 rows must fit one 2 GiB buffer descriptor (include/decds_rlnc.h): the largest
