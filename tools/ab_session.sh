@@ -16,6 +16,11 @@ set -o pipefail
 out=${1:?outdir}; shift
 mkdir -p "$out"
 export TMPDIR=/tmp
+# a line every minute under $out: the first `import torch` on a fresh box can take minutes without
+# output, which the GPU service takes for a hang (every step still has its own time limit)
+( while sleep 60; do date +%T >> "$out/heartbeat"; done ) &
+hb=$!
+trap 'kill $hb 2>/dev/null' EXIT
 fail() { echo "$1 FAILED"; tail -30 "$2"; exit 1; }
 for step in "$@"; do
   kind=${step%%:*}; arg=${step#*:}
