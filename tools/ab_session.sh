@@ -33,6 +33,15 @@ for step in "$@"; do
     ab|fuse)
       sizes=${arg%%:*}; libs=${arg#*:}; tool=tools/abbench.py; extra="--check"
       [ "$kind" = fuse ] && { tool=tools/fusebench.py; extra=""; }
+      # every variant build passes the static ISA checks (no static LDS under the tables, no spills, the
+      # tile counter's pending register read only after its wait) before it runs: a variant that
+      # spilled that register hung a box's A/B (r06z14)
+      for spec in ${libs//,/ }; do
+        lib=${spec%%[:@]*}
+        [ "$lib" = default ] && continue
+        DECDS_LIB=$lib timeout -k 10 300 python -m pytest tests/test_isa.py -q -p no:cacheprovider > "$out/isa_$(basename "$lib" .so).log" 2>&1 \
+          || fail "isa check of $lib" "$out/isa_$(basename "$lib" .so).log"
+      done
       for n in ${sizes//,/ }; do
         timeout -k 10 300 python -u $tool $extra --n "$n" --rounds 12 ${libs//,/ } >> "$out/$kind.jsonl" 2>> "$out/$kind.err" || fail "$kind n=$n" "$out/$kind.err"
       done
