@@ -64,6 +64,8 @@ def parse(argv=None):
     p.add_argument("--no-commit", action="store_true", help="skip timing the commitment kernels (row f1)")
     p.add_argument("--no-sweep", action="store_true", help="skip the encode batch sweep (256..1639 chunksets)")
     p.add_argument("--cpu-sample", type=int, default=0, help="chunksets in the CPU sample (0 = auto)")
+    p.add_argument("--no-extras", action="store_true",
+                   help="skip the pattern ceilings and the end-to-end (PCIe-inclusive) host-path rate")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
     p.add_argument("--rehearse-shard", default=None, metavar="R/W", type=shard_arg,
                    help="one process, no process group: run only rank R's shard of a W-GPU job on this GPU "
@@ -76,14 +78,32 @@ def parse(argv=None):
     return p.parse_args(argv)
 
 
-def cpu_threads():
-    """the host threads the CPU baseline uses: the CPUs this process may run on, at most 16 (the GPU
-    box's CPU share; os.cpu_count() reports the whole machine there)"""
+def usable_cpus():
+    """the CPUs this process may run on (sched affinity; os.cpu_count() if unavailable)"""
     try:
-        avail = len(os.sched_getaffinity(0))
+        return len(os.sched_getaffinity(0))
     except (AttributeError, OSError):
-        avail = os.cpu_count() or 1
-    return max(1, min(16, avail))
+        return os.cpu_count() or 1
+
+
+def cgroup_cpus():
+    """the cgroup v2 CPU quota in CPUs (cpu.max "quota period"), None when unlimited or unreadable"""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        return None if quota == "max" else int(quota) / int(period)
+    except (OSError, ValueError):
+        return None
+
+
+def cpu_threads():
+    """the thread counts the CPU baseline measures: all usable CPUs (rayon's pool on every core,
+    blob.rs:256-264), the count Rust's available_parallelism() — rayon's default pool size — gives
+    (usable CPUs capped by the cgroup quota), and 16 (the box's nominal CPU share per GPU)"""
+    allc = max(1, usable_cpus())
+    q = cgroup_cpus()
+    rayon = max(1, min(allc, int(-(-q // 1)))) if q else allc
+    return {"all_cores": allc, "rayon_default": rayon, "threads_16": min(16, allc)}
 
 
 def host_cpu():
@@ -97,30 +117,32 @@ def host_cpu():
                     break
     except OSError:
         pass
-    try:
-        affinity = len(os.sched_getaffinity(0))
-    except (AttributeError, OSError):
-        affinity = None
-    return {"model": model, "cpus_online": os.cpu_count(), "cpus_usable": affinity}
+    return {"model": model, "cpus_online": os.cpu_count(), "cpus_usable": usable_cpus(), "cgroup_cpu_quota": cgroup_cpus()}
 
 
 def cpu_baseline(n_sample, seed, repeats=5, cfg2_chunksets=103):
     """The CPU restatement (oracle/, "port") on the host cores: chunkset-parallel encode
     (blob.rs:256-264) + per-chunkset repair from 10 survivors (chunkset.rs:173-208).
 
-    Headline = the strongest restatement: column-blocked GFNI affine multiplies on AVX-512
+    Codec = the strongest restatement: column-blocked GFNI affine multiplies on AVX-512
     (oracle/rlnc_cpu_fast.c; coefficient-only rank + inverse, then one blocked pass for the repair),
-    the median of `repeats` runs (each at least 1 s of passes over the sample) with their spread. Beside it (BASELINE.md's plan): the same codec on
-    1 thread, on config 2's sample (the 1 GiB blob's 103 chunksets) with all threads and on config 1's
-    single chunkset (one thread: the work is chunkset-parallel); one run
-    each of the row-pass forms (AVX2 nibble tables; the scalar table-driven loop rlnc 0.4.0 is
-    recalled to use). All produce the same bytes (tests/test_oracle.py)."""
+    the median of `repeats` runs (each at least 1 s of passes over the sample) with their spread, at
+    each of the thread counts cpu_threads() names: `all_cores` (every usable CPU — the reference's
+    shape, rayon over all cores), `rayon_default` (what rayon's default pool takes: usable CPUs capped
+    by the cgroup quota; measured only when it differs) and `threads_16`. The sample holds at least
+    one chunkset per thread. `value` is the strongest of them (its thread count in `cores`): the
+    GPU/CPU ratio is quoted against the fastest CPU configuration measured. Beside it (BASELINE.md's
+    plan): the same codec on 1 thread, on config 2's sample (the 1 GiB blob's 103 chunksets) with all
+    cores and on config 1's single chunkset (one thread: the work is chunkset-parallel); one run each
+    of the row-pass forms (AVX2 nibble tables; the scalar table-driven loop rlnc 0.4.0 is recalled to
+    use) on 16 threads. All produce the same bytes (tests/test_oracle.py)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import numpy as np
     import oracle as o
-    threads = cpu_threads()
+    counts = cpu_threads()
+    allc, t16 = counts["all_cores"], counts["threads_16"]
     if n_sample <= 0:
-        n_sample = 16 * threads
+        n_sample = max(256, allc)  # >= one chunkset per thread
 
     def sample(n, sd):
         blob = o.fill_random(sd, n * o.CS)
@@ -165,43 +187,156 @@ def cpu_baseline(n_sample, seed, repeats=5, cfg2_chunksets=103):
                                               round(max(r["value"] for r in runs), 2)]}
 
     smp = sample(n_sample, seed)
+    desc = lambda n, th: "%d chunksets (%.0f MiB) encode + repair from 10 survivors, %d threads (chunkset-parallel)" % (
+        n, n * o.CS / 2 ** 20, th)
     rows = {}
     o.set_simd(0)
-    rows["scalar tables, row passes"] = run(o.blob_encode, o.blob_repair, smp, threads)
+    rows["scalar tables, row passes"] = dict(rnd(run(o.blob_encode, o.blob_repair, smp, t16)), cores=t16)
     if o.set_simd(1):
-        rows["avx2 nibble tables, row passes"] = run(o.blob_encode, o.blob_repair, smp, threads)
+        rows["avx2 nibble tables, row passes"] = dict(rnd(run(o.blob_encode, o.blob_repair, smp, t16)), cores=t16)
     o.set_simd(0)
     extra = {}
-    if o.fast_supported():
-        head_name = "avx512 gfni affine, column-blocked"
-        head = median([run(o.fast_blob_encode, o.fast_blob_repair, smp, threads, min_s=1.0)
-                       for _ in range(max(1, repeats))])
-        del smp
-        smp2 = sample(cfg2_chunksets, seed + 2)
-        cfg2_tag = " (config 2: the 1 GiB blob)" if cfg2_chunksets == 103 else ""
-        extra["threads_1"] = dict(rnd(run(o.fast_blob_encode, o.fast_blob_repair, smp2, 1, min_s=1.0)), cores=1,
-                                  sample="%d chunksets%s, 1 thread" % (cfg2_chunksets, cfg2_tag))
-        extra["cfg2"] = dict(rnd(median([run(o.fast_blob_encode, o.fast_blob_repair, smp2, threads, min_s=1.0)
-                                         for _ in range(max(1, repeats))])), cores=threads,
-                             sample="%d chunksets%s, %d threads" % (cfg2_chunksets, cfg2_tag, threads))
-        del smp2
-        # config 1: one chunkset (chunkset-parallel, so one thread does all of it), median of repeats
-        smp1 = sample(1, seed + 3)
-        extra["cfg1"] = dict(rnd(median([run(o.fast_blob_encode, o.fast_blob_repair, smp1, 1, min_s=0.5)
-                                         for _ in range(max(1, repeats))])), cores=1,
-                             sample="1 chunkset (config 1), 1 thread")
-        del smp1
-    else:
+    if not o.fast_supported():
         head_name = max(rows, key=lambda k: rows[k]["value"])
         head = dict(rows[head_name], runs=1, spread=None)
-    return dict({"value": round(head["value"], 2), "unit": "GiB/s", "cores": threads, "kind": "port",
-                 "variant": head_name, "median_of": head["runs"], "passes": head.get("passes", 1),
-                 "spread": head["spread"],
-                 "sample": "%d chunksets (%.0f MiB) encode + repair from 10 survivors, %d threads (chunkset-parallel)"
-                           % (n_sample, n_sample * o.CS / 2 ** 20, threads),
-                 "encode_gib_s": round(head["encode_gib_s"], 2), "repair_gib_s": round(head["repair_gib_s"], 2),
-                 "host": host_cpu(),
-                 "other_variants": {k: rnd(v) for k, v in rows.items()}}, **extra)
+        return {"value": head["value"], "unit": "GiB/s", "cores": t16, "kind": "port", "variant": head_name,
+                "sample": desc(n_sample, t16), "host": host_cpu(), "thread_counts": counts, "other_variants": rows}
+    head_name = "avx512 gfni affine, column-blocked"
+    measured = {}
+    for key in ("all_cores", "rayon_default", "threads_16"):
+        th = counts[key]
+        same = [k for k, v in measured.items() if v["cores"] == th]
+        if same:  # the same thread count as a figure already measured
+            extra[key] = {"same_as": same[0], "cores": th}
+            continue
+        m = median([run(o.fast_blob_encode, o.fast_blob_repair, smp, th, min_s=1.0) for _ in range(max(1, repeats))])
+        measured[key] = dict(rnd(m), cores=th, sample=desc(n_sample, th))
+        extra[key] = measured[key]
+    best = max(measured, key=lambda k: measured[k]["value"])
+    head = measured[best]
+    del smp
+    smp2 = sample(cfg2_chunksets, seed + 2)
+    cfg2_tag = " (config 2: the 1 GiB blob)" if cfg2_chunksets == 103 else ""
+    extra["threads_1"] = dict(rnd(run(o.fast_blob_encode, o.fast_blob_repair, smp2, 1, min_s=1.0)), cores=1,
+                              sample="%d chunksets%s, 1 thread" % (cfg2_chunksets, cfg2_tag))
+    th2 = min(allc, cfg2_chunksets)
+    extra["cfg2"] = dict(rnd(median([run(o.fast_blob_encode, o.fast_blob_repair, smp2, th2, min_s=1.0)
+                                     for _ in range(max(1, repeats))])), cores=th2,
+                         sample="%d chunksets%s, %d threads" % (cfg2_chunksets, cfg2_tag, th2))
+    del smp2
+    # config 1: one chunkset (chunkset-parallel, so one thread does all of it), median of repeats
+    smp1 = sample(1, seed + 3)
+    extra["cfg1"] = dict(rnd(median([run(o.fast_blob_encode, o.fast_blob_repair, smp1, 1, min_s=0.5)
+                                     for _ in range(max(1, repeats))])), cores=1,
+                         sample="1 chunkset (config 1), 1 thread")
+    del smp1
+    return dict({"value": head["value"], "unit": "GiB/s", "cores": head["cores"], "kind": "port",
+                 "variant": head_name, "headline": best, "median_of": head["runs"], "passes": head["passes"],
+                 "spread": head["spread"], "sample": head["sample"],
+                 "encode_gib_s": head["encode_gib_s"], "repair_gib_s": head["repair_gib_s"],
+                 "host": host_cpu(), "thread_counts": counts, "other_variants": rows}, **extra)
+
+
+def pattern_ceilings(torch, stream, device, n, src, coeffs, coded, pitch, plan, out, status, reps=10):
+    """Each streaming kernel's own access-pattern ceiling, timed on the headline's buffers after the
+    timed region: tools/bin/libdecds_pattern.so is the product's kernel source built with
+    DECDS_STUDY_PATTERN (rlnc_kernels.hip: the same loads, stores, tile order and table builds, the LDS
+    lookups replaced by one XOR per input dword). It writes wrong bytes by design, so it runs after the
+    repaired data was checked: decode first (on the real plans and coded rows, so its edge pass sees
+    intact tails), then encode. Median of `reps` launches, each between its own events on the bench
+    stream. Loaded privately (RTLD_LOCAL) beside the product library."""
+    import ctypes
+    import numpy as np
+    path = os.path.join(ROOT, "tools", "bin", "libdecds_pattern.so")
+    if not os.path.exists(path):
+        return {"error": "tools/bin/libdecds_pattern.so not built (decds_amd.build.build_pattern)"}
+    L = ctypes.CDLL(path)
+    vp, sz = ctypes.c_void_p, ctypes.c_size_t
+    L.decds_ctx_create.argtypes = [ctypes.c_int, ctypes.POINTER(vp)]
+    L.decds_ctx_destroy.argtypes = [vp]
+    L.decds_encode_batch.argtypes = [vp, vp, sz, vp, vp, sz, vp]
+    L.decds_decode_batch.argtypes = [vp, vp, sz, sz, vp, vp, vp, vp, vp]
+    ctx = vp()
+    if L.decds_ctx_create(device, ctypes.byref(ctx)) != 0:
+        return {"error": "decds_ctx_create failed in the pattern build"}
+    st = vp(stream.cuda_stream)
+
+    def timed(launch):
+        t_w = time.perf_counter()
+        while time.perf_counter() - t_w < 0.2:
+            for _ in range(4):
+                assert launch() == 0
+            stream.synchronize()
+        ev = [[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(reps)]
+        for e in ev:
+            e[0].record(stream)
+            assert launch() == 0
+            e[1].record(stream)
+        stream.synchronize()
+        return float(np.median([a.elapsed_time(b) for a, b in ev]))
+
+    dec_ms = timed(lambda: L.decds_decode_batch(ctx, coded.data_ptr(), pitch, n, plan.data_ptr(), out.data_ptr(),
+                                                status.data_ptr(), None, st))
+    enc_ms = timed(lambda: L.decds_encode_batch(ctx, src.data_ptr(), n, coeffs.data_ptr(), coded.data_ptr(), pitch, st))
+    L.decds_ctx_destroy(ctx)
+    return {"library": "tools/bin/libdecds_pattern.so (DECDS_STUDY_PATTERN)", "launches": reps,
+            "encode_ms": round(enc_ms, 4), "decode_ms": round(dec_ms, 4)}
+
+
+def end_to_end(ctx, chunksets=103, repeats=5, batch=16):
+    """The PCIe-inclusive rate north_star asks for (blob in host memory -> coded chunks in host memory
+    -> repaired blob in host memory): decds_blob_encode_host and decds_blob_repair_host (handle_break.rs
+    / handle_repair.rs's device work, blob.rs:252-264 / 373-473) at config 2's 1 GiB blob, every caller
+    buffer from decds_host_alloc (page-locked: direct DMA), H2D / kernels / D2H overlapped over three
+    slots in the library. One warm-up call each, then the median of `repeats` calls; the repaired
+    chunksets are compared with the blob."""
+    import numpy as np
+    from decds_amd import codec
+    from decds_amd.blob import HostBuffer
+    from decds_amd._capi import CHUNKSET_BYTES as CS, CODED_PIECE_BYTES as F, K, N
+    blob_len = chunksets * CS if chunksets != 103 else 1 << 30
+    n = -(-blob_len // CS)
+    hb_blob, hb_coded, hb_out = HostBuffer(blob_len), HostBuffer(n * N * F), HostBuffer(blob_len)
+    blob = hb_blob.array
+    blob[:] = codec.fill_random_host(0xDEC05004, blob_len)
+    coeffs = codec.fill_random_host(0xC0EF0004, n * N * K)
+    rng = np.random.default_rng(0x5EED0004)
+    cand = np.full((n, N), 0xFF, np.uint8)
+    for c in range(n):
+        cand[c, :K] = rng.permutation(N)[:K]
+    coded_out = hb_coded.array.reshape(n * N, F)
+    enc, rep = [], []
+    for i in range(repeats + 1):
+        t0 = time.perf_counter()
+        codec.blob_encode_host(ctx, blob, coeffs, batch=batch, out=coded_out)
+        t1 = time.perf_counter()
+        _, status = codec.blob_repair_host(ctx, coded_out, cand, blob_len, batch=batch, out=hb_out.array)
+        t2 = time.perf_counter()
+        if i:
+            enc.append(t1 - t0)
+            rep.append(t2 - t1)
+    ok = np.nonzero(status == 0)[0]
+    out = hb_out.array
+    for c in ok.tolist():
+        lo, hi = c * CS, min((c + 1) * CS, blob_len)
+        assert np.array_equal(out[lo:hi], blob[lo:hi]), "end-to-end repaired chunkset %d differs" % c
+    rep_len = sum(min(CS, blob_len - c * CS) for c in ok.tolist())
+    e, r = float(np.median(enc)), float(np.median(rep))
+    res = {"what": "decds_blob_encode_host + decds_blob_repair_host, host memory to host memory (PCIe-inclusive)",
+           "blob_bytes": blob_len, "chunksets": n, "batch": batch, "memory": "decds_host_alloc (page-locked) caller buffers",
+           "calls": repeats, "encode_ms": round(e * 1e3, 3), "repair_ms": round(r * 1e3, 3),
+           "encode_spread_ms": [round(min(enc) * 1e3, 3), round(max(enc) * 1e3, 3)],
+           "repair_spread_ms": [round(min(rep) * 1e3, 3), round(max(rep) * 1e3, 3)],
+           "encode_blob_GiBps": round(blob_len / GIB / e, 2), "repair_blob_GiBps": round(rep_len / GIB / r, 2),
+           "value_GiBps": round((blob_len + rep_len) / 2 / GIB / (e + r), 2),
+           "encode_pcie_GBps": round((blob_len + n * N * F) / e / 1e9, 2),
+           "repair_pcie_GBps": round((len(ok) * K * F + rep_len) / r / 1e9, 2),
+           "ready_chunksets": int(len(ok)), "repaired_checked": int(len(ok))}
+    del coded_out, out, blob
+    for hb in (hb_blob, hb_coded, hb_out):
+        hb.free()
+    return res
+
 
 def init_group(dist, backend, device, rank, world, timeout_s=300):
     """The process group for N > 1 (RCCL; DECDS_BENCH_BACKEND=gloo rehearses the path with ranks
@@ -405,6 +540,13 @@ def main():
                                    "fused_kernels": "rlnc_encode_hash_kernel + commit_fold_kernel + chunkset_merkle_kernel",
                                    "fused_blob_GiBps": round(n * CS / GIB / (f_ms * 1e-3), 1)}}
 
+    # the kernels' own access-pattern ceilings (decode first: it needs the intact coded rows), then the
+    # end-to-end host-memory rate (north_star: written in DESIGN.md §7) — both after the timed region
+    patterns, e2e = None, None
+    if world == 1 and not args.no_extras:
+        patterns = pattern_ceilings(torch, stream, local, n, src, coeffs, coded, pitch, plan, out, status)
+        e2e = end_to_end(ctx)
+
     # encode batch sweep beside the headline step (north_star: "at batch >= 256"):
     # one HBM-resident 16 GiB blob, encode-only launches of its first n chunksets, HIP events on the
     # bench stream. Single-GPU runs only; never inside the timed step.
@@ -499,6 +641,13 @@ def main():
     else:
         per_rank = [mine]
         rep_total = float(rep_len)
+    def pattern_of(nbytes, gbs, key):
+        """the kernel's own access-pattern ceiling (pattern_ceilings) and the fraction of it reached"""
+        if not patterns or key not in patterns:
+            return {}
+        p_gbs = nbytes / (patterns[key] * 1e-3) / 1e9
+        return {"pattern_GBps": round(p_gbs, 1), "frac_of_pattern": round(gbs / p_gbs, 4)}
+
     if rank == 0 or rehearse:
         # whole-job blob bytes (a rehearsal: this shard's bytes only)
         enc_total = float(blob_len_rank if rehearse else blob_per_gpu * world)
@@ -517,12 +666,14 @@ def main():
             "roofline": {"bound": "hbm", "kernel": dominant, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "copy_ceiling": HBM_COPY_GBS, "frac_of_copy": round(achieved / HBM_COPY_GBS, 4),
-                         "decode": {"kernel": dec_kernel, "achieved": round(dec_gbs, 1),
-                                    "frac": round(dec_gbs / HBM_PEAK_GBS, 4),
-                                    "bytes_per_launch": dec_bytes, "ms": round(dec_ms, 4)},
-                         "encode": {"kernel": enc_kernel, "achieved": round(enc_gbs, 1),
-                                    "frac": round(enc_gbs / HBM_PEAK_GBS, 4),
-                                    "bytes_per_launch": enc_bytes, "ms": round(enc_ms, 4)}},
+                         "decode": dict({"kernel": dec_kernel, "achieved": round(dec_gbs, 1),
+                                         "frac": round(dec_gbs / HBM_PEAK_GBS, 4),
+                                         "bytes_per_launch": dec_bytes, "ms": round(dec_ms, 4)},
+                                        **pattern_of(dec_bytes, dec_gbs, "decode_ms")),
+                         "encode": dict({"kernel": enc_kernel, "achieved": round(enc_gbs, 1),
+                                         "frac": round(enc_gbs / HBM_PEAK_GBS, 4),
+                                         "bytes_per_launch": enc_bytes, "ms": round(enc_ms, 4)},
+                                        **pattern_of(enc_bytes, enc_gbs, "encode_ms"))},
             "breakdown": {"encode_ms": round(enc_ms, 4), "plan_ms": round(plan_ms, 4), "decode_ms": round(dec_ms, 4),
                           "encode_GBps": round(enc_gbs, 1), "decode_GBps": round(dec_gbs, 1),
                           "encode_blob_GiBps": round(n * CS / GIB / (enc_ms * 1e-3), 1),
@@ -531,12 +682,14 @@ def main():
             "rehearsal": None if rehearse is None else dict(rehearse, first_chunkset=lo, chunksets=n,
                                                              blob_bytes=blob_per_gpu * world, shard_bytes=blob_len_rank),
             "commitment": commit,
+            "pattern_ceilings": patterns,
+            "end_to_end": e2e,
             "encode_batch_sweep": sweep,
         }
+        line["per_rank"] = per_rank
         if dist_on:
             line["world_size"] = dist.get_world_size()
             line["backend"] = "rccl" if backend == "nccl" else backend
-            line["per_rank"] = per_rank
             devs = [r["device_uuid"] or "%s/%d" % (r["host"], r["local_rank"]) for r in per_rank]
             line["scaling_point"] = len(set(devs)) == world
             if not line["scaling_point"]:

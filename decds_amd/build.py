@@ -10,6 +10,9 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libdecds_rlnc.so")
+# measurement only (bench.py's pattern ceilings): the same sources with DECDS_STUDY_PATTERN, i.e. the
+# streaming kernels' memory pattern without their lookups (wrong bytes by design, never the product)
+PATTERN_LIB = os.path.join(HERE, "..", "tools", "bin", "libdecds_pattern.so")
 SOURCES = ["rlnc_kernels.hip", "commit_kernels.hip", "capi.cpp", "host_util.cpp", "host_mem.cpp", "chunkset.cpp", "blob.cpp",
            "commit.cpp", "wire.cpp", "blake3_host.cpp"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
@@ -20,10 +23,10 @@ FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-u
          "-Wno-unused-command-line-argument", "-I" + os.path.join(HERE, "..", "include")]
 
 
-def _stale():
-    if not os.path.exists(LIB):
+def _stale(lib=LIB):
+    if not os.path.exists(lib):
         return True
-    t = os.path.getmtime(LIB)
+    t = os.path.getmtime(lib)
     deps = [os.path.join(CSRC, f) for f in os.listdir(CSRC)] + [os.path.join(HERE, "..", "include", "decds_rlnc.h"),
                                                                  os.path.abspath(__file__)]  # flags live here
     return any(os.path.getmtime(d) > t for d in deps)
@@ -62,6 +65,14 @@ def build(force=False, verbose=True, defines=(), out=None, mllvm=()):
     return lib
 
 
+def build_pattern(force=False, verbose=True):
+    """tools/bin/libdecds_pattern.so: the pattern-ceiling build bench.py loads beside the product"""
+    if not force and not _stale(PATTERN_LIB):
+        return PATTERN_LIB
+    os.makedirs(os.path.dirname(PATTERN_LIB), exist_ok=True)
+    return build(force=True, verbose=verbose, defines=["DECDS_STUDY_PATTERN=1"], out=PATTERN_LIB)
+
+
 if __name__ == "__main__":
     # python -m decds_amd.build [--force] [--variant NAME -DX=1 ... --mllvm=-opt=v ...]
     args = sys.argv[1:]
@@ -72,5 +83,7 @@ if __name__ == "__main__":
         vdir = os.path.join(HERE, "..", "build", "variants")
         os.makedirs(vdir, exist_ok=True)
         print(build(force=True, defines=defs, out=os.path.join(vdir, "lib_%s.so" % name), mllvm=mll))
+    elif "--pattern" in args:
+        print(build_pattern(force="--force" in args))
     else:
         print(build(force="--force" in args, defines=defs))

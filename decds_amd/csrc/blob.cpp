@@ -57,7 +57,7 @@ struct Pipe {
         return e;
     }
     ~Pipe() {
-        (void)drain();
+        hip_tolerate(drain(), "hipStreamSynchronize (pipe teardown)");
         for (int i = 0; i < SLOTS; i++)
             for (hipEvent_t ev : {in_done[i], k_done[i], out_done[i]})
                 if (ev) hip_tolerate(hipEventDestroy(ev), "hipEventDestroy");

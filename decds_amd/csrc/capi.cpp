@@ -116,7 +116,11 @@ const char *decds_status_string(int s) {
 
 int decds_device_count(void) {
     int n = 0;
-    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    const hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) {
+        hip_tolerate(e, "hipGetDeviceCount");  // no device: 0, and the thread's error slot left clean
+        return 0;
+    }
     return n;
 }
 
@@ -125,6 +129,7 @@ int decds_ctx_create(int device, decds_ctx **out) {
     *out = nullptr;
     int n = 0;
     hipError_t e = hipGetDeviceCount(&n);
+    hip_tolerate(e, "hipGetDeviceCount");  // reported as DECDS_ERR_NO_DEVICE below, not left pending
     if (e != hipSuccess || n == 0)
         return decds_set_error(DECDS_ERR_NO_DEVICE, "no HIP device visible (%s)",
                                e == hipSuccess ? "count 0" : hipGetErrorString(e));

@@ -387,6 +387,9 @@ struct decds_repairing_chunkset {
     uint32_t rank;
     bool repaired;
     std::vector<uint8_t> rows;  // accepted full coded pieces, acceptance order
+    // a repair whose out buffer was too small keeps its result here: the retry only copies it out
+    std::vector<uint8_t> decoded;
+    size_t decoded_len = 0;
 };
 
 extern "C" {
@@ -548,6 +551,29 @@ int decds_repairing_chunkset_repair(decds_repairing_chunkset *r, uint8_t *out, s
     // chunkset.rs:201,206
     if (r->rank != K) return decds_set_error(DECDS_ERR_CHUNKSET_NOT_YET_READY, "chunkset %zu is not ready to repair", r->id);
     if (!out) return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "null out buffer");
+    // the decoder is consumed only by a repair that hands its bytes out (chunkset.rs:200)
+    auto deliver = [&](const uint8_t *body, const uint8_t *tail, size_t len) -> int {
+        if (out_len) *out_len = len;
+        if (out_cap < len) {
+            // kept (decoded bytes + tail): a retry with a larger buffer only copies
+            if (r->decoded.empty()) {
+                r->decoded.resize(CS + K);
+                par_memcpy(r->decoded.data(), body, CS);
+                std::memcpy(r->decoded.data() + CS, tail, K);
+                r->decoded_len = len;
+            }
+            return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "out buffer %zu < decoded length %zu", out_cap, len);
+        }
+        par_memcpy(out, body, std::min<size_t>(len, CS));
+        if (len > CS) std::memcpy(out + CS, tail, len - CS);
+        r->repaired = true;
+        r->rows.clear();
+        r->rows.shrink_to_fit();
+        r->decoded.clear();
+        r->decoded.shrink_to_fit();
+        return DECDS_OK;
+    };
+    if (!r->decoded.empty()) return deliver(r->decoded.data(), r->decoded.data() + CS, r->decoded_len);
     decds_ctx *ctx = r->ctx;
     int s = decds_ctx_bind(ctx);
     if (s) return s;
@@ -579,16 +605,8 @@ int decds_repairing_chunkset_repair(decds_repairing_chunkset *r, uint8_t *out, s
                                r->id, st == DECDS_ERR_CHUNKSET_REPAIRING_FAILED ? "invalid decoded data format" : decds_status_string(st));
     decds_repair_info info;
     std::memcpy(&info, L.h_small + SM_INFO, sizeof info);
-    const size_t len = info.decoded_len;  // get_decoded_data's cut at the last marker (CS when intact)
-    if (out_len) *out_len = len;
-    if (out_cap < len)  // the decoder is not consumed: the caller may retry with a larger buffer
-        return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "out buffer %zu < decoded length %zu", out_cap, len);
-    par_memcpy(out, L.h_big, std::min<size_t>(len, CS));
-    if (len > CS) std::memcpy(out + CS, info.tail, len - CS);
-    r->repaired = true;  // repair(self) consumes the decoder (chunkset.rs:200)
-    r->rows.clear();
-    r->rows.shrink_to_fit();
-    return DECDS_OK;
+    // get_decoded_data's cut at the last marker (CS when intact)
+    return deliver(L.h_big, info.tail, info.decoded_len);
 }
 
 void decds_repairing_chunkset_free(decds_repairing_chunkset *r) { delete r; }

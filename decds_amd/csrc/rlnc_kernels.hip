@@ -17,9 +17,10 @@
 // accumulation into a 16x16 byte block (columns x outputs), a v_perm byte transpose, 16 (or 10)
 // 16-B stores. No MFMA: this is byte-wise finite-field work, bounded by HBM bandwidth.
 //
-// Only the shipped configuration lives here, plus two study hooks that compile to nothing by default
+// Only the shipped configuration lives here, plus three study hooks that compile to nothing by default
 // (DECDS_PHASE_TRACE: per-workgroup phase stamps of the encode sweep for tools/phasetrace.py;
-// DECDS_STUDY_NO_EDGE: the encode without its edge pass, timing only). The round-1 study variants
+// DECDS_STUDY_NO_EDGE: the encode without its edge pass, timing only; DECDS_STUDY_PATTERN: the
+// kernels' memory pattern without their lookups — the pattern ceilings bench.py reports). The round-1 study variants
 // (persistent walks, XCD bands, per-half work shares, per-tile barriers, the warp-specialised kernel)
 // are in git history (tools/study/rlnc_kernels_r01_study.hip at a5d9101) with their measurements in
 // DESIGN.md §8.
@@ -419,7 +420,20 @@ __device__ __forceinline__ void combine_block(Vec<DW> (&x)[NIN], uint8_t *obase,
     for (int c = 0; c < 4 * DW; c++)
 #pragma unroll
         for (int q = 0; q < 4; q++) acc[c][q] = 0;
+#ifdef DECDS_STUDY_PATTERN
+    // pattern-ceiling builds only (bench.py's roofline.*.pattern_GBps, tools/bin/libdecds_pattern.so):
+    // the kernel's own loads, stores, tile order and table builds with the LDS lookups replaced by one
+    // XOR per input dword — input i's next-block load issued as soon as input i is consumed, as in
+    // lds_step. Wrong bytes by design; never in the product library.
+#pragma unroll
+    for (int i = 0; i < NIN; i++) {
+#pragma unroll
+        for (int w = 0; w < DW; w++) acc[4 * w + (i & 3)][(i >> 2) & 3] ^= x[i][w];
+        x[i] = ldrow<DW>(ibase, ioff[i], ncol0);
+    }
+#else
     lookups<NIN, DW, TB, HB, SDWA>(std::make_integer_sequence<int, DW * NIN * (4 / HB)>{}, acc, x, ibase, ioff, ncol0);
+#endif
     // columns x outputs -> outputs x columns
 #pragma unroll
     for (int q = 0; q < 4; q++) {
@@ -706,6 +720,16 @@ void rlnc_encode_hash_kernel(const uint8_t *__restrict__ src, size_t n, const ui
 // their first tile (at n = 1 the edge pass — byte-wise loads, a few dependent HBM round trips — sat on
 // the one critical path of a 13 µs launch). The launcher keeps the whole grid co-resident.
 constexpr uint32_t EDGE_WGS = 64;
+// The sweeps end only because every workgroup's next tile lies strictly past its current one: the
+// counter only grows, and a workgroup's next grab is issued after its previous one returned. A counter
+// value read before its atomic has landed breaks that — in the 3-wave encode build of round 4 (r06z14)
+// hipcc spilled the pending return register straight after the atomic, so the spill slot held the
+// atomic's data operand (1) and every workgroup took tile G + 1 again and again: a silent hang, not a
+// fault. Here a violated order ends the kernel with a trap (a named kernel fault on the
+// host side) instead of spinning. next and cur are wave-uniform (SGPRs): one compare per tile.
+__device__ __forceinline__ void sweep_guard(uint32_t next, uint32_t cur) {
+    if (next <= cur) __builtin_trap();
+}
 // coded-row store cache policy (SAUX, the buffer stores' aux bits): `sc1` (16, write-through) below
 // DECDS_ENC_NT_MIN_N chunksets, `nt` (2) from there on. A plain store leaves its line dirty in the
 // XCD's L2, so a small batch's coded rows were written back by the end-of-kernel release, after its
@@ -843,7 +867,8 @@ void rlnc_encode_sweep_kernel(const uint8_t *__restrict__ src, size_t n, const u
         if (pt_tiles < 16) PT_STAMP(8 + pt_tiles);
         if (pt_tiles++ == 0) PT_STAMP(2);
 #endif
-        const uint32_t tn = QUEUE ? s_next : t + G;
+        const uint32_t tn = QUEUE ? __builtin_amdgcn_readfirstlane(s_next) : t + G;
+        sweep_guard(tn, t);
         grab = grab_next();
         more = tn < total;
         const uint32_t csn = more ? tn / T : cs;
@@ -1178,7 +1203,8 @@ void rlnc_decode_sweep_kernel(const uint8_t *__restrict__ coded, size_t pitch, s
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (threadIdx.x == 0) s_next = counter ? G + grab : k + G;
     lds_barrier();  // also: the edge pass's table readers are done
-    uint32_t kn = s_next;
+    uint32_t kn = __builtin_amdgcn_readfirstlane(s_next);
+    sweep_guard(kn, k);
     uint32_t more;
 #pragma unroll 1
     do {
@@ -1198,7 +1224,8 @@ void rlnc_decode_sweep_kernel(const uint8_t *__restrict__ coded, size_t pitch, s
         if (threadIdx.x == 0) s_next = counter ? G + grab : kn + G;
         lds_barrier();
         k = kn;
-        kn = s_next;
+        kn = __builtin_amdgcn_readfirstlane(s_next);
+        sweep_guard(kn, k);
         cs = csn;
         cur = nxt;
         cw = cwn;

@@ -218,7 +218,8 @@ int decds_repairing_chunkset_is_ready_to_repair(const decds_repairing_chunkset *
  * its length — 10 MiB for any validated chunk set; rows accepted unvalidated can move rlnc's cut at
  * the last boundary marker (decds_repair_info), up to DECDS_DECODED_MAX_BYTES. No marker ->
  * DECDS_ERR_CHUNKSET_REPAIRING_FAILED. out_cap below the decoded length -> DECDS_ERR_INVALID_ARGUMENT
- * with *out_len set and the decoder kept. Consumes the decoder state on success (a second call
+ * with *out_len set and the decoder kept, its result too (a retry with a larger buffer only copies
+ * it out: no second transfer or decode). Consumes the decoder state on success (a second call
  * returns DECDS_ERR_CHUNKSET_ALREADY_REPAIRED). */
 int decds_repairing_chunkset_repair(decds_repairing_chunkset *rcs, uint8_t *out, size_t out_cap, size_t *out_len);
 void decds_repairing_chunkset_free(decds_repairing_chunkset *rcs);

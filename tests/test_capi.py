@@ -127,3 +127,24 @@ def test_decode_kernel_by_batch_size():
     r = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, DECDS_DEC_SWEEP_MIN_N="7"),
                        capture_output=True, text=True, timeout=60)
     assert r.returncode == 0, r.stderr[-2000:]
+
+
+def test_library_consumes_its_hip_failures():
+    # hip_status.h: hip_launch_begin treats an error pending on the thread as left by a HIP call
+    # outside the library, so the library must consume every failure of its own calls (decds_hip_error,
+    # hip_tolerate or an explicit hipGetLastError). Flags: a HIP call cast to (void) or called as a bare
+    # statement (its status dropped, possibly left pending), and a (void)-cast drain() of a stream set.
+    import re
+    csrc = os.path.join(ROOT, "decds_amd", "csrc")
+    bad = []
+    for f in sorted(os.listdir(csrc)):
+        if not f.endswith((".cpp", ".hip", ".h")):
+            continue
+        with open(os.path.join(csrc, f)) as fh:
+            for no, line in enumerate(fh, 1):
+                code = line.split("//")[0]
+                if re.search(r"\(void\)\s*(hip(?!GetLastError)\w+|\w*drain)\s*\(", code):
+                    bad.append("%s:%d: %s" % (f, no, line.strip()))
+                if re.match(r"^\s*hip(?!LaunchKernelGGL|GetLastError)[A-Z]\w*\(", code):
+                    bad.append("%s:%d: %s" % (f, no, line.strip()))
+    assert not bad, "\n".join(bad)

@@ -11,6 +11,14 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+def free_port():
+    """a TCP port on 127.0.0.1 that nothing holds right now (the OS picks it)"""
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
 @pytest.mark.gpu
 def test_bench_line_roofline_is_the_dominant_kernels():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "3", "--warmup", "1", "--settle-s", "0.1",
@@ -51,28 +59,59 @@ def test_bench_rehearsal_runs_one_shard_of_a_larger_job():
     assert d["encode_batch_sweep"] is None and d["value"] > 0
 
 
+CFG5_CHUNKSETS = 13108      # the 128 GiB blob of BASELINE config 5: ceil(2^37 / 10 MiB)
+CFG5_PER_GPU = 1639         # ceil(13108 / 8): ranks 0-6 own 1639 chunksets, rank 7 the last 1635
+
+
+def cfg5_shard(rank):
+    """rank's chunkset range of config 5, written out independently of bench.shard_range"""
+    lo = rank * CFG5_PER_GPU
+    return lo, min(lo + CFG5_PER_GPU, CFG5_CHUNKSETS)
+
+
+def test_cfg5_shards_tile_the_blob():
+    # CPU: the eight shards bench.py runs at N = 8 are contiguous, disjoint and cover [0, 13108)
+    # exactly (blob.rs:252-264: chunkset-index order), and bench.shard_range gives the same ranges
+    sys.path.insert(0, ROOT)
+    import bench
+    ranges = [cfg5_shard(r) for r in range(8)]
+    assert ranges[0][0] == 0 and ranges[-1][1] == CFG5_CHUNKSETS
+    assert all(a[1] == b[0] for a, b in zip(ranges, ranges[1:]))
+    assert [bench.shard_range(CFG5_CHUNKSETS, 8, r) for r in range(8)] == ranges
+    assert -(-(128 << 30) // (10 << 20)) == CFG5_CHUNKSETS
+    assert (128 << 30) - (CFG5_CHUNKSETS - 1) * (10 << 20) == 2 << 20  # the last chunkset holds 2 MiB
+
+
 @pytest.mark.gpu
-def test_bench_cfg5_last_shard_rehearsal_spot_checked(tmp_path):
-    # cfg5's shard geometry on one GPU: rank 7 of the 128 GiB blob over 8 GPUs = chunksets
-    # [11473, 13108), 1635 of them, the last holding 2 MiB of data (blob.rs:252-254 zero-pads it).
-    # bench.py repairs every chunkset and compares it with its source itself; here its first, middle
-    # and last chunkset's coded rows (payload-aligned layout) are checked against the oracle, and
-    # their source bytes against the global synthetic blob at the shard's offset.
+@pytest.mark.parametrize("rank", range(8))
+def test_bench_cfg5_shard_rehearsal_spot_checked(tmp_path, rank):
+    # All of config 5 on one GPU, one shard per test: rank R of the 128 GiB blob over 8 GPUs
+    # (bench.py --rehearse-shard R/8, the process each of the driver's eight ranks runs), at full size.
+    # Rank 7 = chunksets [11473, 13108), the last holding 2 MiB of data (blob.rs:252-254 zero-pads
+    # it). bench.py repairs every chunkset of the shard and compares it with its source itself; here
+    # the shard's range, and its first, middle and last chunkset's source bytes (against the global
+    # synthetic blob at the shard's offset) and coded rows (payload-aligned layout, against the oracle).
     import numpy as np
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as o
+    lo, hi = cfg5_shard(rank)
     spot = str(tmp_path / "spot.npz")
-    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--config", "cfg3", "--rehearse-shard", "7/8",
-                        "--steps", "1", "--warmup", "1", "--settle-s", "0", "--no-cpu-baseline", "--no-commit",
-                        "--spot-out", spot], capture_output=True, text=True, timeout=110, cwd=ROOT)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--config", "cfg3", "--rehearse-shard",
+                        "%d/8" % rank, "--steps", "1", "--warmup", "1", "--settle-s", "0", "--no-cpu-baseline",
+                        "--no-commit", "--no-extras", "--spot-out", spot], capture_output=True, text=True, timeout=110,
+                       cwd=ROOT)
     assert r.returncode == 0, r.stderr[-2000:]
     d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
     reh = d["rehearsal"]
-    assert reh["first_chunkset"] == 11473 and reh["chunksets"] == 1635 and reh["world"] == 8
-    assert reh["shard_bytes"] == (128 << 30) - 11473 * o.CS
-    assert d["config"]["chunksets_per_gpu"] == 1635 and d["breakdown"]["ready_chunksets"] >= 1600
+    assert reh["rank"] == rank and reh["world"] == 8
+    assert reh["first_chunkset"] == lo and reh["chunksets"] == hi - lo
+    assert reh["shard_bytes"] == min(128 << 30, hi * o.CS) - lo * o.CS
+    assert d["config"]["chunksets_per_gpu"] == hi - lo
+    bd = d["breakdown"]
+    assert bd["ready_chunksets"] + bd["not_ready_chunksets"] == hi - lo and bd["ready_chunksets"] >= hi - lo - 40
+    assert d["per_rank"][0]["repaired_checked"] == bd["ready_chunksets"]
     z = np.load(spot)
-    assert z["chunksets"].tolist() == [11473, 11473 + 817, 13107]
+    assert z["chunksets"].tolist() == [lo, lo + (hi - lo) // 2, hi - 1]
     for k, c in enumerate(z["chunksets"].tolist()):
         have = min(o.CS, (128 << 30) - c * o.CS)
         expect = np.zeros(o.CS, np.uint8)
@@ -81,7 +120,6 @@ def test_bench_cfg5_last_shard_rehearsal_spot_checked(tmp_path):
         assert np.array_equal(z["coeffs"][k], o.fill_random(0xC0EF0002, o.N * o.K, c * o.N * o.K)), c
         ref = o.chunkset_encode(expect, z["coeffs"][k], nthreads=8)
         assert np.array_equal(z["coded"][k], ref), c
-    assert (128 << 30) - 13107 * o.CS == 2 << 20
 
 
 @pytest.mark.gpu
@@ -93,7 +131,7 @@ def test_bench_two_ranks_torchrun_per_rank_records():
     # device as not a scaling point.
     env = dict(os.environ, DECDS_BENCH_BACKEND="gloo", MASTER_ADDR="127.0.0.1")
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-                        "--master-addr", "127.0.0.1", "--master-port", "29531", os.path.join(ROOT, "bench.py"),
+                        "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.join(ROOT, "bench.py"),
                         "--gpus", "2", "--steps", "2", "--warmup", "1", "--settle-s", "0.1", "--config", "cfg2",
                         "--no-commit"], capture_output=True, text=True, timeout=240, cwd=ROOT, env=env)
     assert r.returncode == 0, r.stderr[-3000:]

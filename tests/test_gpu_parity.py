@@ -479,6 +479,18 @@ def test_chunkset_mirror_errors(ctx):
     with pytest.raises(decds_amd.DecdsError) as e:
         rcs2.add_chunk_unvalidated(cs.get_chunk(0))
     assert e.value.kind == "ChunkDecodingFailed"
+    # a repair into a too-small buffer reports the decoded length and keeps the decoder (and its
+    # result: the retry only copies); the repair that delivers the bytes consumes it
+    import ctypes
+    from decds_amd._capi import lib
+    rcs3 = decds_amd.RepairingChunkSet(ctx, 3)
+    for i in range(N - K, N):
+        rcs3.add_chunk_unvalidated(cs.get_chunk(i))
+    small, n_out = ctypes.create_string_buffer(64), ctypes.c_size_t()
+    assert lib().decds_repairing_chunkset_repair(rcs3._h, small, 64, ctypes.byref(n_out)) == -2  # invalid argument
+    assert n_out.value == CS and rcs3.is_ready_to_repair()
+    assert rcs3.repair() == data
+    assert not rcs3.is_ready_to_repair()
 
 
 def test_blob_host_roundtrip_partial_last_chunkset(ctx):

@@ -25,10 +25,19 @@ OBJDUMP = "/opt/rocm/lib/llvm/bin/llvm-objdump"
 VMEM = ("buffer_", "global_", "scratch_", "flat_")
 
 
-def _device_code(tmp_path):
+LIBS = ("product", "pattern")  # the in-tree library, and bench.py's pattern-ceiling build (it runs on the GPU too)
+
+
+def _lib(which="product"):
     from decds_amd import build
 
-    lib = os.environ.get("DECDS_LIB") or build.build(verbose=False)  # a variant build, or the in-tree one
+    if which == "pattern":
+        return build.build_pattern(verbose=False)
+    return os.environ.get("DECDS_LIB") or build.build(verbose=False)  # a variant build, or the in-tree one
+
+
+def _device_code(tmp_path, which="product"):
+    lib = _lib(which)
     work = tmp_path / "isa"
     work.mkdir()
     shutil.copy(lib, work / "lib.so")
@@ -111,10 +120,11 @@ def _unsafe_uses(fn):
     return bad
 
 
-def test_counter_atomics_are_waited_for_before_use(tmp_path):
+@pytest.mark.parametrize("which", LIBS)
+def test_counter_atomics_are_waited_for_before_use(tmp_path, which):
     if not os.path.exists(OBJDUMP):
         pytest.skip("llvm-objdump not in this image")
-    funcs = _functions(_device_code(tmp_path))
+    funcs = _functions(_device_code(tmp_path, which))
     sweeps = {k: v for k, v in funcs.items() if "sweep_kernel" in k}
     assert any("encode_sweep" in k for k in sweeps), sorted(funcs)[:20]
     checked = 0
@@ -148,11 +158,9 @@ def test_checker_flags_an_early_read():
     assert not _unsafe_uses(fn(jumped)) and _unsafe_uses(fn(either))
 
 
-def _kernel_notes(tmp_path):
+def _kernel_notes(tmp_path, which="product"):
     """{kernel symbol: {metadata key: value}} from the gfx950 code objects' AMDGPU notes"""
-    from decds_amd import build
-
-    lib = os.environ.get("DECDS_LIB") or build.build(verbose=False)
+    lib = _lib(which)
     work = tmp_path / "notes"
     work.mkdir()
     shutil.copy(lib, work / "lib.so")
@@ -175,14 +183,15 @@ def _kernel_notes(tmp_path):
     return kernels
 
 
-def test_table_kernels_have_no_static_lds(tmp_path):
+@pytest.mark.parametrize("which", LIBS)
+def test_table_kernels_have_no_static_lds(tmp_path, which):
     # The streaming kernels' lookups are inline-asm ds_read_b128 with absolute LDS offsets: their
     # tables must start at LDS address 0, i.e. the dynamic area must come first. A static __shared__
     # variable in such a kernel is placed before the dynamic area and shifts every table (round 4's
     # first TailLds build did that: repaired bytes wrong). Their group segment must be 0.
     if not os.path.exists(OBJDUMP):
         pytest.skip("llvm-objdump not in this image")
-    notes = _kernel_notes(tmp_path)
+    notes = _kernel_notes(tmp_path, which)
     table = {k: v for k, v in notes.items()
              if any(s in k for s in ("encode_sweep_kernel", "decode_sweep_kernel", "rlnc_decode_kernel",
                                      "encode_hash_kernel"))}
@@ -190,3 +199,17 @@ def test_table_kernels_have_no_static_lds(tmp_path):
     for name, md in table.items():
         assert md.get("group_segment_fixed_size") == "0", (name, md.get("group_segment_fixed_size"))
         assert md.get("private_segment_fixed_size") == "0", (name, "spills to scratch")
+
+
+@pytest.mark.parametrize("which", LIBS)
+def test_sweeps_trap_instead_of_spinning(tmp_path, which):
+    # every persistent sweep carries the guard (rlnc_kernels.hip sweep_guard): a next tile not past the
+    # current one — a counter value read before its atomic landed, the round-4 3-wave hang (DESIGN.md
+    # §8) — ends the kernel with s_trap instead of an endless loop over one tile
+    if not os.path.exists(OBJDUMP):
+        pytest.skip("llvm-objdump not in this image")
+    funcs = _functions(_device_code(tmp_path, which))
+    sweeps = {k: v for k, v in funcs.items() if "sweep_kernel" in k}
+    assert sum("encode_sweep" in k for k in sweeps) >= 5 and any("decode_sweep" in k for k in sweeps), sorted(sweeps)
+    for name, ins in sweeps.items():
+        assert any(x.startswith("s_trap 2") for _, x in ins), name

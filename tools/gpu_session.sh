@@ -12,7 +12,7 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $out/smok
 tail -1 $out/smoke.log
 timeout -k 10 600 python bench.py --config $cfg --steps $steps --warmup 5 > $out/bench.json 2> $out/bench.err || { echo "BENCH FAILED"; tail -20 $out/bench.err; exit 1; }
 cat $out/bench.json
-bcmd="python3 bench.py --config $cfg --steps $steps --warmup 5 --no-cpu-baseline --no-sweep"
+bcmd="python3 bench.py --config $cfg --steps $steps --warmup 5 --no-cpu-baseline --no-sweep --no-extras"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $out/trace -o bench -- $bcmd > $out/trace.log 2>&1 || { echo "TRACE FAILED"; tail -5 $out/trace.log; exit 1; }
 i=0
 for pmc in FETCH_SIZE WRITE_SIZE "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE" "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU"; do
