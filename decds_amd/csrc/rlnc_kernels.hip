@@ -727,8 +727,11 @@ constexpr uint32_t EDGE_WGS = 64;
 // atomic's data operand (1) and every workgroup took tile G + 1 again and again: a silent hang, not a
 // fault. Here a violated order ends the kernel with a trap (a named kernel fault on the
 // host side) instead of spinning. next and cur are wave-uniform (SGPRs): one compare per tile.
+#ifndef DECDS_SWEEP_GUARD
+#define DECDS_SWEEP_GUARD 1  // 0: study builds only (the guard's cost A/B)
+#endif
 __device__ __forceinline__ void sweep_guard(uint32_t next, uint32_t cur) {
-    if (next <= cur) __builtin_trap();
+    if (DECDS_SWEEP_GUARD && next <= cur) __builtin_trap();
 }
 // coded-row store cache policy (SAUX, the buffer stores' aux bits): `sc1` (16, write-through) below
 // DECDS_ENC_NT_MIN_N chunksets, `nt` (2) from there on. A plain store leaves its line dirty in the
@@ -923,8 +926,12 @@ __device__ __forceinline__ void tail_note(TailLds &t, uint64_t p, uint32_t z, ui
 // The whole workgroup, after a barrier behind every tail_note; returns at once when a tail byte is
 // the marker. Otherwise the decoded bytes are decoded again here from the accepted rows (the
 // chunkset's tiles are being written by other workgroups at the same time), from the end of the
-// chunkset down, WG x 16 positions per step (4 positions per thread at a time: one round trip for
-// their 40 byte loads), until a step holds a marker. tbl: the decode tables (input k, output i).
+// chunkset down, WG x 16 positions per step, until a step holds a marker. A thread's 16 positions
+// lie in one piece except at the 9 piece boundaries: it loads them as one unaligned 16-byte access
+// per accepted row (10 loads, one round trip — round 4 loaded every byte: 160 loads per 16 positions,
+// ADVICE r04), and byte by byte only across a boundary. tbl: the decode tables (input k, output i).
+// Reached only by rows accepted unvalidated whose tail holds no marker; a chunkset with no marker at
+// all is decoded once more in full by this one workgroup (tests/test_gpu_parity.py times that case).
 __device__ __forceinline__ void tail_scan_decoded(TailLds &t, const uint8_t *tbl, const uint8_t *ibase, const uint32_t (&ioff)[K],
                                   uint32_t marker) {
     if (__builtin_amdgcn_readfirstlane(t.cut)) return;
@@ -933,21 +940,26 @@ __device__ __forceinline__ void tail_scan_decoded(TailLds &t, const uint8_t *tbl
     for (uint32_t blk = (uint32_t)CS; blk > 0;) {
         blk -= STEP;
         uint32_t h = 0;
-#pragma unroll 1
-        for (int g = 3; g >= 0; g--) {
-            const uint32_t b0 = blk + threadIdx.x * 16 + 4 * (uint32_t)g;
-            uint32_t xb[4][K];
+        const uint32_t p0 = blk + threadIdx.x * 16, i0 = p0 / (uint32_t)L, col0 = p0 - i0 * (uint32_t)L;
+        if (col0 + 16 <= (uint32_t)L) {
+            u32x4 x[K];
 #pragma unroll
-            for (uint32_t b = 0; b < 4; b++)
+            for (uint32_t k = 0; k < K; k++) x[k] = ldrow<4>(ibase, ioff[k], col0);
 #pragma unroll
-                for (uint32_t k = 0; k < K; k++) xb[b][k] = ibase[ioff[k] + (b0 + b) % (uint32_t)L];
-#pragma unroll
-            for (uint32_t b = 0; b < 4; b++) {
-                const uint32_t p = b0 + b, i = p / (uint32_t)L;
+            for (uint32_t b = 0; b < 16; b++) {
                 uint32_t z = 0;
 #pragma unroll
-                for (uint32_t k = 0; k < K; k++) z ^= tbl_mul(tbl, k, i, xb[b][k]);
-                if (z == marker) h = h > p + 1 ? h : p + 1;
+                for (uint32_t k = 0; k < K; k++) z ^= tbl_mul(tbl, k, i0, (x[k][b >> 2] >> (8 * (b & 3))) & 0xFFu);
+                if (z == marker) h = p0 + b + 1;  // positions rise with b: the last hit is the highest
+            }
+        } else {
+#pragma unroll 1
+            for (uint32_t b = 0; b < 16; b++) {
+                const uint32_t p = p0 + b, i = p / (uint32_t)L, col = p - i * (uint32_t)L;
+                uint32_t z = 0;
+#pragma unroll
+                for (uint32_t k = 0; k < K; k++) z ^= tbl_mul(tbl, k, i, ibase[ioff[k] + col]);
+                if (z == marker) h = p + 1;
             }
         }
         // (not __syncthreads_or: HIP's keeps a static __shared__ word, which would move the dynamic

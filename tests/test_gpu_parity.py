@@ -415,6 +415,53 @@ def test_decoded_data_cut_at_last_marker_matches_oracle(ctx):
     assert seen == {"error", "short", "long", "cs"}
 
 
+@pytest.mark.parametrize("n", [1, 256])
+def test_no_marker_anywhere_worst_case_cost(ctx, n):
+    """a chunkset whose decoded data holds no boundary marker at all (only rows accepted
+    unvalidated get there) is decoded once more in full by its edge workgroup (tail_scan_decoded) before
+    it is ChunksetRepairingFailed. Its cost, at n = 1 (one-tile decode) and inside a 256-chunkset batch
+    (the sweep), against the same launch with every chunkset intact: status 6 for it, 0 and intact bytes
+    for the others, the extra time recorded and bounded (print: `pytest -s`)."""
+    import time
+    d = o.fill_random(0xBAD0, CS).copy()
+    d[d == MARKER] ^= 1
+    data = np.concatenate([d] + [o.fill_random(0xB000 + c, CS) for c in range(1, n)])
+    coeffs = o.fill_random(0xC0EFBAD0, n * N * K).reshape(n, N, K)
+    coded_d = torch.empty(n * N * F, dtype=torch.uint8, device="cuda")
+    codec.encode_batch(ctx, dev(data), n, dev(coeffs), coded_d)
+    bad = coded_d.clone()
+    bad[:N * F] = dev(_corrupt_tail(host(coded_d[:N * F]).reshape(N, F), coeffs[0], {0: MARKER}).reshape(-1))
+    cand = dev(np.tile(np.arange(N, dtype=np.uint8), (n, 1)))
+    plan = torch.empty(n * 128, dtype=torch.uint8, device="cuda")
+    verd = torch.empty(n * N, dtype=torch.int8, device="cuda")
+    status = torch.empty(n, dtype=torch.int32, device="cuda")
+    out = torch.empty(n * CS, dtype=torch.uint8, device="cuda")
+    ms = {}
+    for name, rows in (("intact", coded_d), ("no_marker", bad)):
+        codec.repair_plan_batch(ctx, rows, n, cand, plan, verd, status)
+        codec.decode_batch(ctx, rows, n, plan, out, status)  # warm
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(6)]
+        ev[0].record()
+        for r in range(5):
+            codec.decode_batch(ctx, rows, n, plan, out, status)
+            ev[r + 1].record()
+        torch.cuda.synchronize()
+        ms[name] = float(np.median([ev[r].elapsed_time(ev[r + 1]) for r in range(5)]))
+        st = host(status)
+        assert st[0] == (6 if name == "no_marker" else 0), (name, st[:4])
+        assert (st[1:] == 0).all(), name
+        assert torch.equal(out[CS:], dev(data[CS:])), name
+    extra = ms["no_marker"] - ms["intact"]
+    print("no-marker worst case n=%d (%s): intact %.3f ms, no marker %.3f ms, extra %.3f ms"
+          % (n, _lib_decode_name(n), ms["intact"], ms["no_marker"], extra))
+    assert extra < 50.0, ms
+
+
+def _lib_decode_name(n):
+    from decds_amd._capi import lib
+    return lib().decds_decode_kernel_name(n).decode()
+
+
 @pytest.mark.usefixtures("decode_form")
 def test_chunkset_mirror_roundtrip_like_reference(ctx):
     # chunkset.rs:257-283 (fixed seeds instead of rand::rng())
