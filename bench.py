@@ -132,8 +132,8 @@ def cpu_baseline(n_sample, seed, repeats=5, cfg2_chunksets=103):
     by the cgroup quota; measured only when it differs) and `threads_16`. The sample holds at least
     one chunkset per thread. `value` is the strongest of them (its thread count in `cores`): the
     GPU/CPU ratio is quoted against the fastest CPU configuration measured. Beside it (BASELINE.md's
-    plan): the same codec on 1 thread, on config 2's sample (the 1 GiB blob's 103 chunksets) with all
-    cores and on config 1's single chunkset (one thread: the work is chunkset-parallel); one run each
+    plan): the same codec on 1 thread, on config 2's sample (the 1 GiB blob's 103 chunksets) with the
+    headline's thread count and on config 1's single chunkset (one thread: the work is chunkset-parallel); one run each
     of the row-pass forms (AVX2 nibble tables; the scalar table-driven loop rlnc 0.4.0 is recalled to
     use) on 16 threads. All produce the same bytes (tests/test_oracle.py)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -219,7 +219,7 @@ def cpu_baseline(n_sample, seed, repeats=5, cfg2_chunksets=103):
     cfg2_tag = " (config 2: the 1 GiB blob)" if cfg2_chunksets == 103 else ""
     extra["threads_1"] = dict(rnd(run(o.fast_blob_encode, o.fast_blob_repair, smp2, 1, min_s=1.0)), cores=1,
                               sample="%d chunksets%s, 1 thread" % (cfg2_chunksets, cfg2_tag))
-    th2 = min(allc, cfg2_chunksets)
+    th2 = min(head["cores"], cfg2_chunksets)  # the headline's thread count (more threads than the cgroup quota throttle, r07a)
     extra["cfg2"] = dict(rnd(median([run(o.fast_blob_encode, o.fast_blob_repair, smp2, th2, min_s=1.0)
                                      for _ in range(max(1, repeats))])), cores=th2,
                          sample="%d chunksets%s, %d threads" % (cfg2_chunksets, cfg2_tag, th2))
