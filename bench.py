@@ -398,7 +398,10 @@ def main():
             raise SystemExit("--rehearse-shard runs in a single process")
         rank, world = args.rehearse_shard
         rehearse = {"rank": rank, "world": world}
-    dist_on = world > 1 and rehearse is None
+    # DECDS_BENCH_DIST=1: the process-group path at any N, also N = 1 (a one-rank RCCL group: the only
+    # way a one-GPU box runs the N > 1 line's RCCL calls — init, barrier, device all_reduce,
+    # all_gather_object — on the device, tests/test_gpu_bench.py)
+    dist_on = (world > 1 or os.environ.get("DECDS_BENCH_DIST") == "1") and rehearse is None
     # DECDS_BENCH_BACKEND=gloo is a rehearsal mode for the N > 1 path on a box with fewer GPUs than
     # ranks (ranks share devices round-robin, timing reduced over gloo); the real runs use RCCL.
     backend = os.environ.get("DECDS_BENCH_BACKEND", "nccl")

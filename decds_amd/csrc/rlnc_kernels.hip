@@ -223,6 +223,16 @@ __device__ __forceinline__ void build_tables(uint8_t *lds, uint32_t cw, uint32_t
     }
 }
 
+// The lookups' inline-asm ds_read_b128 address the tables absolutely, from LDS byte 0 of the dynamic
+// area: a static __shared__ variable in the kernel would be placed first and move every table (round
+// 4's first TailLds build read wrong bytes that way). __builtin_amdgcn_groupstaticsize() is the
+// kernel's static LDS size, a constant the backend resolves: 0 compiles this to nothing, anything else
+// to a trap at the kernel's entry — the contract checked inside the kernel, not only by
+// tests/test_isa.py's look at the built code.
+__device__ __forceinline__ void tables_at_lds_zero() {
+    if (__builtin_amdgcn_groupstaticsize() != 0) __builtin_trap();
+}
+
 // byte product M[j][i] * x read back from the built tables (edge columns)
 __device__ __forceinline__ uint32_t tbl_mul(const uint8_t *lds, uint32_t i, uint32_t j, uint32_t x) {
     return lds[(i * 2 + 0) * TABLE_BYTES + (x & 15u) * ROW_BYTES + j] ^
@@ -594,6 +604,7 @@ void rlnc_encode_hash_kernel(const uint8_t *__restrict__ src, size_t n, const ui
                              uint8_t *__restrict__ dst, size_t pitch, uint32_t poly, uint32_t marker,
                              uint64_t first_id, const uint64_t *__restrict__ ids, uint32_t *__restrict__ sub) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    tables_at_lds_zero();
     constexpr uint32_t STEP = FH_STEP<DW>, STEPS = b3::CHUNK / STEP, BPS = STEP / b3::BLOCK;  // blocks per step
     const uint32_t cs = blockIdx.x / FH_WG_UNITS, gu = blockIdx.x % FH_WG_UNITS;
     if (cs >= n) return;
@@ -764,6 +775,7 @@ void rlnc_encode_sweep_kernel(const uint8_t *__restrict__ src, size_t n, const u
     // no static __shared__ here: the lookups' inline-asm ds_reads address the tables from LDS byte 0,
     // so everything lives in the dynamic allocation (2 table buffers, then the next-tile slot)
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    tables_at_lds_zero();
     PT_STAMP(0);
     constexpr uint32_t T = TILES<DW>;
     uint32_t ioff[K], ooff[N];
@@ -1012,6 +1024,7 @@ void rlnc_decode_kernel(const uint8_t *__restrict__ coded, size_t pitch, size_t 
                         const uint64_t *__restrict__ out_bases, uint32_t poly, uint32_t marker,
                         uint32_t *__restrict__ info) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    tables_at_lds_zero();
     TailLds &s_tail = *reinterpret_cast<TailLds *>(lds + LDS_BYTES);
     constexpr int DW = DECDS_DEC_DW;
     constexpr uint32_t T = TILES<DW>;
@@ -1157,6 +1170,7 @@ void rlnc_decode_sweep_kernel(const uint8_t *__restrict__ coded, size_t pitch, s
                               const uint64_t *__restrict__ out_bases, uint32_t poly, uint32_t marker,
                               uint32_t *__restrict__ counter, uint32_t *__restrict__ info) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    tables_at_lds_zero();
     TailLds &s_tail = *reinterpret_cast<TailLds *>(lds + 2 * LDS_BYTES + 16);
     constexpr uint32_t T = TILES<DW>;
     constexpr uint32_t phase = 0;

@@ -151,3 +151,24 @@ def test_bench_two_ranks_torchrun_per_rank_records():
         assert x["encode_ms"] > 0 and x["decode_ms"] > 0 and x["gpu_GiBps"] > 0
     assert d["scaling_point"] is False and "share" in d["scaling_note"]
     assert d["cpu_baseline"] is None and d["encode_batch_sweep"] is None
+
+
+@pytest.mark.gpu
+def test_bench_one_rank_rccl_group_runs_the_distributed_path():
+    # The N > 1 line's RCCL calls on the device (the RCCL path had never run): a
+    # one-rank process group over RCCL (DECDS_BENCH_DIST=1) — init_process_group("nccl", device_id=...),
+    # the barrier, the MAX all_reduce of the timing on a device tensor, all_gather_object of the per-rank
+    # records, destroy_process_group — around a cfg2 step, every repaired chunkset checked
+    env = dict(os.environ, DECDS_BENCH_DIST="1", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()),
+               RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1", "--steps", "2", "--warmup", "1",
+                        "--settle-s", "0.1", "--config", "cfg2", "--no-cpu-baseline", "--no-commit", "--no-sweep",
+                        "--no-extras"], capture_output=True, text=True, timeout=200, cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["world_size"] == 1 and d["backend"] == "rccl" and d["n_gpus"] == 1
+    assert d["scaling_point"] is True and len(d["per_rank"]) == 1
+    x = d["per_rank"][0]
+    assert x["chunksets"] == [0, 103] and x["repaired_checked"] == x["ready_chunksets"] >= 100

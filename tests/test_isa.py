@@ -213,3 +213,19 @@ def test_sweeps_trap_instead_of_spinning(tmp_path, which):
     assert sum("encode_sweep" in k for k in sweeps) >= 5 and any("decode_sweep" in k for k in sweeps), sorted(sweeps)
     for name, ins in sweeps.items():
         assert any(x.startswith("s_trap 2") for _, x in ins), name
+
+
+@pytest.mark.parametrize("which", LIBS)
+def test_table_kernels_guard_their_lds_base(tmp_path, which):
+    # rlnc_kernels.hip tables_at_lds_zero(): every kernel whose inline-asm lookups address the tables
+    # from LDS byte 0 checks its static LDS size at entry and traps if it is not 0 (the compare survives
+    # as `s_cmp_eq_u32 0, 0` or `s_cmp_lg_u32 0, 0` — the size is filled in after instruction selection)
+    if not os.path.exists(OBJDUMP):
+        pytest.skip("llvm-objdump not in this image")
+    funcs = _functions(_device_code(tmp_path, which))
+    table = {k: v for k, v in funcs.items() if any(s in k for s in ("encode_sweep_kernel", "decode_sweep_kernel",
+                                                                    "rlnc_decode_kernel", "encode_hash_kernel"))}
+    assert len(table) >= 5, sorted(funcs)[:20]
+    for name, ins in table.items():
+        assert any(x.startswith("s_trap 2") for _, x in ins), name
+        assert any(re.match(r"s_cmp_(eq|lg)_u32 0, 0$", x) for _, x in ins[:8]), (name, ins[:8])
