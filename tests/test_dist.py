@@ -124,3 +124,29 @@ def test_init_failure_exits_with_a_message_not_a_hang():
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
     assert r.returncode == 3, (r.returncode, r.stderr[-1500:])
     assert "rank 0/2: gloo process group init failed" in r.stderr and "unreachable" not in r.stdout
+
+
+def test_cpu_baseline_thread_counts(monkeypatch):
+    # bench.cpu_threads: every usable CPU (the reference's rayon pool on all cores), rayon's default pool
+    # (Rust's available_parallelism caps the usable CPUs by the cgroup quota: 16 of 256 on the GPU box,
+    # BENCH r07a) and 16; the quota parsed from cgroup v2 cpu.max
+    monkeypatch.setattr(bench, "usable_cpus", lambda: 256)
+    monkeypatch.setattr(bench, "cgroup_cpus", lambda: 16.0)
+    assert bench.cpu_threads() == {"all_cores": 256, "rayon_default": 16, "threads_16": 16}
+    monkeypatch.setattr(bench, "cgroup_cpus", lambda: 2.5)
+    assert bench.cpu_threads()["rayon_default"] == 3
+    monkeypatch.setattr(bench, "cgroup_cpus", lambda: None)
+    assert bench.cpu_threads() == {"all_cores": 256, "rayon_default": 256, "threads_16": 16}
+    monkeypatch.setattr(bench, "usable_cpus", lambda: 8)
+    assert bench.cpu_threads() == {"all_cores": 8, "rayon_default": 8, "threads_16": 8}
+
+
+def test_cgroup_quota_parsing(monkeypatch, tmp_path):
+    import builtins
+    real_open = builtins.open
+    for text, want in (("1600000 100000\n", 16.0), ("max 100000\n", None), ("garbage\n", None)):
+        f = tmp_path / "cpu.max"
+        f.write_text(text)
+        monkeypatch.setattr(builtins, "open", lambda p, *a, **k: real_open(str(f) if p == "/sys/fs/cgroup/cpu.max" else p, *a, **k))
+        assert bench.cgroup_cpus() == want
+        monkeypatch.setattr(builtins, "open", real_open)
