@@ -35,12 +35,12 @@ for step in "$@"; do
       [ "$kind" = fuse ] && { tool=tools/fusebench.py; extra=""; }
       # every variant build passes the static ISA checks (no static LDS under the tables, no spills, the
       # tile counter's pending register read only after its wait) before it runs: a variant that
-      # spilled that register hung a box's A/B (r06z14). (Not the sweep-guard presence check: the
-      # guard's own cost A/B runs a build without it.)
+      # spilled that register hung a box's A/B (r06z14). (Not the guard presence checks — sweep
+      # guard, LDS-base guard: their own cost A/Bs run builds without them.)
       for spec in ${libs//,/ }; do
         lib=${spec%%[:@]*}
         [ "$lib" = default ] && continue
-        DECDS_LIB=$lib timeout -k 10 300 python -m pytest tests/test_isa.py -q -p no:cacheprovider -k "not trap" > "$out/isa_$(basename "$lib" .so).log" 2>&1 \
+        DECDS_LIB=$lib timeout -k 10 300 python -m pytest tests/test_isa.py -q -p no:cacheprovider -k "not trap and not lds_base" > "$out/isa_$(basename "$lib" .so).log" 2>&1 \
           || fail "isa check of $lib" "$out/isa_$(basename "$lib" .so).log"
       done
       for n in ${sizes//,/ }; do
