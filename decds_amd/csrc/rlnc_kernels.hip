@@ -738,6 +738,15 @@ constexpr uint32_t EDGE_WGS = 64;
 // atomic's data operand (1) and every workgroup took tile G + 1 again and again: a silent hang, not a
 // fault. Here a violated order ends the kernel with a trap (a named kernel fault on the
 // host side) instead of spinning. next and cur are wave-uniform (SGPRs): one compare per tile.
+// Both sweeps take their second tile statically (tile b + G of workgroup b) and only the third one on
+// from the counter (2G + the counter's value), so a workgroup's first grab goes out at its first loop
+// head and has a whole tile to return. Taken at kernel start and waited for before the first tile, the
+// G first grabs — all at once, on one counter line — held every workgroup's first tables back by 6-10
+// µs at 16-64 chunksets (phase trace r07d: first tables 6.6 µs after entry at the earliest, against
+// 2-4 µs for a launch without a counter). 0: round 4's order (study builds, A/B).
+#ifndef DECDS_STATIC_SECOND
+#define DECDS_STATIC_SECOND 1
+#endif
 #ifndef DECDS_SWEEP_GUARD
 #define DECDS_SWEEP_GUARD 1  // 0: study builds only (the guard's cost A/B)
 #endif
@@ -843,10 +852,10 @@ void rlnc_encode_sweep_kernel(const uint8_t *__restrict__ src, size_t n, const u
             asm volatile("global_atomic_add %0, %1, %2, off sc0" : "=v"(r) : "v"(counter), "v"(1u) : "memory");
         return r;
     };
-    // the first grab goes ahead of the tile's coefficient and input loads, so that the first loop head
-    // waits for it (and the coefficients) with vmcnt(26) — the ten input loads and 16 dropped stores
-    // still in flight — and the first tile's lookups take each input as it lands
-    uint32_t grab = grab_next();  // -> the tile after the next
+    // The first loop head waits for the coefficient bytes with vmcnt(26) — the ten input loads and 16
+    // dropped stores still in flight — so the first tile's lookups take each input as it lands. (With
+    // DECDS_STATIC_SECOND 0 the first grab goes out here, ahead of those loads, and that wait covers it.)
+    uint32_t grab = DECDS_STATIC_SECOND ? 0u : grab_next();  // (static second tile: first grab at the loop head)
     asm volatile("" ::: "memory");
     uint32_t cw = table_coeffs_all<K, N>(coeffs + (size_t)cs * N * K, K);
     Vec<DW> x[K];
@@ -874,7 +883,7 @@ void rlnc_encode_sweep_kernel(const uint8_t *__restrict__ src, size_t n, const u
                 asm volatile("s_waitcnt vmcnt(26)" ::: "memory");
             else
                 asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-            if (threadIdx.x == 0) s_next = G + grab;
+            if (threadIdx.x == 0) s_next = DECDS_STATIC_SECOND ? (first ? t + G : 2 * G + grab) : G + grab;
         }
         first = false;
         lds_barrier();
@@ -1225,11 +1234,17 @@ void rlnc_decode_sweep_kernel(const uint8_t *__restrict__ coded, size_t pitch, s
     uint32_t colt = cur.ready ? col_of(k) : OOB_COL;
     Vec<DW> x[K];
     load_block<K, DW>(x, cur.ibase, cur.ioff, colt);
+#if DECDS_STATIC_SECOND
+    uint32_t grab = 0;  // the second tile is static (k + G): the first grab goes out in the loop
+    lds_barrier();      // the edge pass's table readers are done
+    uint32_t kn = k + G;
+#else
     uint32_t grab = grab_next();
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (threadIdx.x == 0) s_next = counter ? G + grab : k + G;
     lds_barrier();  // also: the edge pass's table readers are done
     uint32_t kn = __builtin_amdgcn_readfirstlane(s_next);
+#endif
     sweep_guard(kn, k);
     uint32_t more;
 #pragma unroll 1
@@ -1247,7 +1262,7 @@ void rlnc_decode_sweep_kernel(const uint8_t *__restrict__ coded, size_t pitch, s
         combine_block<K, K, DW, 0, NoSink, 0, true, HB>(x, cur.obase, ooff, colt, nxt.ibase, nxt.ioff, coln);
         // the counter's answer: everything but this tile's 2K prefetch loads and stores has landed
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * K) : "memory");
-        if (threadIdx.x == 0) s_next = counter ? G + grab : kn + G;
+        if (threadIdx.x == 0) s_next = counter ? (DECDS_STATIC_SECOND ? 2 * G : G) + grab : kn + G;
         lds_barrier();
         k = kn;
         kn = __builtin_amdgcn_readfirstlane(s_next);
