@@ -62,6 +62,9 @@ constexpr uint32_t DEC_LDS = LDS_BYTES + 32;                   // one-tile decod
 #ifndef DECDS_ENC_HB
 #define DECDS_ENC_HB 2  // encode lookup group size (bytes of an input dword per group)
 #endif
+#ifndef DECDS_ENC_SMALL_HB
+#define DECDS_ENC_SMALL_HB 2  // the same for the 8-column small-batch form (4 waves/SIMD: groups of 4 spill)
+#endif
 #ifndef DECDS_DEC_UNIT
 #define DECDS_DEC_UNIT 1  // decode tiles per workgroup (+3...+11 % against 8 once the tables stopped being replicated, r02e)
 #endif
@@ -897,7 +900,7 @@ void rlnc_encode_sweep_kernel(const uint8_t *__restrict__ src, size_t n, const u
         more = tn < total;
         const uint32_t csn = more ? tn / T : cs;
         CoeffBytes cb = table_coeff_bytes<K, N>(coeffs + (size_t)csn * N * K, K);
-        combine_block<K, N, DW, 0, NoSink, SAUX, true, DECDS_ENC_HB>(x, dst + (size_t)cs * N * pitch, ooff, col_of(t),
+        combine_block<K, N, DW, 0, NoSink, SAUX, true, DW == 4 ? DECDS_ENC_HB : DECDS_ENC_SMALL_HB>(x, dst + (size_t)cs * N * pitch, ooff, col_of(t),
                                                                   src + (size_t)csn * CS, ioff, more ? col_of(tn) : OOB_COL);
         cw = table_coeff_pack<K>(cb);
         lds_barrier();
