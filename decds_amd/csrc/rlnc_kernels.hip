@@ -750,9 +750,6 @@ constexpr uint32_t EDGE_WGS = 64;
 #ifndef DECDS_STATIC_SECOND
 #define DECDS_STATIC_SECOND 1
 #endif
-#ifndef DECDS_COEFF_FIRST
-#define DECDS_COEFF_FIRST 0  // encode sweep: wait for the first tile's coefficient bytes before its input loads
-#endif
 #ifndef DECDS_SWEEP_GUARD
 #define DECDS_SWEEP_GUARD 1  // 0: study builds only (the guard's cost A/B)
 #endif
@@ -864,11 +861,6 @@ void rlnc_encode_sweep_kernel(const uint8_t *__restrict__ src, size_t n, const u
     uint32_t grab = DECDS_STATIC_SECOND ? 0u : grab_next();  // (static second tile: first grab at the loop head)
     asm volatile("" ::: "memory");
     uint32_t cw = table_coeffs_all<K, N>(coeffs + (size_t)cs * N * K, K);
-#if DECDS_COEFF_FIRST
-    // the coefficient bytes before any input load goes out: issued together with every workgroup's first
-    // inputs (the whole first round's, 20 MB at 16 chunksets) their lines' fills queued behind that flood
-    asm volatile("s_waitcnt vmcnt(0)" : "+v"(cw)::"memory");
-#endif
     Vec<DW> x[K];
     load_block<K, DW>(x, src + (size_t)cs * CS, ioff, col_of(t));
     asm volatile("" ::: "memory");
