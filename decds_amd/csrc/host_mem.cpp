@@ -358,9 +358,31 @@ hipError_t copy_h2d(uint8_t *d, const uint8_t *h, size_t n, bool pinned, BounceR
     return pinned ? hipMemcpyAsync(d, h, n, hipMemcpyHostToDevice, s) : ring.h2d(d, h, n, s);
 }
 
+// Device -> page-locked host copies of more than a few tens of MB are split into D2H_PIECE pieces: one
+// hipMemcpyAsync of 270 MB (a 16-chunkset batch of coded rows) ran at 30 GB/s on the box whatever the
+// host memory (hipHostMalloc coherent or not, hipHostRegister'd), one of 16 MiB at 54 GB/s, and a
+// kernel storing straight into the host buffer at 55 GB/s (tools/d2hbench.hip, r07j); a trace of the
+// blob encode showed the large copy executed as 8 MiB blit kernels with gaps as long as the kernels
+// between them (r07b). DECDS_D2H_PIECE_MB overrides the piece (0: one copy, round 4's behaviour).
+static size_t d2h_piece() {
+    static const size_t piece = [] {
+        const char *v = std::getenv("DECDS_D2H_PIECE_MB");
+        return v && *v ? (size_t)std::strtoull(v, nullptr, 10) << 20 : (size_t)16 << 20;
+    }();
+    return piece;
+}
+
+hipError_t d2h_pieces(uint8_t *h, const uint8_t *d, size_t n, hipStream_t s) {
+    const size_t piece = d2h_piece();
+    if (piece == 0 || n <= piece) return hipMemcpyAsync(h, d, n, hipMemcpyDeviceToHost, s);
+    for (size_t o = 0; o < n; o += piece)
+        if (hipError_t e = hipMemcpyAsync(h + o, d + o, std::min(piece, n - o), hipMemcpyDeviceToHost, s)) return e;
+    return hipSuccess;
+}
+
 hipError_t copy_d2h(uint8_t *h, const uint8_t *d, size_t n, bool pinned, BounceRing &ring, hipStream_t s) {
     if (n == 0) return hipSuccess;
-    return pinned ? hipMemcpyAsync(h, d, n, hipMemcpyDeviceToHost, s) : ring.d2h(h, d, n, s);
+    return pinned ? d2h_pieces(h, d, n, s) : ring.d2h(h, d, n, s);
 }
 
 }  // namespace decds

@@ -83,5 +83,7 @@ struct BounceRing {
 // is registered, else through `ring` (which must then be flushed before the host data is read).
 hipError_t copy_h2d(uint8_t *d, const uint8_t *h, size_t n, bool pinned, BounceRing &ring, hipStream_t s);
 hipError_t copy_d2h(uint8_t *h, const uint8_t *d, size_t n, bool pinned, BounceRing &ring, hipStream_t s);
+// hipMemcpyAsync device -> page-locked host in pieces (host_mem.cpp: large single copies run at half rate)
+hipError_t d2h_pieces(uint8_t *h, const uint8_t *d, size_t n, hipStream_t s);
 
 }  // namespace decds
