@@ -14,6 +14,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <functional>
 #include <mutex>
@@ -41,8 +42,29 @@ struct Pipe {
     hipEvent_t in_done[SLOTS] = {}, k_done[SLOTS] = {}, out_done[SLOTS] = {};
     hipError_t init() {
         hipError_t e;
-        for (hipStream_t *st : {&h2d, &comp, &d2h})
-            if ((e = hipStreamCreateWithFlags(st, hipStreamNonBlocking))) return e;
+        // Stream priorities keep the two copy directions on different hardware queues. HIP backs the
+        // streams of each priority level with a pool of at most GPU_MAX_HW_QUEUES (4) queues and, once
+        // a pool is full, puts a new stream on the pool's least-used queue: with three equal-priority
+        // streams created per call, whether H2D and D2H landed on one queue (copies then run one after
+        // the other: blob encode 49-50 ms instead of 38 at 1 GiB, r07r) depended on how many streams the
+        // process already held. H2D and the kernels go on the high-priority pool (empty in most
+        // processes, so the two get queues of their own), D2H on the normal one: the copy directions can
+        // never share a queue, and encode/repair held 38 / 30 ms with 0-4 caller streams alive (r07u).
+        // The range is [0, -1] here: two levels. DECDS_PIPE_STREAMS=plain (all normal) | h2d (only H2D
+        // high) are study switches.
+        static const int mode = [] {
+            const char *v = std::getenv("DECDS_PIPE_STREAMS");
+            return !v ? 2 : !std::strcmp(v, "plain") ? 0 : !std::strcmp(v, "h2d") ? 1 : 2;
+        }();
+        int least = 0, greatest = 0;
+        if (mode == 0) {
+            for (hipStream_t *st : {&h2d, &comp, &d2h})
+                if ((e = hipStreamCreateWithFlags(st, hipStreamNonBlocking))) return e;
+        } else if ((e = hipDeviceGetStreamPriorityRange(&least, &greatest)) ||
+                   (e = hipStreamCreateWithPriority(&h2d, hipStreamNonBlocking, mode ? greatest : least)) ||
+                   (e = hipStreamCreateWithPriority(&comp, hipStreamNonBlocking, mode == 2 ? greatest : least)) ||
+                   (e = hipStreamCreateWithPriority(&d2h, hipStreamNonBlocking, least)))
+            return e;
         for (int i = 0; i < SLOTS; i++)
             for (hipEvent_t *ev : {&in_done[i], &k_done[i], &out_done[i]}) {
                 if ((e = hipEventCreateWithFlags(ev, hipEventDisableTiming))) return e;

@@ -283,3 +283,30 @@ def test_launch_reports_an_earlier_pending_hip_error_by_name(ctx):
     codec.encode_batch(ctx, src, n, cv, dst)       # consumed: the next launch runs
     torch.cuda.synchronize()
     assert dst.view(n * N, F)[:, :K].cpu().numpy().tolist() == [[1] * K] * (n * N)
+
+
+
+def test_blob_host_rate_does_not_depend_on_caller_streams():
+    # The host pipeline's H2D and D2H streams must never share a hardware queue: HIP backs the streams
+    # of a priority level with at most 4 queues and puts a new stream on the least-used one, so with
+    # equal priorities the two copy directions could land on one queue — and run one after the other —
+    # depending on how many streams the process held (blob encode 49-50 ms instead of 38 at 1 GiB with
+    # one caller stream alive, r07r). blob.cpp Pipe::init gives them different priority levels. Fresh
+    # processes (tools/e2e_bench.py) holding 0, 1 and 2 caller streams when the context is created must
+    # encode a 1 GiB blob at one rate.
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    enc = []
+    for pre in (0, 1, 2):
+        r = subprocess.run([sys.executable, os.path.join(root, "tools", "e2e_bench.py"), "--gib", "1", "--batch", "16",
+                            "--reps", "4", "--memory", "alloc", "--pre-streams", str(pre)], capture_output=True, text=True,
+                           timeout=100, cwd=root)
+        assert r.returncode == 0, r.stderr[-2000:]
+        d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith('{"blob')][-1])
+        assert d["ready"] == d["chunksets"] and d["spot_check_ok"]
+        enc.append(d["encode_median_s"])
+    print("encode medians (s) with 0, 1, 2 caller streams:", enc)
+    assert max(enc) < 1.15 * min(enc), enc

@@ -18,8 +18,40 @@ def main():
     ap.add_argument("--gib", type=float, default=4.0)
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--reps", type=int, default=2)
+    ap.add_argument("--memory", choices=("register", "alloc"), default="register",
+                    help="caller buffers page-locked by decds_host_register (default) or allocated by decds_host_alloc")
+    ap.add_argument("--with-torch", action="store_true", help="initialise torch on the device first (as bench.py does)")
+    ap.add_argument("--with-pattern", action="store_true", help="load and use the pattern-ceiling build first (as bench.py does)")
+    ap.add_argument("--device-gib", type=float, default=0.0,
+                    help="hold this much device memory (torch) before the page-locked buffers are allocated")
+    ap.add_argument("--pre-streams", type=int, default=0,
+                    help="create this many HIP streams (torch.cuda.Stream) before the library's, and keep them")
+    ap.add_argument("--cpus", default=None, help="run on these CPUs only (e.g. 0-15 or 128-143): NUMA placement of the "
+                                                    "page-locked buffers")
     a = ap.parse_args()
+    if a.cpus:
+        lo, _, hi = a.cpus.partition("-")
+        os.sched_setaffinity(0, range(int(lo), int(hi or lo) + 1))
     import numpy as np
+    if a.with_torch or a.with_pattern or a.device_gib or a.pre_streams:
+        import torch
+        torch.cuda.init()
+        torch.zeros(1, device="cuda")
+        print(json.dumps({"stream_priority_range": torch.cuda.Stream.priority_range()}))
+        streams = [torch.cuda.Stream() for _ in range(a.pre_streams)]
+        for s_ in streams:  # a stream takes its hardware queue when first used
+            with torch.cuda.stream(s_):
+                torch.zeros(1, device="cuda")
+        torch.cuda.synchronize()
+        held = torch.empty(int(a.device_gib * (1 << 30)), dtype=torch.uint8, device="cuda") if a.device_gib else None
+    if a.with_pattern:
+        import ctypes
+        Lp = ctypes.CDLL(os.path.join(ROOT, "tools", "bin", "libdecds_pattern.so"))
+        h = ctypes.c_void_p()
+        Lp.decds_ctx_create.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]
+        Lp.decds_ctx_destroy.argtypes = [ctypes.c_void_p]
+        assert Lp.decds_ctx_create(0, ctypes.byref(h)) == 0
+        Lp.decds_ctx_destroy(h)
     import decds_amd
     from decds_amd import codec
     from decds_amd._capi import CHUNKSET_BYTES as CS, K, N
@@ -37,10 +69,16 @@ def main():
     gen_s = time.time() - t
     # cold: every call pins/unpins the caller buffers itself (first rep); warm: buffers pinned once
     enc, rep = [], []
-    coded_buf = np.empty((n * N, CS // K + 1 + K), dtype=np.uint8)
-    out_buf = np.empty(blob_len, dtype=np.uint8)
+    if a.memory == "alloc":  # page-locked from the start: every call is warm
+        from decds_amd.blob import HostBuffer
+        hbs = [HostBuffer(blob_len), HostBuffer(n * N * (CS // K + 1 + K)), HostBuffer(blob_len)]
+        hbs[0].array[:] = blob
+        blob, coded_buf, out_buf = hbs[0].array, hbs[1].array.reshape(n * N, -1), hbs[2].array
+    else:
+        coded_buf = np.empty((n * N, CS // K + 1 + K), dtype=np.uint8)
+        out_buf = np.empty(blob_len, dtype=np.uint8)
     for rep_i in range(a.reps + 1):
-        if rep_i == 1:
+        if rep_i == 1 and a.memory == "register":
             for b in (blob, coeffs, coded_buf, out_buf):
                 codec.host_register(b)
         t = time.perf_counter()
@@ -54,7 +92,9 @@ def main():
                for c in np.nonzero(ok)[0][:8])
     cold_e, cold_r = enc[0], rep[0]
     e, r = min(enc[1:]), min(rep[1:])
-    print(json.dumps({"blob_gib": a.gib, "chunksets": n, "batch": a.batch, "encode_s": round(e, 4),
+    e_med, r_med = float(np.median(enc[1:])), float(np.median(rep[1:]))
+    print(json.dumps({"blob_gib": a.gib, "memory": a.memory, "cpus": a.cpus, "device_gib": a.device_gib, "pre_streams": a.pre_streams, "chunksets": n, "batch": a.batch,
+                      "encode_median_s": round(e_med, 4), "repair_median_s": round(r_med, 4), "encode_s": round(e, 4),
                       "repair_s": round(r, 4), "encode_blob_GiBps": round(blob_len / (1 << 30) / e, 2),
                       "repair_blob_GiBps": round(blob_len / (1 << 30) / r, 2),
                       "encode_pcie_GBps": round((blob_len + n * N * (CS // K + 1 + K)) / e / 1e9, 2),
