@@ -95,6 +95,39 @@ struct CommitOut {
     uint64_t first_id;
 };
 
+// Batch sizes of a host-path call over n chunksets. A pipeline over the three engines only overlaps
+// once its first batch is in and until its last one is out: the first H2D and the last D2H run with
+// the link's other direction idle (a 16-chunkset batch: 168 MB of inputs, ~3 ms). Ramped, the call
+// starts and ends with small batches (batch/8, /4, /2 ... /2, /4, /8, /8) so those unoverlapped ends
+// are short, and runs full batches in between: blob encode of 1 GiB −5 % at batch 16, −10 % at 32,
+// repair ±1 % (r08c). DECDS_HOST_RAMP=0: fixed batches, =enc: ramped encode
+// only (study switches).
+std::vector<size_t> batch_sizes(size_t n, size_t batch, bool repair) {
+    static const int mode = [] {  // 0 off, 1 encode only, 2 both
+        const char *v = std::getenv("DECDS_HOST_RAMP");
+        return !v ? 2 : !std::strcmp(v, "0") ? 0 : !std::strcmp(v, "enc") ? 1 : 2;
+    }();
+    const bool ramp = repair ? mode == 2 : mode >= 1;
+    std::vector<size_t> head, tail, out;
+    if (ramp && batch >= 16) {  // at 8, batches of 1 cost more than the short ends save (r08c)
+        head = {batch / 8, batch / 4, batch / 2};
+        tail = {batch / 2, batch / 4, batch / 8, batch / 8};
+    }
+    size_t ends = 0;
+    for (size_t x : head) ends += x;
+    for (size_t x : tail) ends += x;
+    if (ends == 0 || n < ends + batch) {  // too short to ramp
+        for (size_t b0 = 0; b0 < n; b0 += batch) out.push_back(std::min(batch, n - b0));
+        return out;
+    }
+    out = head;
+    size_t mid = n - ends;
+    if (mid % batch) out.push_back(mid % batch);  // the odd batch first: it overlaps like the rest
+    for (size_t i = 0; i < mid / batch; i++) out.push_back(batch);
+    out.insert(out.end(), tail.begin(), tail.end());
+    return out;
+}
+
 // End of a host-path call: complete the deferred copy-outs, drain every stream; after a failure
 // the rings drop whatever they still hold for this call.
 int finish_call(decds_ctx *ctx, Pipe &pp, int rc) {
@@ -150,9 +183,10 @@ int encode_range(decds_ctx *ctx, const uint8_t *blob, size_t blob_len, const uin
     };
     int rc = DECDS_OK, pend = -1;
     size_t pend_b0 = 0, pend_nb = 0;
-    for (size_t b0 = 0, it = 0; b0 < n && rc == DECDS_OK; b0 += batch, it++) {
+    const std::vector<size_t> sizes = batch_sizes(n, batch, false);
+    for (size_t b0 = 0, it = 0; it < sizes.size() && rc == DECDS_OK; b0 += sizes[it], it++) {
         const int k = (int)(it % SLOTS);
-        const size_t nb = std::min(batch, n - b0);
+        const size_t nb = sizes[it];
         const size_t off = b0 * CS, have = std::min(blob_len - off, nb * CS);
         // inputs of slot k: free once the slot's previous kernel has read them
         if ((e = hipStreamWaitEvent(pp.h2d, pp.k_done[k], 0)) ||
@@ -267,10 +301,11 @@ int repair_range(decds_ctx *ctx, const uint8_t *coded_host, size_t n, const uint
         pending_b0[k] = (size_t)-1;
         return DECDS_OK;
     };
-    for (size_t b0 = 0, it = 0; b0 < n && rc == DECDS_OK; b0 += batch, it++) {
+    const std::vector<size_t> sizes = batch_sizes(n, batch, true);
+    for (size_t b0 = 0, it = 0; it < sizes.size() && rc == DECDS_OK; b0 += sizes[it], it++) {
         const int k = (int)(it % SLOTS);
         if ((rc = finish(k))) break;  // slot k's previous batch fully done: all its buffers are free
-        const size_t nb = std::min(batch, n - b0);
+        const size_t nb = sizes[it];
         // the accepted rows keep their own row slots on the device (slot layout = host layout less
         // b0 chunksets), so runs of consecutive accepted rows — across chunkset boundaries too —
         // cross the link as one copy each instead of one copy per row

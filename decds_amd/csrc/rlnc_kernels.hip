@@ -20,7 +20,10 @@
 // Only the shipped configuration lives here, plus three study hooks that compile to nothing by default
 // (DECDS_PHASE_TRACE: per-workgroup phase stamps of the encode sweep for tools/phasetrace.py;
 // DECDS_STUDY_NO_EDGE: the encode without its edge pass, timing only; DECDS_STUDY_PATTERN: the
-// kernels' memory pattern without their lookups — the pattern ceilings bench.py reports). The round-1 study variants
+// kernels' memory pattern without their lookups — the pattern ceilings bench.py reports;
+// DECDS_STUDY_ALIGNED_PIECES=1/2/3: piece i of a chunkset addressed at i * L rounded down to 256 bytes /
+// at i * (L - 1) - 16 i / - 4 i in the streaming kernels, timing only — what the pieces' i-byte
+// misalignment costs). The round-1 study variants
 // (persistent walks, XCD bands, per-half work shares, per-tile barriers, the warp-specialised kernel)
 // are in git history (tools/study/rlnc_kernels_r01_study.hip at a5d9101) with their measurements in
 // DESIGN.md §8.
@@ -485,6 +488,18 @@ __device__ __forceinline__ void combine_block(Vec<DW> (&x)[NIN], uint8_t *obase,
 // (rlnc_encode_hash_kernel) walks the same geometry in 128-byte steps. On rows at 16 mod 128 every
 // wave's store run is then 128-byte aligned.
 constexpr uint32_t MAX_FULL_PHASE = (uint32_t)(CS - (K - 1) * L) - MAIN_COLS;
+// piece i's byte offset in a chunkset (the study build rounds it down to 256 bytes: timing only)
+__device__ __forceinline__ uint32_t piece_off(int i) {
+#if DECDS_STUDY_ALIGNED_PIECES == 1
+    return (uint32_t)(i * L) & ~255u;
+#elif DECDS_STUDY_ALIGNED_PIECES == 2  // 16-byte aligned, lines not (never past i * L: stays in bounds)
+    return (uint32_t)(i * (L - 1) - 16 * i);
+#elif DECDS_STUDY_ALIGNED_PIECES == 3  // dword aligned
+    return (uint32_t)(i * (L - 1) - 4 * i);
+#else
+    return (uint32_t)(i * L);
+#endif
+}
 static_assert(MAX_FULL_PHASE == 7, "layout");
 template <int DW> constexpr uint32_t COLS = 4 * DW;
 template <int DW> constexpr uint32_t BLOCKS = MAIN_COLS / COLS<DW>;                 // 65535 / 131070
@@ -792,7 +807,7 @@ void rlnc_encode_sweep_kernel(const uint8_t *__restrict__ src, size_t n, const u
     constexpr uint32_t T = TILES<DW>;
     uint32_t ioff[K], ooff[N];
 #pragma unroll
-    for (int i = 0; i < (int)K; i++) ioff[i] = (uint32_t)(i * L);
+    for (int i = 0; i < (int)K; i++) ioff[i] = piece_off(i);
 #pragma unroll
     for (int j = 0; j < (int)N; j++) ooff[j] = (uint32_t)(j * pitch + K);
     // 1. coding-vector prefixes and edge columns of chunksets b, b + G, ... (tables in buffer 1); with
@@ -1066,7 +1081,7 @@ void rlnc_decode_kernel(const uint8_t *__restrict__ coded, size_t pitch, size_t 
 #pragma unroll
     for (int k = 0; k < (int)K; k++) ioff[k] = (uint32_t)(sel[k] * pitch + K);
 #pragma unroll
-    for (int i = 0; i < (int)K; i++) ooff[i] = (uint32_t)(i * L);
+    for (int i = 0; i < (int)K; i++) ooff[i] = piece_off(i);
     const uint8_t *ibase;
     uint8_t *obase;
     if (in_bases) {
@@ -1188,7 +1203,7 @@ void rlnc_decode_sweep_kernel(const uint8_t *__restrict__ coded, size_t pitch, s
     constexpr uint32_t phase = 0;
     uint32_t ooff[K];
 #pragma unroll
-    for (int i = 0; i < (int)K; i++) ooff[i] = (uint32_t)(i * L);
+    for (int i = 0; i < (int)K; i++) ooff[i] = piece_off(i);
     // 1. edge columns of the ready chunksets b, b + gridDim, ... (tables in buffer 1)
     for (uint32_t c = blockIdx.x; c < n; c += gridDim.x) {
         DecodeDesc d;

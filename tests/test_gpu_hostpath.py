@@ -39,11 +39,12 @@ def _cand_with_failures(coded, coeffs, n, rng, not_ready, broken, short):
     return cand, coded
 
 
-@pytest.mark.parametrize("batch,pinned", [(1, False), (2, True), (2, False), (3, True)])
-def test_blob_host_paths_reuse_every_slot(ctx, batch, pinned):
+@pytest.mark.parametrize("n,batch,pinned", [(7, 1, False), (7, 2, True), (7, 2, False), (7, 3, True), (48, 16, True),
+                                             (48, 16, False)])
+def test_blob_host_paths_reuse_every_slot(ctx, n, batch, pinned):
     # 7 chunksets in batches of 1-3: 3-7 batches over the 3 slots, so every slot is reused; the
-    # unready chunkset (4) and the repair-failed one (5) sit in reused slots; last chunkset ragged
-    n = 7
+    # unready chunkset (4) and the repair-failed one (5) sit in reused slots; last chunkset ragged.
+    # 48 in batches of 16: the ramped sizes (blob.cpp batch_sizes: 2, 4, 8, 2, 16, 8, 4, 2, 2)
     blob_len = (n - 1) * CS + 12345
     blob = o.fill_random(0xA5A5 + batch, blob_len).copy()
     part = blob[5 * CS:6 * CS]
@@ -63,8 +64,8 @@ def test_blob_host_paths_reuse_every_slot(ctx, batch, pinned):
     if pinned:
         coded_bad = _as(coded_out, coded_bad)
     out, status = codec.blob_repair_host(ctx, coded_bad, cand, blob_len, batch=batch, out=rep_out)
-    assert status.tolist() == [0, 0, 0, 0, 5, 6, 0]
-    assert ref_st.tolist() == [o.OK, o.OK, o.OK, o.OK, o.NOT_ALL, o.INVALID_DATA, o.OK]
+    assert status.tolist() == [0, 0, 0, 0, 5, 6] + [0] * (n - 6)
+    assert ref_st.tolist() == [o.OK, o.OK, o.OK, o.OK, o.NOT_ALL, o.INVALID_DATA] + [o.OK] * (n - 6)
     cut = int(np.nonzero(blob[2 * CS:3 * CS] == o.MARKER)[0][-1])
     for c in range(n):
         lo, hi = c * CS, min(blob_len, (c + 1) * CS)
