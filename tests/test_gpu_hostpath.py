@@ -294,20 +294,22 @@ def test_blob_host_rate_does_not_depend_on_caller_streams():
     # depending on how many streams the process held (blob encode 49-50 ms instead of 38 at 1 GiB with
     # one caller stream alive, r07r). blob.cpp Pipe::init gives them different priority levels. Fresh
     # processes (tools/e2e_bench.py) holding 0, 1 and 2 caller streams when the context is created must
-    # encode a 1 GiB blob at one rate.
+    # encode a 1 GiB blob at one rate. Each case runs twice, interleaved, and keeps its faster run: the
+    # queue sharing is a property of the process's stream state (slow on every run), while the box's
+    # link can be slow for one whole process now and then (60 ms once in r08e, 36-39 ms otherwise).
     import json
     import os
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    enc = []
-    for pre in (0, 1, 2):
+    enc = {}
+    for pre in (0, 1, 2, 0, 1, 2):
         r = subprocess.run([sys.executable, os.path.join(root, "tools", "e2e_bench.py"), "--gib", "1", "--batch", "16",
                             "--reps", "4", "--memory", "alloc", "--pre-streams", str(pre)], capture_output=True, text=True,
                            timeout=100, cwd=root)
         assert r.returncode == 0, r.stderr[-2000:]
         d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith('{"blob')][-1])
         assert d["ready"] == d["chunksets"] and d["spot_check_ok"]
-        enc.append(d["encode_median_s"])
-    print("encode medians (s) with 0, 1, 2 caller streams:", enc)
-    assert max(enc) < 1.15 * min(enc), enc
+        enc[pre] = min(enc.get(pre, 1e9), d["encode_median_s"])
+    print("encode medians (s), faster of two processes, with 0, 1, 2 caller streams:", enc)
+    assert max(enc.values()) < 1.15 * min(enc.values()), enc

@@ -9,7 +9,12 @@
 //               workgroups), alone
 //   memcpy+h2d  the hipMemcpyAsync D2H beside an H2D hipMemcpyAsync of the same size on another stream
 //   kernel+h2d  the kernel D2H beside the same H2D
-// Prints one JSON line per variant (GB/s of the D2H; the H2D's own rate beside it).
+//   h2dkernel   the reverse direction by kernel: the copy kernel loading from the host buffer into device
+//               memory (a gather of host rows without per-run hipMemcpyAsync calls), alone
+//   h2dkernel+d2h  that kernel beside a hipMemcpyAsync D2H of the same size on another stream
+// With a fifth argument "sizes": only hipMemcpyAsync D2H alone at 1, 4, 16, 64 MiB and BYTES, in one process.
+// Prints one JSON line per variant (GB/s of the D2H; the H2D's own rate beside it; for the h2dkernel
+// variants the kernel's H2D rate, and the D2H's beside it).
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/d2hbench.hip -o tools/bin/d2hbench
 #include <hip/hip_runtime.h>
 
@@ -71,7 +76,63 @@ int main(int argc, char **argv) {
     CK(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
     hipEvent_t a1, b1, a2, b2;
     for (hipEvent_t *e : {&a1, &b1, &a2, &b2}) CK(hipEventCreate(e));
-    for (int variant = 0; variant < 4; variant++) {
+    void *hsrc_dev = nullptr;
+    CK(hipHostGetDevicePointer(&hsrc_dev, hsrc, 0));
+    if (argc > 5 && !std::strcmp(argv[5], "sizes")) {  // hipMemcpyAsync D2H alone at 1 MiB ... BYTES, one process
+        for (size_t sz : {(size_t)1 << 20, (size_t)4 << 20, (size_t)16 << 20, (size_t)64 << 20, bytes}) {
+            if (sz > bytes) continue;
+            std::vector<double> ms;
+            for (int r = 0; r < reps + 1; r++) {
+                CK(hipDeviceSynchronize());
+                CK(hipEventRecord(a1, s1));
+                CK(hipMemcpyAsync(hdst, dsrc, sz, hipMemcpyDeviceToHost, s1));
+                CK(hipEventRecord(b1, s1));
+                CK(hipEventSynchronize(b1));
+                float m = 0;
+                CK(hipEventElapsedTime(&m, a1, b1));
+                if (r) ms.push_back(m);
+            }
+            const double t = median(ms);
+            std::printf("{\"variant\": \"memcpy-size\", \"bytes\": %zu, \"d2h_ms\": %.3f, \"d2h_GBps\": %.1f}\n", sz, t,
+                        sz / (t * 1e-3) / 1e9);
+        }
+        std::fflush(stdout);
+        return 0;
+    }
+    for (int variant = 0; variant < 6; variant++) {
+        if (variant >= 4) {  // H2D by kernel, alone / beside a D2H memcpy
+            const bool d2h = variant == 5;
+            std::vector<double> k_ms, d_ms;
+            for (int r = 0; r < reps + 1; r++) {
+                CK(hipDeviceSynchronize());
+                if (d2h) {
+                    CK(hipEventRecord(a2, s2));
+                    CK(hipMemcpyAsync(hdst, dsrc, bytes, hipMemcpyDeviceToHost, s2));
+                    CK(hipEventRecord(b2, s2));
+                }
+                CK(hipEventRecord(a1, s1));
+                hipLaunchKernelGGL(d2h_k, dim3(wgs), dim3(256), 0, s1, (const u32x4 *)hsrc_dev, (u32x4 *)ddst, n16);
+                CK(hipEventRecord(b1, s1));
+                CK(hipDeviceSynchronize());
+                CK(hipGetLastError());
+                float m1 = 0, m2 = 0;
+                CK(hipEventElapsedTime(&m1, a1, b1));
+                if (d2h) CK(hipEventElapsedTime(&m2, a2, b2));
+                if (r) {
+                    k_ms.push_back(m1);
+                    d_ms.push_back(m2);
+                }
+            }
+            unsigned char probe = 0;
+            CK(hipMemcpy(&probe, static_cast<unsigned char *>(ddst) + bytes / 2, 1, hipMemcpyDeviceToHost));
+            const double t1 = median(k_ms), t2 = median(d_ms);
+            std::printf("{\"variant\": \"h2dkernel%s\", \"bytes\": %zu, \"workgroups\": %d, \"h2d_ms\": %.3f, "
+                        "\"h2d_GBps\": %.1f, \"d2h_GBps\": %s, \"check\": %s}\n",
+                        d2h ? "+d2h" : "", bytes, wgs, t1, bytes / (t1 * 1e-3) / 1e9,
+                        d2h ? std::to_string(bytes / (t2 * 1e-3) / 1e9).c_str() : "null", probe == 1 ? "true" : "false");
+            std::fflush(stdout);
+            continue;
+        }
         const bool kern = variant & 1, h2d = variant & 2;
         std::vector<double> d2h_ms, h2d_ms;
         for (int r = 0; r < reps + 1; r++) {

@@ -26,6 +26,8 @@ def main():
                     help="hold this much device memory (torch) before the page-locked buffers are allocated")
     ap.add_argument("--pre-streams", type=int, default=0,
                     help="create this many HIP streams (torch.cuda.Stream) before the library's, and keep them")
+    ap.add_argument("--cand", choices=("random", "first", "all"), default="random",
+                    help="the rows repair gets: 10 random of 16 (default), rows 0-9, or all 16 in order")
     ap.add_argument("--cpus", default=None, help="run on these CPUs only (e.g. 0-15 or 128-143): NUMA placement of the "
                                                     "page-locked buffers")
     a = ap.parse_args()
@@ -65,7 +67,12 @@ def main():
     rng = np.random.default_rng(0x5EED0003)
     cand = np.full((n, N), 0xFF, np.uint8)
     for c in range(n):
-        cand[c, :K] = rng.permutation(N)[:K]
+        if a.cand == "random":
+            cand[c, :K] = rng.permutation(N)[:K]
+        elif a.cand == "first":
+            cand[c, :K] = np.arange(K)
+        else:
+            cand[c, :] = np.arange(N)
     gen_s = time.time() - t
     # cold: every call pins/unpins the caller buffers itself (first rep); warm: buffers pinned once
     enc, rep = [], []
@@ -93,7 +100,7 @@ def main():
     cold_e, cold_r = enc[0], rep[0]
     e, r = min(enc[1:]), min(rep[1:])
     e_med, r_med = float(np.median(enc[1:])), float(np.median(rep[1:]))
-    print(json.dumps({"blob_gib": a.gib, "memory": a.memory, "cpus": a.cpus, "device_gib": a.device_gib, "pre_streams": a.pre_streams, "chunksets": n, "batch": a.batch,
+    print(json.dumps({"blob_gib": a.gib, "memory": a.memory, "cpus": a.cpus, "device_gib": a.device_gib, "pre_streams": a.pre_streams, "cand": a.cand, "chunksets": n, "batch": a.batch,
                       "encode_median_s": round(e_med, 4), "repair_median_s": round(r_med, 4), "encode_s": round(e, 4),
                       "repair_s": round(r, 4), "encode_blob_GiBps": round(blob_len / (1 << 30) / e, 2),
                       "repair_blob_GiBps": round(blob_len / (1 << 30) / r, 2),
