@@ -699,7 +699,13 @@ def main():
                 line["scaling_note"] = ("ranks share devices (%d ranks on %d devices): a rehearsal of the N-rank "
                                         "path, not a scaling measurement" % (world, len(set(devs))))
         if world == 1 and not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(args.cpu_sample, 0xDEC05002)
+            cb = line["cpu_baseline"] = cpu_baseline(args.cpu_sample, 0xDEC05002)
+            # the GPU/CPU ratio against each CPU figure: `value` (the strongest CPU configuration: the
+            # cgroup's 16 CPUs, what rayon's default pool takes on the box) and all usable cores (throttled
+            # by that quota on the box) — a reported baseline, not kernel quality
+            ac = (cb.get("all_cores") or {}).get("value")
+            cb["gpu_over_cpu"] = {"vs_value": round(line["value"] / cb["value"], 2) if cb.get("value") else None,
+                                  "vs_all_cores": round(line["value"] / ac, 2) if ac else None}
         else:
             line["cpu_baseline"] = None
         print(json.dumps(line), flush=True)
