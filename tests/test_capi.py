@@ -148,3 +148,35 @@ def test_library_consumes_its_hip_failures():
                 if re.match(r"^\s*hip(?!LaunchKernelGGL|GetLastError)[A-Z]\w*\(", code):
                     bad.append("%s:%d: %s" % (f, no, line.strip()))
     assert not bad, "\n".join(bad)
+
+
+def _hip_versions(path, section):
+    """hip_X.Y symbol versions a shared object needs ("needs") or defines ("defs"), from readelf -V"""
+    import subprocess
+    out = subprocess.run(["readelf", "-V", path], capture_output=True, text=True, check=True).stdout
+    if section == "needs":
+        out = out.split("Version needs", 1)[-1]
+        return set(re.findall(r"Name: (hip_[0-9.]+)\s+Flags", out))
+    out = out.split("Version definition", 1)[-1].split("Version needs", 1)[0]
+    return set(re.findall(r"Name: (hip_[0-9.]+)", out))
+
+
+@pytest.mark.parametrize("lib", ["decds_amd/libdecds_rlnc.so", "tools/bin/libdecds_pattern.so"])
+def test_library_needs_only_hip_versions_torch_provides(lib):
+    # The library is loaded into processes whose HIP runtime is torch's bundled libamdhip64 (ROCm 7.0
+    # here), not /opt/rocm's (7.2): a HIP call newer than that runtime (hipMemcpyBatchAsync needs
+    # hip_7.1) makes the library fail to load at all there. Every hip_X.Y version it needs must be one
+    # torch's runtime defines.
+    import shutil
+    torch = pytest.importorskip("torch")
+    if not shutil.which("readelf"):
+        pytest.skip("readelf not in this image")
+    path = os.path.join(ROOT, lib)
+    if not os.path.exists(path):
+        pytest.skip("%s not built" % lib)
+    rt = os.path.join(os.path.dirname(torch.__file__), "lib", "libamdhip64.so")
+    if not os.path.exists(rt):
+        pytest.skip("torch has no bundled HIP runtime")
+    needs, defs = _hip_versions(path, "needs"), _hip_versions(rt, "defs")
+    assert needs, "no hip_* version needs found in %s" % lib
+    assert needs <= defs, sorted(needs - defs)
