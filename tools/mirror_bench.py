@@ -55,7 +55,7 @@ def main():
             x.join()
         dt = time.perf_counter() - t0
         print(json.dumps({"path": "decds_chunkset_new (ChunkSet::new + commitment)", "threads": T,
-                          "coalesced": os.environ.get("DECDS_CHUNKSET_COALESCE", "1") != "0",
+                          "coalesced": os.environ.get("DECDS_CHUNKSET_COALESCE", "0").strip() not in ("", "0"),
                           "chunksets": sum(counts), "GiBps": round(sum(counts) * CS / GIB / dt, 2)}), flush=True)
         # repair: RepairingChunkSet with 10 chunks already added, repair() timed
         cs = [decds_amd.ChunkSet(ctx, t, datas[t], coeffs[t]) for t in range(T)]
