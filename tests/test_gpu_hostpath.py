@@ -306,7 +306,7 @@ def test_blob_host_rate_does_not_depend_on_caller_streams():
     for pre in (0, 1, 2, 0, 1, 2):
         r = subprocess.run([sys.executable, os.path.join(root, "tools", "e2e_bench.py"), "--gib", "1", "--batch", "16",
                             "--reps", "4", "--memory", "alloc", "--pre-streams", str(pre)], capture_output=True, text=True,
-                           timeout=100, cwd=root)
+                           timeout=180, cwd=root)
         assert r.returncode == 0, r.stderr[-2000:]
         d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith('{"blob')][-1])
         assert d["ready"] == d["chunksets"] and d["spot_check_ok"]
