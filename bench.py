@@ -32,6 +32,48 @@ CONFIGS = {
 }
 
 
+class FenceFreeEvents:
+    """HIP timing events created with hipEventDisableSystemFence, recorded on a torch stream through the
+    HIP runtime torch already loaded. A default event (torch.cuda.Event) performs a system-scope fence —
+    an L2 writeback and invalidate — when it is recorded; these skip it ("can improve the accuracy of
+    timing measurements", hip_runtime_api.h), which matters only for launches of a few microseconds."""
+    DISABLE_SYSTEM_FENCE = 0x20000000
+
+    def __init__(self, k):
+        import ctypes
+        with open("/proc/self/maps") as f:
+            paths = sorted({ln.split()[-1] for ln in f if "libamdhip64.so" in ln})
+        self.hip = h = ctypes.CDLL(paths[0])  # already mapped: the same runtime, no second copy
+        vp = ctypes.c_void_p
+        h.hipEventCreateWithFlags.argtypes = [ctypes.POINTER(vp), ctypes.c_uint]
+        h.hipEventRecord.argtypes = [vp, vp]
+        h.hipEventElapsedTime.argtypes = [ctypes.POINTER(ctypes.c_float), vp, vp]
+        h.hipEventDestroy.argtypes = [vp]
+        self.ev = []
+        for _ in range(k):
+            e = vp()
+            if h.hipEventCreateWithFlags(ctypes.byref(e), self.DISABLE_SYSTEM_FENCE) != 0:
+                raise RuntimeError("hipEventCreateWithFlags(hipEventDisableSystemFence) failed")
+            self.ev.append(e)
+
+    def record(self, i, stream):
+        import ctypes
+        if self.hip.hipEventRecord(self.ev[i], ctypes.c_void_p(stream.cuda_stream)) != 0:
+            raise RuntimeError("hipEventRecord failed")
+
+    def elapsed_ms(self, i, j):
+        import ctypes
+        t = ctypes.c_float()
+        if self.hip.hipEventElapsedTime(ctypes.byref(t), self.ev[i], self.ev[j]) != 0:
+            raise RuntimeError("hipEventElapsedTime failed")
+        return t.value
+
+    def close(self):
+        for e in self.ev:
+            self.hip.hipEventDestroy(e)
+        self.ev = []
+
+
 def shard_range(n_total, world, rank):
     """contiguous chunkset-index shard of rank"""
     per = -(-n_total // world)
@@ -597,6 +639,19 @@ def main():
                 sms = b0.elapsed_time(b1) / (4 * reps)
                 rec["stream"] = {"launches": 4 * reps, "encode_ms": round(sms, 4),
                                  "frac": round(ns * (CS + N * F) / (sms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+                # and the same single launches between timing events that skip the system-scope fence
+                # (hipEventDisableSystemFence): `frac` above keeps torch's default events, as in every
+                # round before; the difference is the events' own L2 writeback + invalidate
+                fe = FenceFreeEvents(2 * reps)
+                for r in range(reps):
+                    fe.record(2 * r, stream)
+                    codec.encode_batch(ctx, big, ns, cbig, obig, bpitch, stream=stream)
+                    fe.record(2 * r + 1, stream)
+                stream.synchronize()
+                fms = float(np.median([fe.elapsed_ms(2 * r, 2 * r + 1) for r in range(reps)]))
+                fe.close()
+                rec["no_system_fence"] = {"launches": reps, "encode_ms": round(fms, 4),
+                                          "frac": round(ns * (CS + N * F) / (fms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
             sweep.append(rec)
         del big, cbig, obig
 

@@ -29,11 +29,13 @@ def test_tool_microbenchmarks_compile():
 
 
 def test_study_builds_of_the_kernels_compile():
-    # the timing-study forms DESIGN.md §8 cites (per-workgroup phase trace, no edge pass) stay buildable
+    # the timing-study forms DESIGN.md §8 cites (per-workgroup phase trace, no edge pass, the pattern
+    # ceiling, the aligned-piece layouts) stay buildable
     if not os.path.exists(HIPCC) and not shutil.which("hipcc"):
         pytest.skip("hipcc not in this image")
     src = os.path.join(ROOT, "decds_amd", "csrc", "rlnc_kernels.hip")
-    for defs in (["-DDECDS_PHASE_TRACE=1"], ["-DDECDS_PHASE_TRACE=1", "-DDECDS_STUDY_NO_EDGE=1"]):
+    for defs in (["-DDECDS_PHASE_TRACE=1"], ["-DDECDS_PHASE_TRACE=1", "-DDECDS_STUDY_NO_EDGE=1"],
+                 ["-DDECDS_STUDY_PATTERN=1"], ["-DDECDS_STUDY_ALIGNED_PIECES=1"], ["-DDECDS_STUDY_ALIGNED_PIECES=3"]):
         r = subprocess.run([HIPCC, "--offload-arch=gfx950", "-std=c++17", "-I" + os.path.join(ROOT, "include"),
                             "-fsyntax-only"] + defs + [src], capture_output=True, text=True, timeout=300)
         assert r.returncode == 0, (defs, r.stderr[-1500:])
