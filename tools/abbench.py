@@ -74,10 +74,14 @@ def main():
     torch.cuda.synchronize()
     sp = vp(st.cuda_stream)
 
+    # every knob any build sets, per library handle: a build that does not set one must run at its default
+    # (knobs are process-wide per loaded library, and two specs of one .so share that library)
+    knob_names = sorted({b["knob"][0] for b in builds if b["knob"]})
+
     def run(b, ev=None, encode=True):
         L, h, p = b["lib"], b["ctx"], b["pitch"]
-        if b["knob"]:
-            L.decds_tuning(b["knob"][0], b["knob"][1], 1)
+        for name in knob_names:
+            L.decds_tuning(name, b["knob"][1] if b["knob"] and b["knob"][0] == name else (1 << 64) - 1, 1)
         coded = coded0[b["off"]:]
         if ev:
             ev[0].record(st)
