@@ -172,3 +172,26 @@ def test_bench_one_rank_rccl_group_runs_the_distributed_path():
     assert d["scaling_point"] is True and len(d["per_rank"]) == 1
     x = d["per_rank"][0]
     assert x["chunksets"] == [0, 103] and x["repaired_checked"] == x["ready_chunksets"] >= 100
+
+
+@pytest.mark.gpu
+def test_bench_encode_batch_sweep_fields():
+    # the encode batch sweep (north_star "at batch >= 256"): one record per size, kernel and
+    # fraction of 8 TB/s; small sizes also as a stream of launches and between timing events that skip the
+    # system-scope fence (bench.FenceFreeEvents) — those can only be faster than torch's fencing events
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--config", "cfg2", "--steps", "1", "--warmup", "1",
+                        "--settle-s", "0", "--no-cpu-baseline", "--no-commit", "--no-extras"], capture_output=True,
+                       text=True, timeout=200, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    sw = d["encode_batch_sweep"]
+    assert [x["chunksets"] for x in sw] == [1, 16, 64, 256, 1024, 1639]
+    for x in sw:
+        assert x["kernel"].startswith("rlnc_encode") and 0 < x["frac"] < 1
+        if x["chunksets"] <= 64:
+            nf = x["no_system_fence"]
+            assert nf["launches"] >= 10 and 0 < nf["frac"] < 1
+            assert nf["encode_ms"] <= x["encode_ms"] * 1.05, (x["chunksets"], nf, x["encode_ms"])
+        else:
+            assert "no_system_fence" not in x
+    assert min(x["frac"] for x in sw if x["chunksets"] >= 256) > 0.6  # north_star: >= 0.70 (measured 0.73-0.76)
