@@ -1528,7 +1528,7 @@ hipError_t configure_kernels() {
 }
 
 #ifndef DECDS_DEC_SWEEP_MIN_N
-#define DECDS_DEC_SWEEP_MIN_N 256
+#define DECDS_DEC_SWEEP_MIN_N 1536
 #endif
 #ifndef DECDS_ENC_SMALL_MAX_N
 #define DECDS_ENC_SMALL_MAX_N 2
@@ -1624,9 +1624,10 @@ hipError_t launch_encode(const LaunchGeom &geom, const uint8_t *src, size_t n, c
 }
 
 // The decode's two forms: batches of DECDS_DEC_SWEEP_MIN_N chunksets or more run the
-// persistent sweep (-1.5...-3.3 % decode time at 256-1639 chunksets, r05p-r05s), smaller ones one-tile
-// workgroups (the sweep measured 1.5-2.6 % slower at 103, r05p/r05q). The environment variable of that
-// name overrides the threshold per launch (tests force either form at any size).
+// persistent sweep, smaller ones one-tile workgroups. Round 3 measured the sweep -1.5...-3.3 % from 256
+// chunksets on (r05p-r05s); on round 5's kernels the one-tile form is 1-2 % faster at 256-512 and even to
+// 1280, the sweep 0.4-0.9 % faster at 1639 (r08w / r08za / r08zb), hence 1536. The environment variable of
+// that name overrides the threshold per launch (tests force either form at any size).
 const char *decode_kernel_name(size_t n) { return decode_sweeps(n) ? "rlnc_decode_sweep_kernel" : "rlnc_decode_kernel"; }
 
 const char *encode_kernel_name(size_t) { return "rlnc_encode_sweep_kernel"; }

@@ -93,7 +93,7 @@ def test_layout_constants():
 
 
 def test_decode_kernel_by_batch_size():
-    # launch_decode (rlnc_kernels.hip decode_sweeps): the persistent sweep from 256 chunksets on,
+    # launch_decode (rlnc_kernels.hip decode_sweeps): the persistent sweep from 1536 chunksets on,
     # one-tile workgroups below; decds_tuning moves the threshold for the process (UINT64_MAX = back
     # to the start value); the environment variable of the same name sets that start value, read once
     import subprocess
@@ -104,9 +104,9 @@ def test_decode_kernel_by_batch_size():
     reset = (1 << 64) - 1
     try:
         if "DECDS_DEC_SWEEP_MIN_N" not in os.environ:
-            assert tune("DECDS_DEC_SWEEP_MIN_N", reset) == 256
-            assert name(1) == name(255) == "rlnc_decode_kernel"
-            assert name(256) == name(1639) == "rlnc_decode_sweep_kernel"
+            assert tune("DECDS_DEC_SWEEP_MIN_N", reset) == 1536
+            assert name(1) == name(255) == name(1535) == "rlnc_decode_kernel"
+            assert name(1536) == name(1639) == "rlnc_decode_sweep_kernel"
         assert tune("DEC_SWEEP_MIN_N", 1) == 1 and name(1) == "rlnc_decode_sweep_kernel"  # prefix optional
         tune("DECDS_DEC_SWEEP_MIN_N", 1 << 40)
         assert name(1639) == "rlnc_decode_kernel"

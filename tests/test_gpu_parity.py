@@ -417,6 +417,15 @@ def test_decoded_data_cut_at_last_marker_matches_oracle(ctx):
 
 @pytest.mark.parametrize("n", [1, 256])
 def test_no_marker_anywhere_worst_case_cost(ctx, n):
+    from decds_amd._capi import lib
+    lib().decds_tuning(b"DECDS_DEC_SWEEP_MIN_N", 256, 1)  # n = 256: the sweep (its default threshold is higher)
+    try:
+        _no_marker_worst_case(ctx, n)
+    finally:
+        lib().decds_tuning(b"DECDS_DEC_SWEEP_MIN_N", (1 << 64) - 1, 1)
+
+
+def _no_marker_worst_case(ctx, n):
     """a chunkset whose decoded data holds no boundary marker at all (only rows accepted
     unvalidated get there) is decoded once more in full by its edge workgroup (tail_scan_decoded) before
     it is ChunksetRepairingFailed. Its cost, at n = 1 (one-tile decode) and inside a 256-chunkset batch
