@@ -34,6 +34,9 @@ def main():
     sp = vp(st.cuda_stream)
     builds = []
     for path in a.libs:
+        if path == "default":  # the in-tree library, as in tools/abbench.py
+            from decds_amd import build as _build
+            path = _build.LIB
         L = ctypes.CDLL(os.path.abspath(path), mode=ctypes.RTLD_LOCAL)
         _declare(L)
         h = ctypes.c_void_p()
