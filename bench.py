@@ -115,6 +115,9 @@ def parse(argv=None):
     p.add_argument("--spot-out", default=None, metavar="PATH.npz",
                    help="after the timed region, save the source bytes, coding vectors and coded rows of the "
                         "shard's first, middle and last chunkset (the GPU tests check them against the oracle)")
+    p.add_argument("--digest-out", default=None, metavar="PATH.npy",
+                   help="after the timed region, save the chunk digest (chunk.rs:40-46, decds_commit_batch) of every "
+                        "coded row of the shard: the GPU tests compare all of them with the oracle's rows' digests")
     p.add_argument("--packed", action="store_true",
                    help="coded rows packed at pitch 1,048,587 instead of the recommended 128-B-aligned layout")
     return p.parse_args(argv)
@@ -541,6 +544,16 @@ def main():
                  coeffs=np.stack([coeffs_h[c * N * K:(c + 1) * N * K] for c in spots]),
                  coded=np.stack([rows[c * N:(c + 1) * N].cpu().numpy() for c in spots]),
                  shard_bytes=np.int64(blob_len_rank), pitch=np.int64(pitch))
+
+    if args.digest_out:
+        with torch.cuda.stream(stream):
+            ddig = torch.empty(n * N * 32, dtype=torch.uint8, device=dev)
+            droots = torch.empty(n * 32, dtype=torch.uint8, device=dev)
+            dproofs = torch.empty(n * N * 128, dtype=torch.uint8, device=dev)
+        codec.commit_batch(ctx, coded, n, ddig, droots, dproofs, first_chunkset_id=lo, pitch=pitch, stream=stream)
+        stream.synchronize()
+        np.save(args.digest_out, ddig.cpu().numpy().reshape(n * N, 32))
+        del ddig, droots, dproofs
 
     # the next row, timed beside the headline step, never inside it: ChunkSet::new's
     # commitment (BLAKE3 of every coded row + 16-leaf Merkle trees/proofs) over the same coded rows

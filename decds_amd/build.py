@@ -38,7 +38,7 @@ def build(force=False, verbose=True, defines=(), out=None, mllvm=()):
     lib = out or LIB
     if not force and out is None and not _stale():
         return LIB
-    tag = "_".join([d.replace("=", "") for d in defines] + [m.strip("-").replace("=", "") for m in mllvm]) or "default"
+    tag = "_".join([d.replace("=", "_") for d in defines] + [m.strip("-").replace("=", "") for m in mllvm]) or "default"
     objdir = os.path.join(HERE, "..", "build", "obj", tag)
     os.makedirs(objdir, exist_ok=True)
     objs, procs = [], []
@@ -70,7 +70,11 @@ def build_pattern(force=False, verbose=True):
     if not force and not _stale(PATTERN_LIB):
         return PATTERN_LIB
     os.makedirs(os.path.dirname(PATTERN_LIB), exist_ok=True)
-    return build(force=True, verbose=verbose, defines=["DECDS_STUDY_PATTERN=1"], out=PATTERN_LIB)
+    # decds=decds_pattern: every C++ symbol of this build, kernels included, lives in namespace
+    # decds_pattern (the token `decds` appears in the sources only as that namespace's name), so a
+    # rocprof trace of a process that loads both libraries lists the pattern launches under their own
+    # names (_ZN13decds_pattern...) and never merges them into the product kernels' statistics
+    return build(force=True, verbose=verbose, defines=["DECDS_STUDY_PATTERN=1", "decds=decds_pattern"], out=PATTERN_LIB)
 
 
 if __name__ == "__main__":

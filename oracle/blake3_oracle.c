@@ -199,6 +199,16 @@ void orc_chunk_digest(uint64_t chunkset_id, uint64_t chunk_id, const uint8_t *da
     free(buf);
 }
 
+/* chunk.rs:40-46 over n_rows coded rows at `pitch` bytes apart, each ORC_F bytes long: row r is chunk
+ * first_row + r of chunkset (first_row + r) / 16 (chunkset.rs:47: chunk id = chunkset_id * 16 + i).
+ * One thread; tests/fullcheck.py runs batches of rows on a thread pool. */
+void orc_chunk_digest_rows(const uint8_t *rows, size_t n_rows, size_t pitch, uint64_t first_row, uint8_t *out) {
+    for (size_t r = 0; r < n_rows; r++) {
+        const uint64_t id = first_row + r;
+        orc_chunk_digest(id / ORC_N, id, rows + r * pitch, ORC_F, out + 32 * r);
+    }
+}
+
 /* merkle_tree.rs:158-160 */
 static void parent_hash(const uint8_t *l, const uint8_t *r, uint8_t out[32]) {
     uint8_t b[64];

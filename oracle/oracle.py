@@ -65,6 +65,7 @@ def lib():
             ("orc_fast_blob_repair", c.c_int, [vp, sz, vp, sz, vp, vp, u32, u8, c.c_int]),
             ("orc_blake3", None, [vp, sz, vp]),
             ("orc_chunk_digest", None, [u64, u64, vp, sz, vp]),
+            ("orc_chunk_digest_rows", None, [vp, sz, sz, u64, vp]),
             ("orc_merkle", c.c_int, [vp, sz, vp, vp]),
             ("orc_merkle_verify", c.c_int, [sz, vp, vp, sz, vp]),
         ]:
@@ -239,6 +240,16 @@ def chunk_digest(chunkset_id, chunk_id, data):
     out = np.empty(32, np.uint8)
     lib().orc_chunk_digest(chunkset_id, chunk_id, _p(data), data.size, _p(out))
     return out.tobytes()
+
+
+def chunk_digest_rows(rows, first_row):
+    """chunk.rs:40-46 for every row of a (m, F) array of coded rows, rows first_row .. first_row + m - 1
+    of the blob (chunk id = chunkset_id * 16 + i, chunkset.rs:47) -> (m, 32) digests"""
+    rows = np.ascontiguousarray(rows, dtype=np.uint8)
+    m = rows.shape[0]
+    out = np.empty((m, 32), np.uint8)
+    lib().orc_chunk_digest_rows(_p(rows), m, rows.shape[1] if rows.ndim == 2 else F, first_row, _p(out))
+    return out
 
 
 def merkle(leaves):

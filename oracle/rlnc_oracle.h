@@ -99,6 +99,7 @@ int orc_matrix_inverse(const uint8_t *m, uint8_t *inv, size_t k, uint32_t poly);
 /* commitment layer (blake3_oracle.c): BLAKE3, Chunk::digest, MerkleTree root/proofs/verify */
 void orc_blake3(const uint8_t *in, size_t len, uint8_t out[32]);
 void orc_chunk_digest(uint64_t chunkset_id, uint64_t chunk_id, const uint8_t *data, size_t len, uint8_t out[32]);
+void orc_chunk_digest_rows(const uint8_t *rows, size_t n_rows, size_t pitch, uint64_t first_row, uint8_t *out);
 int orc_merkle(const uint8_t *leaves, size_t n, uint8_t root[32], uint8_t *proofs);
 int orc_merkle_verify(size_t leaf_index, const uint8_t leaf[32], const uint8_t *proof, size_t plen,
                       const uint8_t root[32]);

@@ -84,21 +84,25 @@ def test_cfg5_shards_tile_the_blob():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("rank", range(8))
-def test_bench_cfg5_shard_rehearsal_spot_checked(tmp_path, rank):
+def test_bench_cfg5_shard_rehearsal_all_rows_checked(tmp_path, rank):
     # All of config 5 on one GPU, one shard per test: rank R of the 128 GiB blob over 8 GPUs
     # (bench.py --rehearse-shard R/8, the process each of the driver's eight ranks runs), at full size.
     # Rank 7 = chunksets [11473, 13108), the last holding 2 MiB of data (blob.rs:252-254 zero-pads
     # it). bench.py repairs every chunkset of the shard and compares it with its source itself; here
-    # the shard's range, and its first, middle and last chunkset's source bytes (against the global
-    # synthetic blob at the shard's offset) and coded rows (payload-aligned layout, against the oracle).
+    # the shard's range, its first, middle and last chunkset's source bytes (against the global synthetic
+    # blob at the shard's offset) and coded rows (payload-aligned layout, against the oracle), and the
+    # chunk digests of ALL its ~26,200 coded rows (bench.py --digest-out, decds_commit_batch on the
+    # device) against the digests of the oracle's rows for the same global chunksets (tests/fullcheck.py).
     import numpy as np
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as o
     lo, hi = cfg5_shard(rank)
     spot = str(tmp_path / "spot.npz")
+    digs = str(tmp_path / "digests.npy")
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--config", "cfg3", "--rehearse-shard",
                         "%d/8" % rank, "--steps", "1", "--warmup", "1", "--settle-s", "0", "--no-cpu-baseline",
-                        "--no-commit", "--no-extras", "--spot-out", spot], capture_output=True, text=True, timeout=110,
+                        "--no-commit", "--no-extras", "--spot-out", spot, "--digest-out", digs], capture_output=True,
+                       text=True, timeout=110,
                        cwd=ROOT)
     assert r.returncode == 0, r.stderr[-2000:]
     d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
@@ -120,6 +124,13 @@ def test_bench_cfg5_shard_rehearsal_spot_checked(tmp_path, rank):
         assert np.array_equal(z["coeffs"][k], o.fill_random(0xC0EF0002, o.N * o.K, c * o.N * o.K)), c
         ref = o.chunkset_encode(expect, z["coeffs"][k], nthreads=8)
         assert np.array_equal(z["coded"][k], ref), c
+    # every coded row of the shard: device digests against the oracle rows' digests
+    from fullcheck import shard_oracle_digests
+    dev = np.load(digs)
+    assert dev.shape == ((hi - lo) * o.N, 32)
+    ref = shard_oracle_digests(lo, hi, 0xDEC05002, 0xC0EF0002, 128 << 30)
+    bad = np.nonzero((dev != ref).any(axis=1))[0]
+    assert bad.size == 0, "rows differ from the oracle's: chunksets %s" % sorted({lo + int(r) // o.N for r in bad[:64]})
 
 
 @pytest.mark.gpu

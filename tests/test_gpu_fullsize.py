@@ -1,7 +1,8 @@
 """BASELINE config 3/4 at full size on one GPU: a 16 GiB blob (1639 chunksets, the last one holding
 4 MiB of data) encoded in one batch, repaired from exactly 10 random survivors per chunkset, and
-committed (separately and fused into the encode) + validated (rows f1, f2). Spot chunksets / rows are bit-exact against the oracle; every
-other check is a size-independent property (decode∘encode = id, rank-deficient sets reported
+committed (separately and fused into the encode) + validated (rows f1, f2). Every coded row of the
+1639-chunkset launches is compared byte for byte with the oracle's (tests/fullcheck.py); the other
+checks are size-independent properties (decode∘encode = id, rank-deficient sets reported
 not-ready exactly where the oracle's rank test says so, every row's proof verifies, a flipped byte
 does not)."""
 import numpy as np
@@ -12,6 +13,7 @@ torch = pytest.importorskip("torch")
 from decds_amd import codec  # noqa: E402
 from decds_amd._capi import CHUNKSET_BYTES as CS, CODED_PIECE_BYTES as F, K, N  # noqa: E402
 import oracle as o  # noqa: E402
+from fullcheck import compare_device_rows  # noqa: E402
 
 pytestmark = pytest.mark.gpu
 
@@ -36,9 +38,12 @@ def test_cfg3_16gib_encode_repair_commit_validate(ctx):
     coded = torch.empty(n * N * F, dtype=torch.uint8, device="cuda")
     codec.encode_batch(ctx, src, n, torch.from_numpy(coeffs).cuda(), coded)
     torch.cuda.synchronize()
-    for c in (0, 820, n - 1):
-        ref = o.chunkset_encode(src[c * CS:(c + 1) * CS].cpu().numpy(), coeffs[c * 160:(c + 1) * 160], nthreads=8)
-        assert np.array_equal(coded[c * N * F:(c + 1) * N * F].cpu().numpy().reshape(N, F), ref), c
+    # every one of the 26,224 coded rows (packed layout) against the oracle's, byte for byte
+    assert compare_device_rows(coded.view(n * N, F), 0, n, 0xDEC05003, 0xC0EF0003, blob_len) == n * N
+    # and one chunkset through the oracle's scalar chunkset path on the device's own source bytes
+    c = 820
+    ref = o.chunkset_encode(src[c * CS:(c + 1) * CS].cpu().numpy(), coeffs[c * 160:(c + 1) * 160], nthreads=8)
+    assert np.array_equal(coded[c * N * F:(c + 1) * N * F].cpu().numpy().reshape(N, F), ref), c
 
     # repair from exactly 10 random survivors per chunkset (cfg4)
     rng = np.random.default_rng(0x5EED0003)
@@ -112,8 +117,8 @@ def test_cfg3_16gib_encode_repair_commit_validate(ctx):
 
 def test_payload_aligned_layout_at_the_bench_batches(ctx):
     # the layout bench.py and the encode sweep time (pitch 1,048,704, payloads 128-byte aligned) at the
-    # north-star batches: launches of 256 and of all 1639 chunksets of a 16 GiB blob, first / middle /
-    # last chunkset of each bit-exact against the oracle; then every chunkset of the 1639 repaired
+    # north-star batches: launches of 256 (first / middle / last chunkset) and of all 1639 chunksets
+    # (every coded row) of a 16 GiB blob bit-exact against the oracle; then every chunkset of the 1639 repaired
     # from 10 survivors equals its source
     blob_len = 16 << 30
     n = -(-blob_len // CS)
@@ -128,9 +133,12 @@ def test_payload_aligned_layout_at_the_bench_batches(ctx):
         coded.fill_(0xA5)
         codec.encode_batch(ctx, src, nb, dco, coded, pitch)
         torch.cuda.synchronize()
-        for c in sorted({0, nb // 2, nb - 1}):
-            ref = o.chunkset_encode(src[c * CS:(c + 1) * CS].cpu().numpy(), coeffs[c * 160:(c + 1) * 160], nthreads=8)
-            assert np.array_equal(rows[c * N:(c + 1) * N].cpu().numpy(), ref), (nb, c)
+        if nb == n:  # the whole launch: every coded row against the oracle's
+            assert compare_device_rows(rows, 0, n, 0xDEC05004, 0xC0EF0004, blob_len) == n * N
+        else:
+            for c in sorted({0, nb // 2, nb - 1}):
+                ref = o.chunkset_encode(src[c * CS:(c + 1) * CS].cpu().numpy(), coeffs[c * 160:(c + 1) * 160], nthreads=8)
+                assert np.array_equal(rows[c * N:(c + 1) * N].cpu().numpy(), ref), (nb, c)
         if nb < n:  # nothing past the batch was written
             assert int(rows[nb * N].cpu()[0]) == 0xA5 and int(rows[n * N - 1].cpu()[-1]) == 0xA5
     rng = np.random.default_rng(0x5EED0004)

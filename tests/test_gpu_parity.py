@@ -24,7 +24,8 @@ def sha(a):
 
 
 def dev(a):
-    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    # a writable copy: torch.from_numpy warns on read-only arrays (np.frombuffer over bytes, golden fixtures)
+    return torch.from_numpy(np.array(a, copy=True)).cuda()
 
 
 def host(t):

@@ -229,3 +229,23 @@ def test_table_kernels_guard_their_lds_base(tmp_path, which):
     for name, ins in table.items():
         assert any(x.startswith("s_trap 2") for _, x in ins), name
         assert any(re.match(r"s_cmp_(eq|lg)_u32 0, 0$", x) for _, x in ins[:8]), (name, ins[:8])
+
+
+def test_pattern_build_symbols_are_disjoint_from_the_product(tmp_path):
+    # bench.py loads tools/bin/libdecds_pattern.so (wrong bytes by design) into the same process as the
+    # product: its kernels must carry names of their own (namespace decds_pattern, decds_amd/build.py
+    # build_pattern), so no profile can merge their launches into the product kernels' statistics
+    if not os.path.exists(OBJDUMP):
+        pytest.skip("llvm-objdump not in this image")
+    (tmp_path / "p").mkdir()
+    (tmp_path / "q").mkdir()
+    prod, pat = set(_kernel_notes(tmp_path / "p", "product")), set(_kernel_notes(tmp_path / "q", "pattern"))
+    assert len(prod) >= 10 and len(pat) >= 10, (len(prod), len(pat))
+    assert not prod & pat, sorted(prod & pat)[:5]
+    assert all(k.startswith("_ZN5decds") for k in prod), [k for k in prod if not k.startswith("_ZN5decds")][:5]
+    assert all(k.startswith("_ZN13decds_pattern") for k in pat), [k for k in pat if not k.startswith("_ZN13decds_pattern")][:5]
+    # the host-side launch stubs too
+    nm = lambda lib: {ln.split()[-1] for ln in subprocess.run(["nm", lib], capture_output=True, text=True, check=True)
+                      .stdout.splitlines() if "_kernel" in ln and ln.split()[-1].startswith("_ZN")}
+    hp, hq = nm(_lib("product")), nm(_lib("pattern"))
+    assert hp and hq and not hp & hq
