@@ -43,6 +43,15 @@ class FenceFreeEvents:
         import ctypes
         with open("/proc/self/maps") as f:
             paths = sorted({ln.split()[-1] for ln in f if "libamdhip64.so" in ln})
+        # the runtime that owns torch's streams: the one under torch's own lib directory when torch
+        # bundles one, else the only one mapped (two runtimes and neither torch's: refuse)
+        import torch
+        tlib = os.path.realpath(os.path.join(os.path.dirname(torch.__file__), "lib"))
+        own = [p for p in paths if os.path.realpath(os.path.dirname(p)) == tlib]
+        if own:
+            paths = own
+        if len(paths) != 1:
+            raise RuntimeError("FenceFreeEvents: expected one HIP runtime mapped, found %s" % paths)
         self.hip = h = ctypes.CDLL(paths[0])  # already mapped: the same runtime, no second copy
         vp = ctypes.c_void_p
         h.hipEventCreateWithFlags.argtypes = [ctypes.POINTER(vp), ctypes.c_uint]
@@ -108,6 +117,8 @@ def parse(argv=None):
     p.add_argument("--cpu-sample", type=int, default=0, help="chunksets in the CPU sample (0 = auto)")
     p.add_argument("--no-extras", action="store_true",
                    help="skip the pattern ceilings and the end-to-end (PCIe-inclusive) host-path rate")
+    p.add_argument("--no-api-shapes", action="store_true",
+                   help="skip the reference's build_blob / repair_blob shapes through the blob API (1 MiB .. 4 GiB)")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
     p.add_argument("--rehearse-shard", default=None, metavar="R/W", type=shard_arg,
                    help="one process, no process group: run only rank R's shard of a W-GPU job on this GPU "
@@ -275,6 +286,39 @@ def cpu_baseline(n_sample, seed, repeats=5, cfg2_chunksets=103):
                                      for _ in range(max(1, repeats))])), cores=1,
                          sample="1 chunkset (config 1), 1 thread")
     del smp1
+    # the reference's bench shapes (build_blob.rs / repair_blob.rs, API_SIZES) on the same codec and the
+    # headline's thread count: encode of the whole blob (Blob::new's RLNC part) and repair of every
+    # chunkset from the first 10 useful of shares 0..11 in a shuffled order (RepairingBlob's add_chunk
+    # rank step + decode). RLNC only: the restatement carries no SIMD BLAKE3, so the commitment and the
+    # chunk validation the GPU figures (api_shapes) include are not in these.
+    th = head["cores"]
+    api = []
+    for size in API_SIZES:
+        n = -(-size // o.CS)
+        blob = o.fill_random(0xA91 + size.bit_length(), size)
+        coeffs = o.fill_random(0xC0EF0A91, n * o.N * o.K)
+        rng = np.random.default_rng(0x5EED + size.bit_length())
+        cand = np.full((n, o.N), 0xFF, np.uint8)
+        for c in range(n):
+            cand[c, :12] = rng.permutation(12)
+        t_enc, t_rep, reps = 0.0, 0.0, 0
+        while reps < 3 or t_enc + t_rep < 0.5:
+            t0 = time.perf_counter()
+            coded = o.fast_blob_encode(blob, coeffs, nthreads=th)
+            t1 = time.perf_counter()
+            out, status = o.fast_blob_repair(coded, cand, size, nthreads=th)
+            t2 = time.perf_counter()
+            if reps == 0:
+                assert (status == 0).all() and np.array_equal(out, blob), "CPU repair of the api shape differs"
+            del coded, out
+            t_enc, t_rep, reps = t_enc + t1 - t0, t_rep + t2 - t1, reps + 1
+        api.append({"blob_bytes": size, "chunksets": n, "encode_ms": round(t_enc / reps * 1e3, 3),
+                    "repair_ms": round(t_rep / reps * 1e3, 3), "encode_GiBps": round(reps * size / GIB / t_enc, 2),
+                    "repair_GiBps": round(reps * size / GIB / t_rep, 2), "passes": reps})
+        del blob
+    extra["api_shapes"] = {"cores": th, "what": "GFNI restatement, RLNC encode / repair only (no commitment, no "
+                                                "validation), the reference's build_blob / repair_blob sizes",
+                           "sizes": api}
     return dict({"value": head["value"], "unit": "GiB/s", "cores": head["cores"], "kind": "port",
                  "variant": head_name, "headline": best, "median_of": head["runs"], "passes": head["passes"],
                  "spread": head["spread"], "sample": head["sample"],
@@ -381,6 +425,117 @@ def end_to_end(ctx, chunksets=103, repeats=5, batch=16):
     for hb in (hb_blob, hb_coded, hb_out):
         hb.free()
     return res
+
+
+API_SIZES = (1 << 20, 1 << 24, 1 << 28, 1 << 30, 1 << 32)  # decds-lib/benches/build_blob.rs:38-44, repair_blob.rs:35-41
+
+
+def api_shapes(ctx, sizes=API_SIZES, repeats=5, repair_repeats=3):
+    """The reference's own benchmarks through the reference-facing C-ABI, at their five blob sizes
+    (1 MiB .. 4 GiB), on one GPU, host memory in and out:
+
+    * build_blob (decds-lib/benches/build_blob.rs:47-55): Blob::new(Vec<u8>) = decds_blob_new on a
+      plain (pageable) random blob — whole-blob BLAKE3, encode + commitment of every chunkset, the
+      blob-level tree, coded chunks in host memory. `cold_ms`: the first call at that size (the
+      coded store is page-locked then; later calls reuse it from the library's block cache);
+      `warm_ms`: the median of `repeats` further calls.
+    * repair_blob (decds-lib/benches/repair_blob.rs:47-65): the header and shares 0..11 of a Blob,
+      their chunks shuffled (seeded), then RepairingBlob::new + add_chunk of every chunk in that order
+      (each validated: chunk digest + both proofs; chunks of a chunkset already at rank 10 are refused
+      ChunksetReadyToRepair, which the reference ignores) — and, beyond the reference's timed region
+      (its add_chunk already decodes), get_repaired_chunkset of every chunkset, each compared with the
+      blob after the timing. `add_chunk_ms` / `get_ms` split the median run; `batched` times the same
+      arrivals through decds_repairing_blob_add_chunks (validation as device batches).
+    Python calls the C-ABI through ctypes with pointers into numpy arrays (no per-chunk copies)."""
+    import ctypes
+    import numpy as np
+    from decds_amd import codec
+    from decds_amd._capi import CHUNKSET_BYTES as CS, CODED_PIECE_BYTES as F, N, check, lib
+    from decds_amd.blob import Blob, RepairingBlob
+    L = lib()
+    vp = ctypes.c_void_p
+    ptr = lambda a: vp(a.ctypes.data)
+    rows = []
+    for size in sizes:
+        n = -(-size // CS)
+        data = codec.fill_random_host(0xA91 + size.bit_length(), size)
+        t0 = time.perf_counter()
+        blob = Blob(ctx, data)
+        cold = time.perf_counter() - t0
+        warm = []
+        for _ in range(repeats):
+            blob.free()
+            t0 = time.perf_counter()
+            blob = Blob(ctx, data)
+            warm.append(time.perf_counter() - t0)
+        header = blob.get_blob_header()
+        plen = blob.proof_len()
+        shares, proofs = np.empty((12, n, F), np.uint8), np.empty((12, n, plen * 32), np.uint8)
+        for sh in range(12):  # DECDS_NUM_ERASURE_CODED_SHARES - 4 (repair_blob.rs:51)
+            check(L.decds_blob_get_share(blob._h, sh, ptr(shares[sh]), shares[sh].nbytes, ptr(proofs[sh]), proofs[sh].nbytes))
+        blob.free()
+        del blob
+        arrivals = [(sh, c) for sh in range(12) for c in range(n)]
+        np.random.default_rng(0x5EED + size.bit_length()).shuffle(arrivals)
+        out = np.empty(size, np.uint8)
+
+        def repair_seq():
+            t0 = time.perf_counter()
+            rb = RepairingBlob(ctx, header)
+            h = rb._h
+            for sh, c in arrivals:
+                st = L.decds_repairing_blob_add_chunk(h, c, c * N + sh, ptr(shares[sh, c]), F, ptr(proofs[sh, c]), plen)
+                if st not in (0, 3, 4):  # ok, ChunksetReadyToRepair, ChunkDecodingFailed (repair_blob.rs:62 ignores them)
+                    check(st)
+            t1 = time.perf_counter()
+            ok = 0
+            for c in range(n):
+                if rb.is_chunkset_ready_to_repair(c):
+                    rb.get_repaired_chunkset(c, out=out[c * CS:min(size, (c + 1) * CS)])
+                    ok += 1
+            t2 = time.perf_counter()
+            rb.free()
+            return t1 - t0, t2 - t1, ok
+
+        rows_a = np.ascontiguousarray(shares[[a[0] for a in arrivals], [a[1] for a in arrivals]])
+        ids = np.array([(c, c * N + sh) for sh, c in arrivals], np.uint64)
+        prf_a = np.ascontiguousarray(proofs[[a[0] for a in arrivals], [a[1] for a in arrivals]])
+
+        def repair_batched():
+            t0 = time.perf_counter()
+            rb = RepairingBlob(ctx, header)
+            st = rb.add_rows(rows_a, ids, prf_a, plen)
+            assert set(np.unique(st).tolist()) <= {0, 3, 4}, np.unique(st)
+            t1 = time.perf_counter()
+            ok = 0
+            for c in range(n):
+                if rb.is_chunkset_ready_to_repair(c):
+                    rb.get_repaired_chunkset(c, out=out[c * CS:min(size, (c + 1) * CS)])
+                    ok += 1
+            t2 = time.perf_counter()
+            rb.free()
+            return t1 - t0, t2 - t1, ok
+
+        rec = {"blob_bytes": size, "chunksets": n,
+               "blob_new": {"cold_ms": round(cold * 1e3, 3), "warm_ms": round(float(np.median(warm)) * 1e3, 3),
+                            "warm_spread_ms": [round(min(warm) * 1e3, 3), round(max(warm) * 1e3, 3)],
+                            "warm_GiBps": round(size / GIB / float(np.median(warm)), 2), "calls": repeats}}
+        for key, fn in (("repair", repair_seq), ("repair_batched", repair_batched)):
+            runs = []
+            for _ in range(repair_repeats):
+                out[:] = 0
+                runs.append(fn())
+                assert runs[-1][2] == n, "not every chunkset was ready after shares 0..11"
+                assert np.array_equal(out, data), "repaired blob differs (%s, %d bytes)" % (key, size)
+            tot = sorted(runs, key=lambda r: r[0] + r[1])[len(runs) // 2]
+            rec[key] = {"ms": round((tot[0] + tot[1]) * 1e3, 3), "add_chunk_ms": round(tot[0] * 1e3, 3),
+                        "get_ms": round(tot[1] * 1e3, 3), "GiBps": round(size / GIB / (tot[0] + tot[1]), 2),
+                        "chunks_added": len(arrivals), "runs": repair_repeats}
+        rows.append(rec)
+        del shares, proofs, rows_a, prf_a, out, data
+    return {"what": "the reference's build_blob / repair_blob benches through decds_blob_new / decds_repairing_blob_*",
+            "memory": "pageable numpy blob in, the library's own coded store; host-memory end to end (PCIe-inclusive)",
+            "sizes": rows}
 
 
 def init_group(dist, backend, device, rank, world, timeout_s=300):
@@ -600,10 +755,12 @@ def main():
 
     # the kernels' own access-pattern ceilings (decode first: it needs the intact coded rows), then the
     # end-to-end host-memory rate (north_star: written in DESIGN.md §7) — both after the timed region
-    patterns, e2e = None, None
+    patterns, e2e, shapes = None, None, None
     if world == 1 and not args.no_extras:
         patterns = pattern_ceilings(torch, stream, local, n, src, coeffs, coded, pitch, plan, out, status)
         e2e = end_to_end(ctx)
+        if not args.no_api_shapes:
+            shapes = api_shapes(ctx)
 
     # encode batch sweep beside the headline step (north_star: "at batch >= 256"):
     # one HBM-resident 16 GiB blob, encode-only launches of its first n chunksets, HIP events on the
@@ -755,6 +912,7 @@ def main():
             "commitment": commit,
             "pattern_ceilings": patterns,
             "end_to_end": e2e,
+            "api_shapes": shapes,
             "encode_batch_sweep": sweep,
         }
         line["per_rank"] = per_rank

@@ -34,12 +34,13 @@ using namespace decds;
 
 namespace {
 
-constexpr int SLOTS = 3;
+constexpr int SLOTS = 3;      // buffer slots of the encode pipeline and of the repair run form
+constexpr int MAX_SLOTS = 6;  // events a Pipe holds (the gather form's slot count is tunable)
 inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 struct Pipe {
     hipStream_t h2d = nullptr, comp = nullptr, d2h = nullptr;
-    hipEvent_t in_done[SLOTS] = {}, k_done[SLOTS] = {}, out_done[SLOTS] = {};
+    hipEvent_t in_done[MAX_SLOTS] = {}, k_done[MAX_SLOTS] = {}, out_done[MAX_SLOTS] = {};
     hipError_t init() {
         hipError_t e;
         // Stream priorities keep the two copy directions on different hardware queues. HIP backs the
@@ -151,7 +152,24 @@ int encode_range(decds_ctx *ctx, const uint8_t *blob, size_t blob_len, const uin
     batch = std::min(batch, n);
     const size_t PRF = N * PROOF_SIZE * 32;
     HostUse uin(blob, blob_len), ucv(coeffs, n * N * K), uout(coded, n * N * F);
-    HostUse urt(cm ? cm->roots : nullptr, n * 32), uprf(cm ? cm->proofs : nullptr, n * PRF);
+    // the commitment outputs (roots, proofs: 2,080 bytes per chunkset) land in one page-locked area
+    // of the call and are copied to the caller's memory at the end: staged through the out ring, two
+    // small copies per batch held ring pieces, and the host thread waited on them while the direct
+    // input copies of a page-locked blob could have run ahead (Blob::new of a page-locked 1 GiB blob
+    // 69 ms against 41 from pageable memory, r09c)
+    struct PinnedCm {
+        void *p = nullptr;
+        ~PinnedCm() {
+            if (p) hip_tolerate(hipHostFree(p), "hipHostFree");
+        }
+    } cmh;
+    uint8_t *h_roots = nullptr, *h_prf = nullptr;
+    if (cm) {
+        hipError_t pe = hipHostMalloc(&cmh.p, n * (32 + PRF), DECDS_HOST_MALLOC_FLAGS);
+        if (pe) return decds_hip_error(pe, "hipHostMalloc (commitment outputs)");
+        h_roots = static_cast<uint8_t *>(cmh.p);
+        h_prf = h_roots + n * 32;
+    }
     std::lock_guard<std::mutex> lock(ctx->host_mu);
     // the coding vectors of the whole range go over in one copy ahead of the first batch (160 bytes
     // per chunkset): staged per batch from pageable memory, each small copy held a ring piece and
@@ -175,8 +193,8 @@ int encode_range(decds_ctx *ctx, const uint8_t *blob, size_t blob_len, const uin
     auto issue_d2h = [&](int k, size_t b0, size_t nb) -> int {
         if ((e = hipStreamWaitEvent(pp.d2h, pp.k_done[k], 0)) ||
             (e = copy_d2h(coded + b0 * N * F, dout[k], nb * N * F, uout.pinned(), ctx->out_ring, pp.d2h)) ||
-            (cm && (e = copy_d2h(cm->roots + b0 * 32, drt[k], nb * 32, urt.pinned(), ctx->out_ring, pp.d2h))) ||
-            (cm && (e = copy_d2h(cm->proofs + b0 * PRF, dprf[k], nb * PRF, uprf.pinned(), ctx->out_ring, pp.d2h))) ||
+            (cm && (e = hipMemcpyAsync(h_roots + b0 * 32, drt[k], nb * 32, hipMemcpyDeviceToHost, pp.d2h))) ||
+            (cm && (e = hipMemcpyAsync(h_prf + b0 * PRF, dprf[k], nb * PRF, hipMemcpyDeviceToHost, pp.d2h))) ||
             (e = hipEventRecord(pp.out_done[k], pp.d2h)))
             return decds_hip_error(e, "D2H");
         return DECDS_OK;
@@ -214,20 +232,19 @@ int encode_range(decds_ctx *ctx, const uint8_t *blob, size_t blob_len, const uin
         pend = k, pend_b0 = b0, pend_nb = nb;
     }
     if (rc == DECDS_OK && pend >= 0) rc = issue_d2h(pend, pend_b0, pend_nb);
-    return finish_call(ctx, pp, rc);
+    rc = finish_call(ctx, pp, rc);
+    if (rc == DECDS_OK && cm) {
+        std::memcpy(cm->roots, h_roots, n * 32);
+        std::memcpy(cm->proofs, h_prf, n * PRF);
+    }
+    return rc;
 }
 
-// RepairingBlob::add_chunk over every arrival + get_repaired_chunkset for chunksets [0, n) of a
-// shard: coded / cand / out / status point at the shard's first chunkset, blob_len is its length
-int repair_range(decds_ctx *ctx, const uint8_t *coded_host, size_t n, const uint8_t *cand_host, size_t blob_len,
-                 uint8_t *out, int32_t *status_host, size_t batch) {
-    int s = decds_ctx_bind(ctx);
-    if (s) return s;
-    if (batch == 0) batch = 16;  // 8-32 measured best (DESIGN.md §7)
-    batch = std::min(batch, n);
-    // RepairingBlob::add_chunk over the arrival order (blob.rs:373-394): the rank test runs on the
-    // 10-byte coding vectors on the host, so only the 10 accepted rows of each chunkset cross PCIe
-    std::vector<uint8_t> sel(n * K, 0);
+// RepairingBlob::add_chunk's rank step over the arrival order of every chunkset (blob.rs:373-394,
+// chunkset.rs:173-184) on the 10-byte coding vectors: sel[c*K + a] = the a-th accepted row of
+// chunkset c, status NOT_YET_READY where the rank stays below 10
+void accept_rows(decds_ctx *ctx, const uint8_t *coded_host, size_t n, const uint8_t *cand_host, uint8_t *sel,
+                 int32_t *status_host) {
     for (size_t c = 0; c < n; c++) {
         uint8_t basis[K * K], piv[K];
         uint32_t rank = 0;
@@ -238,6 +255,192 @@ int repair_range(decds_ctx *ctx, const uint8_t *coded_host, size_t n, const uint
         }
         status_host[c] = rank == K ? DECDS_OK : DECDS_ERR_CHUNKSET_NOT_YET_READY;
     }
+}
+
+// The repair host path (RepairingBlob over every arrival + get_repaired_chunkset for chunksets [0, n)
+// of a shard; coded / cand / out / status point at the shard's first chunkset, blob_len is its
+// length), host-gather form: per batch, the host pool copies each ready chunkset's 10 accepted rows
+// into the slot's page-locked staging buffer, densely (chunkset i of the batch's ready ones at
+// i * 10 * F, rows in acceptance order), and the whole batch crosses the link as ONE copy; the plans
+// (rows 0..9 in order + the inverse of the accepted coding vectors, host_gf_invert — RepairingBlob's
+// decode_ready) go over beside them and the decode runs in its gather form. The gather of batch b+1
+// overlaps batch b's copy. The run form below (repair_range_runs) sent each run of consecutive
+// accepted rows as its own hipMemcpyAsync — about 500 per GiB, 30.9 ms at 1 GiB (r08zf) against a
+// duplex link bound of about 22 ms. DECDS_REPAIR_GATHER=0 selects the run form (A/B switch).
+int repair_range_gather(decds_ctx *ctx, const uint8_t *coded_host, size_t n, const uint8_t *cand_host, size_t blob_len,
+                        uint8_t *out, int32_t *status_host, size_t batch) {
+    int s = decds_ctx_bind(ctx);
+    if (s) return s;
+    if (batch == 0) batch = 16;
+    batch = std::min(batch, n);
+    // four slots: the gather of batch b needs slot b mod S free, i.e. batch b-S's D2H done; with three
+    // the host gathered while the link's H2D side sat idle behind the previous batch (DECDS_REPAIR_SLOTS)
+    static const int S = [] {
+        const char *v = std::getenv("DECDS_REPAIR_SLOTS");
+        return v ? std::max(2, std::min(MAX_SLOTS, std::atoi(v))) : 4;
+    }();
+    std::vector<uint8_t> sel(n * K, 0);
+    accept_rows(ctx, coded_host, n, cand_host, sel.data(), status_host);
+    // per slot, page-locked: the staged rows (batch x 10 x F), and a small area of plans + decode
+    // bases (H2D) and statuses + repair infos (D2H)
+    const size_t stage = align256(batch * K * F);
+    const size_t sm_plan = 0, sm_inb = align256(batch * sizeof(RepairPlan)), sm_outb = sm_inb + align256(batch * 8),
+                 sm_h2d = sm_outb + align256(batch * 8), sm_stat = sm_h2d, sm_info = sm_stat + align256(batch * 4),
+                 sm_bytes = sm_info + align256(batch * sizeof(decds_repair_info));
+    struct Pinned {
+        void *p = nullptr;
+        size_t n = 0;
+        ~Pinned() {
+            if (p) host_pinned_free(p, n);
+        }
+    } hst;
+    struct PinnedSmall {
+        void *p = nullptr;
+        ~PinnedSmall() {
+            if (p) hip_tolerate(hipHostFree(p), "hipHostFree");
+        }
+    } hsm;
+    hipError_t e;
+    if ((e = host_pinned_alloc(S * stage, &hst.p))) return decds_hip_error(e, "page-locked staging for accepted rows");
+    hst.n = S * stage;
+    if ((e = hipHostMalloc(&hsm.p, S * sm_bytes, DECDS_HOST_MALLOC_FLAGS))) return decds_hip_error(e, "hipHostMalloc");
+    uint8_t *hstage[MAX_SLOTS], *hsmall[MAX_SLOTS];
+    for (int i = 0; i < S; i++) {
+        hstage[i] = static_cast<uint8_t *>(hst.p) + i * stage;
+        hsmall[i] = static_cast<uint8_t *>(hsm.p) + i * sm_bytes;
+    }
+    HostUse uout(out, blob_len);
+    std::lock_guard<std::mutex> lock(ctx->host_mu);
+    const size_t dsz = stage + sm_bytes + align256(batch * CS);
+    uint8_t *base, *dstage[MAX_SLOTS], *dsmall[MAX_SLOTS], *ddst[MAX_SLOTS];
+    if ((e = decds_ctx_scratch(ctx, S * dsz, &base))) return decds_hip_error(e, "hipMalloc");
+    for (int i = 0; i < S; i++, base += dsz) {
+        dstage[i] = base;
+        dsmall[i] = base + stage;
+        ddst[i] = base + stage + sm_bytes;
+    }
+    Pipe pp;
+    if ((e = pp.init())) return decds_hip_error(e, "stream/event setup");
+    int rc = DECDS_OK;
+    size_t pending_b0[MAX_SLOTS];
+    std::vector<size_t> ready[MAX_SLOTS];  // batch positions of the slot's decoded chunksets
+    for (int i = 0; i < S; i++) pending_b0[i] = (size_t)-1;
+    // host side of slot k once its D2H is done (as repair_range_runs' finish): a chunkset whose decoded
+    // data holds no boundary marker is ChunksetRepairingFailed and gets no data; one whose cut falls
+    // inside the chunkset is zero past the cut (blob.rs:464 truncates only)
+    auto finish = [&](int k) -> int {
+        if (pending_b0[k] == (size_t)-1) return DECDS_OK;
+        hipError_t ee = hipEventSynchronize(pp.out_done[k]);
+        if (ee) return decds_hip_error(ee, "hipEventSynchronize");
+        const int32_t *stat = reinterpret_cast<const int32_t *>(hsmall[k] + sm_stat);
+        const decds_repair_info *info = reinterpret_cast<const decds_repair_info *>(hsmall[k] + sm_info);
+        for (size_t i = 0; i < ready[k].size(); i++) {
+            const size_t cs = pending_b0[k] + ready[k][i];
+            const size_t off = cs * CS, size = std::min(blob_len - off, (size_t)CS);
+            const size_t keep = stat[i] != DECDS_OK ? 0 : std::min<size_t>(info[i].decoded_len, size);
+            if (stat[i] != DECDS_OK) status_host[cs] = DECDS_ERR_CHUNKSET_REPAIRING_FAILED;
+            if (keep < size) {
+                if (!uout.pinned() && (ee = ctx->out_ring.flush())) return decds_hip_error(ee, "D2H (staged)");
+                std::memset(out + off + keep, 0, size - keep);
+            }
+        }
+        pending_b0[k] = (size_t)-1;
+        return DECDS_OK;
+    };
+    const std::vector<size_t> sizes = batch_sizes(n, batch, true);
+    for (size_t b0 = 0, it = 0; it < sizes.size() && rc == DECDS_OK; b0 += sizes[it], it++) {
+        const int k = (int)(it % S);
+        if ((rc = finish(k))) break;  // slot k's previous batch fully done: all its buffers are free
+        const size_t nb = sizes[it];
+        std::vector<size_t> &rl = ready[k];
+        rl.clear();
+        for (size_t c = 0; c < nb; c++)
+            if (status_host[b0 + c] == DECDS_OK) rl.push_back(c);
+        const size_t m = rl.size();
+        RepairPlan *plans = reinterpret_cast<RepairPlan *>(hsmall[k] + sm_plan);
+        uint64_t *inb = reinterpret_cast<uint64_t *>(hsmall[k] + sm_inb), *outb = reinterpret_cast<uint64_t *>(hsmall[k] + sm_outb);
+        for (size_t i = 0; i < m && rc == DECDS_OK; i++) {
+            const size_t c = b0 + rl[i];
+            uint8_t cv[K * K], inv[K * K];
+            for (uint32_t a = 0; a < K; a++) std::memcpy(cv + a * K, coded_host + (c * N + sel[c * K + a]) * F, K);
+            std::memset(&plans[i], 0, sizeof(RepairPlan));
+            for (uint32_t a = 0; a < K; a++) plans[i].sel[a] = (uint8_t)a;
+            plans[i].rank = K;
+            if (!host_gf_invert(cv, inv, ctx->poly)) {  // rank 10 was just established: cannot happen
+                rc = decds_set_error(DECDS_ERR_CHUNKSET_REPAIRING_FAILED, "accepted coding vectors of chunkset %zu are singular", c);
+                break;
+            }
+            for (uint32_t r = 0; r < K; r++)  // RepairPlan::inv is input-major
+                for (uint32_t q = 0; q < K; q++) plans[i].inv[q * K + r] = inv[r * K + q];
+            inb[i] = reinterpret_cast<uint64_t>(dstage[k] + i * K * F);
+            outb[i] = reinterpret_cast<uint64_t>(ddst[k] + rl[i] * CS);
+        }
+        if (rc) break;
+        // the gather: one 1 MiB row per job on the host pool, overlapping the previous batch's copies
+        host_parallel(m * K, [&](size_t j) {
+            const size_t i = j / K, a = j % K, c = b0 + rl[i];
+            std::memcpy(hstage[k] + (i * K + a) * F, coded_host + (c * N + sel[c * K + a]) * F, F);
+        });
+        if ((m && (e = hipMemcpyAsync(dstage[k], hstage[k], m * K * F, hipMemcpyHostToDevice, pp.h2d))) ||
+            (e = hipMemcpyAsync(dsmall[k], hsmall[k], sm_h2d, hipMemcpyHostToDevice, pp.h2d)) ||
+            (e = hipMemsetAsync(dsmall[k] + sm_stat, 0, align256(batch * 4), pp.h2d)) ||
+            (e = hipEventRecord(pp.in_done[k], pp.h2d)) || (e = hipStreamWaitEvent(pp.comp, pp.in_done[k], 0))) {
+            rc = decds_hip_error(e, "H2D");
+            break;
+        }
+        if (m && (e = launch_decode(ctx->geom, nullptr, F, m, dsmall[k] + sm_plan, nullptr,
+                                    reinterpret_cast<int32_t *>(dsmall[k] + sm_stat),
+                                    reinterpret_cast<const uint64_t *>(dsmall[k] + sm_inb),
+                                    reinterpret_cast<const uint64_t *>(dsmall[k] + sm_outb), ctx->poly, ctx->marker,
+                                    dsmall[k] + sm_info, pp.comp))) {
+            rc = decds_hip_error(e, "rlnc decode launch");
+            break;
+        }
+        if ((e = hipEventRecord(pp.k_done[k], pp.comp)) || (e = hipStreamWaitEvent(pp.d2h, pp.k_done[k], 0)) ||
+            (m && (e = hipMemcpyAsync(hsmall[k] + sm_stat, dsmall[k] + sm_stat, sm_bytes - sm_stat, hipMemcpyDeviceToHost,
+                                      pp.d2h)))) {
+            rc = decds_hip_error(e, "D2H");
+            break;
+        }
+        // repaired data of the ready chunksets, runs of consecutive ones as one copy each; the last
+        // chunkset of the blob truncated to its real size (blob.rs:464). Unready chunksets get no data.
+        for (size_t c0 = 0; c0 < nb && rc == DECDS_OK;) {
+            const size_t off0 = (b0 + c0) * CS;
+            if (status_host[b0 + c0] != DECDS_OK) {
+                std::memset(out + off0, 0, std::min(blob_len - off0, (size_t)CS));
+                c0++;
+                continue;
+            }
+            size_t c1 = c0 + 1;
+            while (c1 < nb && status_host[b0 + c1] == DECDS_OK) c1++;
+            const size_t len = std::min(blob_len - off0, (c1 - c0) * CS);
+            if ((e = copy_d2h(out + off0, ddst[k] + c0 * CS, len, uout.pinned(), ctx->out_ring, pp.d2h)))
+                rc = decds_hip_error(e, "D2H");
+            c0 = c1;
+        }
+        if (rc) break;
+        if ((e = hipEventRecord(pp.out_done[k], pp.d2h))) {
+            rc = decds_hip_error(e, "hipEventRecord");
+            break;
+        }
+        pending_b0[k] = b0;
+    }
+    for (int j = 0; j < S && rc == DECDS_OK; j++) rc = finish(j);  // each finish() waits on its own event
+    return finish_call(ctx, pp, rc);
+}
+
+// The run form of the repair host path (DECDS_REPAIR_GATHER=0): accepted rows keep their row slots on
+// the device, each run of consecutive accepted rows one hipMemcpyAsync, the device plan kernel
+int repair_range_runs(decds_ctx *ctx, const uint8_t *coded_host, size_t n, const uint8_t *cand_host, size_t blob_len,
+                      uint8_t *out, int32_t *status_host, size_t batch) {
+    int s = decds_ctx_bind(ctx);
+    if (s) return s;
+    if (batch == 0) batch = 16;  // 8-32 measured best (DESIGN.md §7)
+    batch = std::min(batch, n);
+    // the rank test runs on the 10-byte coding vectors on the host, so only the 10 accepted rows of
+    // each chunkset cross PCIe
+    std::vector<uint8_t> sel(n * K, 0);
+    accept_rows(ctx, coded_host, n, cand_host, sel.data(), status_host);
     // per-slot candidate lists and device statuses in page-locked memory (tiny, per call)
     struct Pinned {
         void *p = nullptr;
@@ -371,6 +574,16 @@ int repair_range(decds_ctx *ctx, const uint8_t *coded_host, size_t n, const uint
     }
     for (int j = 0; j < SLOTS && rc == DECDS_OK; j++) rc = finish(j);  // each finish() waits on its own event
     return finish_call(ctx, pp, rc);
+}
+
+int repair_range(decds_ctx *ctx, const uint8_t *coded_host, size_t n, const uint8_t *cand_host, size_t blob_len,
+                 uint8_t *out, int32_t *status_host, size_t batch) {
+    static const bool gather = [] {
+        const char *v = std::getenv("DECDS_REPAIR_GATHER");
+        return !v || std::strcmp(v, "0") != 0;
+    }();
+    return gather ? repair_range_gather(ctx, coded_host, n, cand_host, blob_len, out, status_host, batch)
+                  : repair_range_runs(ctx, coded_host, n, cand_host, blob_len, out, status_host, batch);
 }
 
 // Runs fn(ctx_g, lo, hi) for contiguous chunkset shards [lo, hi) of [0, n), one host thread per

@@ -23,6 +23,7 @@
 #include <mutex>
 #include <random>
 #include <string>
+#include <new>
 #include <vector>
 
 #include "../../include/decds_rlnc.h"
@@ -555,9 +556,16 @@ int decds_repairing_chunkset_repair(decds_repairing_chunkset *r, uint8_t *out, s
     auto deliver = [&](const uint8_t *body, const uint8_t *tail, size_t len) -> int {
         if (out_len) *out_len = len;
         if (out_cap < len) {
-            // kept (decoded bytes + tail): a retry with a larger buffer only copies
+            // kept (decoded bytes + tail, CS + 10 bytes held until the repair completes or the
+            // object is freed): a retry with a larger buffer only copies. Without the memory for the
+            // copy the caller still learns the length and the retry decodes again.
             if (r->decoded.empty()) {
-                r->decoded.resize(CS + K);
+                try {
+                    r->decoded.resize(CS + K);
+                } catch (const std::bad_alloc &) {
+                    return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "out buffer %zu < decoded length %zu "
+                                           "(no host memory to keep the decoded bytes: a retry decodes again)", out_cap, len);
+                }
                 par_memcpy(r->decoded.data(), body, CS);
                 std::memcpy(r->decoded.data() + CS, tail, K);
                 r->decoded_len = len;

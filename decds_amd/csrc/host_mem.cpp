@@ -166,7 +166,8 @@ HostUse::~HostUse() {
 // ---- page-locked block cache ---------------------------------------------------------------------
 // Page-locking costs ~0.25 s per GiB on the GPU box (hipHostMalloc of a Blob's 1.6 GiB coded store
 // 0.08-0.16 s, its hipHostFree 0.07 s): blocks of at least CACHE_MIN bytes are kept on free, up to
-// DECDS_PINNED_CACHE_MB in total (default 4 GiB), and handed out again for requests of 80-100 % of
+// DECDS_PINNED_CACHE_MB in total (default 8 GiB: a 4 GiB Blob's coded store is 6.4 GiB, the largest
+// size of the reference's build_blob bench), and handed out again for requests of 80-100 % of
 // their size. decds_host_cache_trim() returns them to the system; so does destroying the process's
 // last context (capi.cpp), so an idle process holds no cached page-locked memory.
 namespace {
@@ -178,7 +179,7 @@ size_t g_cached = 0;
 size_t cache_cap() {
     static const size_t cap = [] {
         const char *v = std::getenv("DECDS_PINNED_CACHE_MB");
-        return v ? (size_t)std::strtoull(v, nullptr, 10) << 20 : (size_t)4 << 30;
+        return v ? (size_t)std::strtoull(v, nullptr, 10) << 20 : (size_t)8 << 30;
     }();
     return cap;
 }

@@ -219,7 +219,9 @@ int decds_repairing_chunkset_is_ready_to_repair(const decds_repairing_chunkset *
  * the last boundary marker (decds_repair_info), up to DECDS_DECODED_MAX_BYTES. No marker ->
  * DECDS_ERR_CHUNKSET_REPAIRING_FAILED. out_cap below the decoded length -> DECDS_ERR_INVALID_ARGUMENT
  * with *out_len set and the decoder kept, its result too (a retry with a larger buffer only copies
- * it out: no second transfer or decode). Consumes the decoder state on success (a second call
+ * it out: no second transfer or decode; the kept result is CS + 10 bytes of host memory held by the
+ * object until the repair completes or the object is freed — without memory for it the retry
+ * decodes again). Consumes the decoder state on success (a second call
  * returns DECDS_ERR_CHUNKSET_ALREADY_REPAIRED). */
 int decds_repairing_chunkset_repair(decds_repairing_chunkset *rcs, uint8_t *out, size_t out_cap, size_t *out_len);
 void decds_repairing_chunkset_free(decds_repairing_chunkset *rcs);
@@ -405,7 +407,7 @@ int decds_host_register(const void *ptr, size_t len);
 int decds_host_unregister(const void *ptr);
 /* page-locked host memory the host paths DMA directly (hipHostMalloc + the same registry). Blocks
  * of 64 MiB and more (the library's own, e.g. a Blob's coded store, and these) go to a cache when
- * freed — up to DECDS_PINNED_CACHE_MB (default 4096; all of them freed when the last context is destroyed) — and serve later requests of 80-100 % of
+ * freed — up to DECDS_PINNED_CACHE_MB (default 8192; all of them freed when the last context is destroyed) — and serve later requests of 80-100 % of
  * their size without page-locking again (~0.25 s per GiB); decds_host_cache_trim releases them and
  * returns the bytes released. Memory from the cache is not zeroed. */
 int decds_host_alloc(size_t len, void **out);

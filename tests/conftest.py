@@ -10,6 +10,8 @@ sys.path.insert(0, os.path.join(ROOT, "oracle"))
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a gfx950 (MI355X) device; runs the HIP kernels")
+    config.addinivalue_line("markers", "perf: a wall-clock gate (kernel fractions of the HBM roofline, host-path "
+                                       "rates); also marked gpu, deselect with -m 'gpu and not perf'")
 
 
 @pytest.fixture(scope="session")

@@ -186,6 +186,7 @@ def test_bench_one_rank_rccl_group_runs_the_distributed_path():
 
 
 @pytest.mark.gpu
+@pytest.mark.perf
 def test_bench_encode_batch_sweep_fields():
     # the encode batch sweep (north_star "at batch >= 256"): one record per size, kernel and
     # fraction of 8 TB/s; small sizes also as a stream of launches and between timing events that skip the
@@ -205,4 +206,28 @@ def test_bench_encode_batch_sweep_fields():
             assert nf["encode_ms"] <= x["encode_ms"] * 1.05, (x["chunksets"], nf, x["encode_ms"])
         else:
             assert "no_system_fence" not in x
-    assert min(x["frac"] for x in sw if x["chunksets"] >= 256) > 0.6  # north_star: >= 0.70 (measured 0.73-0.76)
+    # north_star: >= 0.70 at batch >= 256 (measured 0.73-0.76 over rounds 3-5): a 10 % regression fails here
+    assert min(x["frac"] for x in sw if x["chunksets"] >= 256) >= 0.68, [(x["chunksets"], x["frac"]) for x in sw]
+
+
+R08ZF_FUSED_MS_PER_CHUNKSET = 15.02 / 1639   # round 5's final library: decds_encode_commit_batch at cfg3, HIP events
+
+
+@pytest.mark.gpu
+@pytest.mark.perf
+def test_perf_gates_cfg3_encode_decode_fused():
+    # The three streaming kernels at the headline's size (cfg3: 1639 chunksets, 16 GiB) against floors a
+    # 10 % regression crosses: encode >= 0.68 of 8 TB/s (north_star 0.70; measured 0.735-0.757), decode
+    # >= 0.60 (measured 0.646-0.666), the fused ChunkSet::new (rlnc_encode_hash_kernel + fold + trees)
+    # <= 1.15 x round 5's time per chunkset
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--config", "cfg3", "--steps", "5", "--warmup", "2",
+                        "--settle-s", "0.3", "--no-cpu-baseline", "--no-extras", "--no-sweep"], capture_output=True,
+                       text=True, timeout=200, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    rf, n = d["roofline"], d["config"]["chunksets_per_gpu"]
+    assert n == 1639
+    assert rf["encode"]["frac"] >= 0.68, rf["encode"]
+    assert rf["decode"]["frac"] >= 0.60, rf["decode"]
+    fused = d["commitment"]["chunkset_new"]["fused_ms"]
+    assert fused / n <= 1.15 * R08ZF_FUSED_MS_PER_CHUNKSET, (fused, n)

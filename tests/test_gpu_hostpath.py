@@ -287,6 +287,7 @@ def test_launch_reports_an_earlier_pending_hip_error_by_name(ctx):
 
 
 
+@pytest.mark.perf
 def test_blob_host_rate_does_not_depend_on_caller_streams():
     # The host pipeline's H2D and D2H streams must never share a hardware queue: HIP backs the streams
     # of a priority level with at most 4 queues and puts a new stream on the least-used one, so with
