@@ -372,6 +372,43 @@ def pattern_ceilings(torch, stream, device, n, src, coeffs, coded, pitch, plan, 
             "encode_ms": round(enc_ms, 4), "decode_ms": round(dec_ms, 4)}
 
 
+def copy_pattern_ceiling(torch, stream, n, coded, pitch, plan, out, reps=10):
+    """The decode's copy ceiling (tools/copypattern.hip, built into tools/bin/libdecds_copypattern.so): the
+    decode's exact HBM address stream — per ready chunkset the plan's ten selected coded rows read at
+    their payload offsets, ten byte-misaligned piece stores at i*L — with no tables, no arithmetic and
+    no tile counter, in each of its launch geometries; the fastest is the ceiling. Timed on the
+    headline's own plans and coded rows after the repaired bytes were checked (it overwrites the repaired
+    output). Median of `reps` launches per geometry, each between its own events on the bench stream."""
+    import ctypes
+    import numpy as np
+    path = os.path.join(ROOT, "tools", "bin", "libdecds_copypattern.so")
+    if not os.path.exists(path):
+        return {"error": "tools/bin/libdecds_copypattern.so not built (decds_amd.build.build_copypattern)"}
+    L = ctypes.CDLL(path)
+    vp, sz = ctypes.c_void_p, ctypes.c_size_t
+    L.decds_copy_pattern_decode.argtypes = [vp, sz, sz, vp, vp, ctypes.c_int, vp]
+    L.decds_copy_pattern_variant_name.restype = ctypes.c_char_p
+    st = vp(stream.cuda_stream)
+    res = {}
+    for v in range(4):
+        launch = lambda: L.decds_copy_pattern_decode(coded.data_ptr(), pitch, n, plan.data_ptr(), out.data_ptr(), v, st)
+        t_w = time.perf_counter()
+        while time.perf_counter() - t_w < 0.2:
+            for _ in range(4):
+                assert launch() == 0
+            stream.synchronize()
+        ev = [[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(reps)]
+        for e in ev:
+            e[0].record(stream)
+            assert launch() == 0
+            e[1].record(stream)
+        stream.synchronize()
+        res[L.decds_copy_pattern_variant_name(v).decode()] = round(float(np.median([a.elapsed_time(b) for a, b in ev])), 4)
+    best = min(res, key=res.get)
+    return {"library": "tools/bin/libdecds_copypattern.so (tools/copypattern.hip)", "launches": reps,
+            "variants_ms": res, "best": best, "decode_ms": res[best]}
+
+
 def end_to_end(ctx, chunksets=103, repeats=5, batch=16):
     """The PCIe-inclusive rate north_star asks for (blob in host memory -> coded chunks in host memory
     -> repaired blob in host memory): decds_blob_encode_host and decds_blob_repair_host (handle_break.rs
@@ -755,9 +792,10 @@ def main():
 
     # the kernels' own access-pattern ceilings (decode first: it needs the intact coded rows), then the
     # end-to-end host-memory rate (north_star: written in DESIGN.md §7) — both after the timed region
-    patterns, e2e, shapes = None, None, None
+    patterns, copy_ceiling, e2e, shapes = None, None, None, None
     if world == 1 and not args.no_extras:
         patterns = pattern_ceilings(torch, stream, local, n, src, coeffs, coded, pitch, plan, out, status)
+        copy_ceiling = copy_pattern_ceiling(torch, stream, n, coded, pitch, plan, out)
         e2e = end_to_end(ctx)
         if not args.no_api_shapes:
             shapes = api_shapes(ctx)
@@ -876,6 +914,13 @@ def main():
         p_gbs = nbytes / (patterns[key] * 1e-3) / 1e9
         return {"pattern_GBps": round(p_gbs, 1), "frac_of_pattern": round(gbs / p_gbs, 4)}
 
+    def copy_of(nbytes, gbs):
+        """the decode's copy ceiling (copy_pattern_ceiling) and the fraction of it reached"""
+        if not copy_ceiling or "decode_ms" not in copy_ceiling:
+            return {}
+        c_gbs = nbytes / (copy_ceiling["decode_ms"] * 1e-3) / 1e9
+        return {"copy_pattern_GBps": round(c_gbs, 1), "frac_of_copy_pattern": round(gbs / c_gbs, 4)}
+
     if rank == 0 or rehearse:
         # whole-job blob bytes (a rehearsal: this shard's bytes only)
         enc_total = float(blob_len_rank if rehearse else blob_per_gpu * world)
@@ -897,7 +942,7 @@ def main():
                          "decode": dict({"kernel": dec_kernel, "achieved": round(dec_gbs, 1),
                                          "frac": round(dec_gbs / HBM_PEAK_GBS, 4),
                                          "bytes_per_launch": dec_bytes, "ms": round(dec_ms, 4)},
-                                        **pattern_of(dec_bytes, dec_gbs, "decode_ms")),
+                                        **pattern_of(dec_bytes, dec_gbs, "decode_ms"), **copy_of(dec_bytes, dec_gbs)),
                          "encode": dict({"kernel": enc_kernel, "achieved": round(enc_gbs, 1),
                                          "frac": round(enc_gbs / HBM_PEAK_GBS, 4),
                                          "bytes_per_launch": enc_bytes, "ms": round(enc_ms, 4)},
@@ -911,6 +956,7 @@ def main():
                                                              blob_bytes=blob_per_gpu * world, shard_bytes=blob_len_rank),
             "commitment": commit,
             "pattern_ceilings": patterns,
+            "decode_copy_ceiling": copy_ceiling,
             "end_to_end": e2e,
             "api_shapes": shapes,
             "encode_batch_sweep": sweep,

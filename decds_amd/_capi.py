@@ -155,6 +155,7 @@ def _declare(L):
         "decds_encode_commit_workspace_bytes": (SZ, [SZ]),
         "decds_encode_kernel_name": (c.c_char_p, [SZ]),
         "decds_decode_kernel_name": (c.c_char_p, [SZ]),
+        "decds_repair_kernel_name": (c.c_char_p, [SZ]),
         "decds_tuning": (c.c_uint64, [c.c_char_p, c.c_uint64, c.c_int]),
         "decds_encode_commit_batch": (c.c_int, [P, VP, SZ, VP, VP, SZ, c.c_uint64, VP, VP, VP, VP, VP]),
     }
@@ -187,7 +188,7 @@ EXPORTED = [
     "decds_repairing_blob_get_repaired_chunkset", "decds_repairing_blob_free", "decds_repairing_blob_new_multi",
     "decds_repairing_blob_set_device_budget", "decds_repairing_blob_memory",
     "decds_encode_commit_workspace_bytes", "decds_encode_commit_batch", "decds_encode_kernel_name",
-    "decds_decode_kernel_name", "decds_host_cache_trim", "decds_blake3_stream_new", "decds_blake3_stream_update",
+    "decds_decode_kernel_name", "decds_repair_kernel_name", "decds_host_cache_trim", "decds_blake3_stream_new", "decds_blake3_stream_update",
     "decds_blake3_stream_finalize", "decds_blake3_stream_free", "decds_tuning",
 ]
 

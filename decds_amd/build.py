@@ -77,6 +77,26 @@ def build_pattern(force=False, verbose=True):
     return build(force=True, verbose=verbose, defines=["DECDS_STUDY_PATTERN=1", "decds=decds_pattern"], out=PATTERN_LIB)
 
 
+COPYPATTERN_LIB = os.path.join(HERE, "..", "tools", "bin", "libdecds_copypattern.so")
+COPYPATTERN_SRC = os.path.join(HERE, "..", "tools", "copypattern.hip")
+
+
+def build_copypattern(force=False):
+    """tools/bin/libdecds_copypattern.so: the decode's copy ceiling bench.py times (measurement only)"""
+    if not force and os.path.exists(COPYPATTERN_LIB) and \
+            os.path.getmtime(COPYPATTERN_LIB) >= max(os.path.getmtime(COPYPATTERN_SRC),
+                                                     os.path.getmtime(os.path.join(CSRC, "rlnc_layout.h"))):
+        return COPYPATTERN_LIB
+    os.makedirs(os.path.dirname(COPYPATTERN_LIB), exist_ok=True)
+    tmp = COPYPATTERN_LIB + ".tmp"
+    cmd = [HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-I" + CSRC, COPYPATTERN_SRC, "-o", tmp]
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+    if r.returncode != 0:
+        raise RuntimeError("hipcc failed: %s\n%s" % (" ".join(cmd), r.stdout.decode()))
+    os.replace(tmp, COPYPATTERN_LIB)
+    return COPYPATTERN_LIB
+
+
 if __name__ == "__main__":
     # python -m decds_amd.build [--force] [--variant NAME -DX=1 ... --mllvm=-opt=v ...]
     args = sys.argv[1:]

@@ -81,8 +81,19 @@ def decode_batch(ctx, coded, n, plan, dst, status, pitch=CODED_PIECE_BYTES, stre
 
 
 def repair_batch(ctx, coded, n, cand, plan, verdicts, dst, status, pitch=CODED_PIECE_BYTES, stream=None, info=None):
-    repair_plan_batch(ctx, coded, n, cand, plan, verdicts, status, pitch, stream)
-    decode_batch(ctx, coded, n, plan, dst, status, pitch, stream, info)
+    """decds_repair_batch: repair_plan_batch + decode_batch in one call — up to DECDS_PLAN_DECODE_MAX_N
+    chunksets (default 16) one kernel launch (rlnc_plan_decode_kernel), the same outputs either way"""
+    _need(coded, (n * N - 1) * pitch + CODED_PIECE_BYTES, "coded")
+    _need(cand, n * N, "cand")
+    _need(plan, n * REPAIR_PLAN_BYTES, "plan")
+    _need(verdicts, n * N, "verdicts")
+    _need(dst, n * CHUNKSET_BYTES, "dst")
+    _need(status, n * 4, "status")
+    if info is not None:
+        _need(info, n * REPAIR_INFO_BYTES, "info")
+    check(lib().decds_repair_batch(ctx.handle, _ptr(coded), pitch, n, _ptr(cand), _ptr(plan),
+                                   _ptr(verdicts), _ptr(dst), _ptr(status), None if info is None else _ptr(info),
+                                   _stream(stream)))
 
 
 def repair_info(info, n):

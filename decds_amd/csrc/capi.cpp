@@ -266,10 +266,17 @@ int decds_decode_batch(decds_ctx *ctx, const uint8_t *coded, size_t coded_pitch,
 int decds_repair_batch(decds_ctx *ctx, const uint8_t *coded, size_t coded_pitch, size_t n,
                        const uint8_t *cand, uint8_t *plan, int8_t *verdicts, uint8_t *dst,
                        int32_t *status, decds_repair_info *info, void *stream) {
-    int s = decds_repair_plan_batch(ctx, coded, coded_pitch, n, cand, plan, verdicts, status, stream);
-    if (s) return s;
-    return decds_decode_batch(ctx, coded, coded_pitch, n, plan, dst, status, info, stream);
+    int s;
+    if ((s = decds_ctx_bind(ctx)) || (s = check_n(n)) || (s = check_pitch(coded_pitch))) return s;
+    if (!coded || !cand || !plan || !verdicts || !dst || !status)
+        return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "null buffer");
+    if (reinterpret_cast<uintptr_t>(info) & 3u) return decds_set_error(DECDS_ERR_INVALID_ARGUMENT, "info not 4-byte aligned");
+    hipError_t e = launch_repair(ctx->geom, coded, coded_pitch, n, cand, plan, verdicts, dst, status, ctx->poly, ctx->gen,
+                                 ctx->marker, reinterpret_cast<uint8_t *>(info), (hipStream_t)stream);
+    return e == hipSuccess ? DECDS_OK : decds_hip_error(e, "repair launch");
 }
+
+const char *decds_repair_kernel_name(size_t n_chunksets) { return repair_kernel_name(n_chunksets); }
 
 int decds_fill_random_device(decds_ctx *ctx, uint64_t seed, uint64_t byte_offset, uint8_t *dst,
                              size_t nbytes, void *stream) {

@@ -20,7 +20,8 @@ struct LaunchGeom {
     uint32_t enc_grid = 0, enc_small_grid = 0, dec_grid = 0;
 };
 void configure_geom(LaunchGeom &g);
-// launch-shape thresholds by name (DECDS_DEC_SWEEP_MIN_N, DECDS_ENC_SMALL_MAX_N, DECDS_ENC_NT_MIN_N, with or without the
+// launch-shape thresholds by name (DECDS_DEC_SWEEP_MIN_N, DECDS_ENC_SMALL_MAX_N, DECDS_ENC_NT_MIN_N,
+// DECDS_PLAN_DECODE_MAX_N, with or without the
 // DECDS_ prefix): set (set = true; UINT64_MAX = the default again) and/or read; UINT64_MAX if unknown
 uint64_t set_tuning(const char *name, uint64_t value, bool set);
 
@@ -48,6 +49,13 @@ hipError_t launch_decode(const LaunchGeom &g, const uint8_t *coded, size_t pitch
                          const uint8_t *plan, uint8_t *dst, int32_t *status, const uint64_t *in_bases,
                          const uint64_t *out_bases, uint32_t poly, uint32_t marker, uint8_t *info,
                          hipStream_t stream);
+// RepairingChunkSet's rank step + repair for n chunksets (decds_repair_batch): the plan kernel then
+// the decode, or — up to DECDS_PLAN_DECODE_MAX_N chunksets (one-tile decode form) — both as one launch
+// (rlnc_plan_decode_kernel), with the same outputs
+hipError_t launch_repair(const LaunchGeom &g, const uint8_t *coded, size_t pitch, size_t n, const uint8_t *cand,
+                         uint8_t *plan, int8_t *verdicts, uint8_t *dst, int32_t *status, uint32_t poly, uint32_t gen,
+                         uint32_t marker, uint8_t *info, hipStream_t stream);
+const char *repair_kernel_name(size_t n);  // the first kernel launch_repair runs for n chunksets
 hipError_t launch_fill_random(uint64_t seed, uint64_t byte_offset, uint8_t *dst, size_t nbytes,
                               hipStream_t stream);
 const char *encode_kernel_name(size_t n);  // the kernel launch_encode runs for n chunksets

@@ -1318,13 +1318,28 @@ struct GfExpTable {
 };
 constexpr uint32_t PLAN_LOG0 = 512;
 constexpr uint32_t PLAN_EXP_BYTES = 2 * PLAN_LOG0 + 4;  // largest index: log0 + log0
-__global__ __launch_bounds__(64) void rlnc_plan_kernel(const uint8_t *__restrict__ coded, size_t pitch, size_t n,
-                                                       const uint8_t *__restrict__ cand,
-                                                       RepairPlan *__restrict__ plan,
-                                                       int8_t *__restrict__ verdicts,
-                                                       int32_t *__restrict__ status, GfExpTable tab) {
-    const size_t cs = blockIdx.x;
-    const uint32_t lane = threadIdx.x;
+// the plan's LDS scratch: exp / log tables and the logs of every coded row's coding vector
+struct PlanLds {
+    uint8_t exp[(PLAN_EXP_BYTES + 15) & ~15u];
+    uint16_t log[256];
+    uint16_t lcv[N * 16];  // log of byte c of row r's coding vector at r * 16 + c
+};
+
+// LDS visibility among the lanes of one wave: its LDS operations complete in order, so waiting for
+// them is enough (the fused kernel's plan runs on one wave while the others wait at a barrier)
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+    __builtin_amdgcn_wave_barrier();
+}
+
+// The plan of chunkset cs on one wave (lane = threadIdx.x & 63): writes *pl (rank always; sel and the
+// input-major inverse when ready) and, when status is given, status[cs]; returns lane a's verdict for
+// candidate a (< 16). WAVE_SYNC: the caller's other waves do not take part (wave-level LDS syncs).
+template <bool WAVE_SYNC>
+__device__ __forceinline__ int32_t plan_wave(const uint8_t *__restrict__ coded, size_t pitch, size_t cs,
+                                             const uint8_t *__restrict__ cand, PlanLds &sl, const GfExpTable &tab,
+                                             RepairPlan *pl, int32_t *__restrict__ status) {
+    const uint32_t lane = threadIdx.x & 63u;
     const bool col = lane < K;
     // the arrival order and the coding vector of every coded row of the chunkset (lane c < 10
     // loads byte c of rows 0..15): all in flight while the tables below are built
@@ -1332,9 +1347,8 @@ __global__ __launch_bounds__(64) void rlnc_plan_kernel(const uint8_t *__restrict
     uint32_t rowcv[N];
 #pragma unroll
     for (int r = 0; r < (int)N; r++) rowcv[r] = col ? coded[(cs * N + r) * pitch + lane] : 0u;
-    __shared__ __attribute__((aligned(16))) uint8_t s_exp[PLAN_EXP_BYTES];
-    __shared__ uint16_t s_log[256];
-    __shared__ uint16_t s_lcv[N * 16];  // log of byte c of row r's coding vector at r * 16 + c
+    uint8_t *s_exp = sl.exp;
+    uint16_t *s_log = sl.log, *s_lcv = sl.lcv;
     {
         // exp[i] = gen^i for i < 510 (doubled: a sum of two logs needs no reduction), zeros after
         const uint32_t e4 = tab.w[lane];  // exp[4 lane .. 4 lane + 3]
@@ -1351,12 +1365,12 @@ __global__ __launch_bounds__(64) void rlnc_plan_kernel(const uint8_t *__restrict
         if (lane < 2) s_exp[510 + lane] = 0;
         if (lane == 0) s_log[0] = PLAN_LOG0;
     }
-    __syncthreads();
+    if constexpr (WAVE_SYNC) wave_lds_sync(); else __syncthreads();
     if (col) {
 #pragma unroll
         for (int r = 0; r < (int)N; r++) s_lcv[r * 16 + lane] = s_log[rowcv[r]];
     }
-    __syncthreads();
+    if constexpr (WAVE_SYNC) wave_lds_sync(); else __syncthreads();
     // Basis slot k is filled by the k-th accepted candidate, so the slot loop is unrolled with k a
     // constant: step k reduces against k basis rows only, and the pivots stay in SGPRs. Candidates
     // are taken in arrival order by a uniform inner loop until one raises the rank.
@@ -1416,12 +1430,10 @@ __global__ __launch_bounds__(64) void rlnc_plan_kernel(const uint8_t *__restrict
             a++;
         }
     }
-    if (lane < N) verdicts[cs * N + lane] = (int8_t)my_verdict;
-    RepairPlan *pl = plan + cs;
     if (lane == 0) pl->rank = (uint8_t)rank;
     if (rank < K) {
-        if (lane == 0) status[cs] = 5;  // DECDS_ERR_CHUNKSET_NOT_YET_READY
-        return;
+        if (lane == 0 && status) status[cs] = 5;  // DECDS_ERR_CHUNKSET_NOT_YET_READY
+        return my_verdict;
     }
     // inverse row piv[e] = combination part of basis row e: lane 10 + k writes inverse entry
     // (piv[e], k), stored input-major at k * K + piv[e] (so a table build reads 4 outputs' coefficients
@@ -1433,9 +1445,112 @@ __global__ __launch_bounds__(64) void rlnc_plan_kernel(const uint8_t *__restrict
     if (lane == 0) {
 #pragma unroll
         for (int e = 0; e < (int)K; e++) pl->sel[e] = (uint8_t)sel[e];
-        status[cs] = 0;
+        if (status) status[cs] = 0;
+    }
+    return my_verdict;
+}
+
+__global__ __launch_bounds__(64) void rlnc_plan_kernel(const uint8_t *__restrict__ coded, size_t pitch, size_t n,
+                                                       const uint8_t *__restrict__ cand,
+                                                       RepairPlan *__restrict__ plan,
+                                                       int8_t *__restrict__ verdicts,
+                                                       int32_t *__restrict__ status, GfExpTable tab) {
+    __shared__ __attribute__((aligned(16))) PlanLds sl;
+    const size_t cs = blockIdx.x;
+    const int32_t v = plan_wave<false>(coded, pitch, cs, cand, sl, tab, plan + cs, status);
+    if (threadIdx.x < N) verdicts[cs * N + threadIdx.x] = (int8_t)v;
+}
+
+// table_coeffs_imaj from an input-major inverse held in LDS (the fused plan + decode's own plan)
+template <int NIN, int NOUT>
+__device__ __forceinline__ uint32_t table_coeffs_imaj_lds(const uint8_t *M) {
+    const uint32_t p0 = threadIdx.x;
+    const bool live = p0 < NIN * 8;
+    const uint32_t p = live ? p0 : 0u, q = p & 3u, i = p >> 3;
+    uint32_t w = 0;
+#pragma unroll
+    for (uint32_t jj = 0; jj < 4; jj++)
+        if (4 * q + jj < (uint32_t)NOUT) w |= (uint32_t)M[i * NOUT + 4 * q + jj] << (8 * jj);
+    return live ? w : 0u;
+}
+
+// Repair of a small batch as ONE launch (decds_repair_batch for n <= DECDS_PLAN_DECODE_MAX_N): the
+// one-tile decode (rlnc_decode_kernel) whose workgroups first run their chunkset's plan themselves —
+// wave 0 replays the rank test and inverts the accepted coding vectors (plan_wave, into LDS) while
+// the other waves wait at the barrier; the workgroup of tile 0 also writes the plan, the verdicts and
+// the status to memory, as rlnc_plan_kernel would. Every workgroup of a chunkset computes the same
+// plan (about 256 per chunkset: the plan's few microseconds of one wave, in parallel, against a
+// second launch and its plan round trip through memory). Same bytes as plan + decode.
+template <int SAUX = 0>
+__global__ __launch_bounds__(WG, DECDS_DEC_WAVES) __attribute__((amdgpu_waves_per_eu(DECDS_DEC_WAVES, DECDS_DEC_WAVES)))
+void rlnc_plan_decode_kernel(const uint8_t *__restrict__ coded, size_t pitch, size_t n, const uint8_t *__restrict__ cand,
+                             RepairPlan *__restrict__ plan, int8_t *__restrict__ verdicts, uint8_t *__restrict__ dst,
+                             int32_t *__restrict__ status, uint32_t poly, uint32_t marker, uint32_t *__restrict__ info,
+                             GfExpTable tab) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    tables_at_lds_zero();
+    TailLds &s_tail = *reinterpret_cast<TailLds *>(lds + LDS_BYTES);
+    PlanLds &s_plan = *reinterpret_cast<PlanLds *>(lds + LDS_BYTES + TAIL_LDS);
+    RepairPlan &s_rp = *reinterpret_cast<RepairPlan *>(lds + LDS_BYTES + TAIL_LDS + sizeof(PlanLds));
+    constexpr int DW = DECDS_DEC_DW;
+    constexpr uint32_t T = TILES<DW>;
+    constexpr uint32_t phase = 0;
+    uint32_t u = blockIdx.x;
+    if constexpr (DEC_XCD_RUN > 1) {  // runs of consecutive tiles per XCD, as rlnc_decode_kernel
+        constexpr uint32_t R = DEC_XCD_RUN;
+        if (gridDim.x % (8 * R) == 0) u = (u / (8 * R)) * 8 * R + (u % 8) * R + (u / 8) % R;
+    }
+    const uint32_t cs = u / T, tile0 = u % T;
+    if (cs >= n) return;
+    const bool first = tile0 == 0;
+    if (threadIdx.x < 64) {
+        const int32_t v = plan_wave<true>(coded, pitch, cs, cand, s_plan, tab, &s_rp, first ? status : nullptr);
+        if (first && threadIdx.x < N) verdicts[(size_t)cs * N + threadIdx.x] = (int8_t)v;
+    }
+    if (first) tail_reset(s_tail);
+    lds_barrier();
+    const uint32_t *pw = reinterpret_cast<const uint32_t *>(&s_rp);
+    if (first && threadIdx.x < sizeof(RepairPlan) / 4)  // the plan, as rlnc_plan_kernel leaves it
+        reinterpret_cast<uint32_t *>(plan + cs)[threadIdx.x] = pw[threadIdx.x];
+    const uint32_t w0 = __builtin_amdgcn_readfirstlane(pw[0]);
+    const uint32_t w1 = __builtin_amdgcn_readfirstlane(pw[1]);
+    const uint32_t w2 = __builtin_amdgcn_readfirstlane(pw[2]);
+    if (((w2 >> 16) & 0xFFu) != K) return;  // RepairPlan::rank at byte 10: not ready
+    const uint32_t sel[K] = {w0 & 0xFFu, (w0 >> 8) & 0xFFu, (w0 >> 16) & 0xFFu, w0 >> 24,
+                             w1 & 0xFFu, (w1 >> 8) & 0xFFu, (w1 >> 16) & 0xFFu, w1 >> 24,
+                             w2 & 0xFFu, (w2 >> 8) & 0xFFu};
+    uint32_t ioff[K], ooff[K];
+#pragma unroll
+    for (int k = 0; k < (int)K; k++) ioff[k] = (uint32_t)(sel[k] * pitch + K);
+#pragma unroll
+    for (int i = 0; i < (int)K; i++) ooff[i] = piece_off(i);
+    const uint8_t *ibase = coded + (size_t)cs * N * pitch;
+    uint8_t *obase = dst + (size_t)cs * CS;
+    const uint32_t cw = table_coeffs_imaj_lds<K, K>(s_rp.inv);
+    Vec<DW> x[K];
+    if constexpr (DECDS_PREFETCH_FIRST) load_block<K, DW>(x, ibase, ioff, tile_col<DW, false>(tile0, tile0 + 1, phase));
+    build_tables<K, K>(lds, cw, poly);
+    lds_barrier();
+    stream_range<K, K, DW, DECDS_PREFETCH_FIRST, false, DECDS_DEC_HB, SAUX>(tile0, tile0 + 1, phase, ibase, ioff, obase, ooff, x);
+    if (first) {
+        // the edge columns and get_decoded_data's cut, as rlnc_decode_kernel's edge pass
+        for (uint32_t idx = threadIdx.x; idx < edge_cols<DW, false>(phase) * K; idx += WG) {
+            const uint32_t i = idx % K, col = edge_col<DW, false>(idx / K, phase);
+            uint32_t z = 0;
+#pragma unroll
+            for (uint32_t k = 0; k < K; k++) z ^= tbl_mul(lds, k, i, ibase[ioff[k] + col]);
+            const uint64_t p = (uint64_t)i * L + col;
+            if (p < CS)
+                obase[p] = (uint8_t)z;
+            else
+                tail_note(s_tail, p, z, marker);
+        }
+        lds_barrier();
+        tail_scan_decoded(s_tail, lds, ibase, ioff, marker);
+        tail_finish(s_tail, cs, status, info);
     }
 }
+constexpr uint32_t PLAN_DEC_LDS = DEC_LDS + sizeof(PlanLds) + sizeof(RepairPlan);
 
 __device__ __forceinline__ uint64_t splitmix_word(uint64_t seed, uint64_t w) {
     uint64_t z = seed + (w + 1) * 0x9E3779B97F4A7C15ull;
@@ -1517,7 +1632,9 @@ hipError_t configure_kernels() {
     }
     // every other kernel's code object resolved now, on the creating thread, not lazily by the first
     // launch — which may come from several caller threads at once (the coalesced ChunkSet::new)
-    const void *rest[] = {reinterpret_cast<const void *>(rlnc_plan_kernel), reinterpret_cast<const void *>(fill_random_words_kernel),
+    const void *rest[] = {reinterpret_cast<const void *>(rlnc_plan_kernel), reinterpret_cast<const void *>(rlnc_plan_decode_kernel<0>),
+                          reinterpret_cast<const void *>(rlnc_plan_decode_kernel<STORE_SC1>),
+                          reinterpret_cast<const void *>(fill_random_words_kernel),
                           reinterpret_cast<const void *>(fill_random_bytes_kernel)};
     for (const void *f : rest) {
         hipFuncAttributes a;
@@ -1536,6 +1653,9 @@ hipError_t configure_kernels() {
 #ifndef DECDS_ENC_NT_MIN_N
 #define DECDS_ENC_NT_MIN_N 256
 #endif
+#ifndef DECDS_PLAN_DECODE_MAX_N
+#define DECDS_PLAN_DECODE_MAX_N 16  // decds_repair_batch: plan + decode as one launch up to this many chunksets
+#endif
 // Launch-shape thresholds (process-wide): the environment variable of the same name read once (at
 // first use), else the build's default; decds_set_tuning changes one for the process (tests force
 // either form of a kernel pair, tools A/B them). Every form gives identical bytes.
@@ -1549,14 +1669,17 @@ struct Tunable {
 };
 static const Tunable TUNABLES[] = {{"DECDS_DEC_SWEEP_MIN_N", DECDS_DEC_SWEEP_MIN_N},
                                    {"DECDS_ENC_SMALL_MAX_N", DECDS_ENC_SMALL_MAX_N},
-                                   {"DECDS_ENC_NT_MIN_N", DECDS_ENC_NT_MIN_N}};
-constexpr int TUNE_DEC_SWEEP_MIN_N = 0, TUNE_ENC_SMALL_MAX_N = 1, TUNE_ENC_NT_MIN_N = 2, N_TUNABLES = 3;
+                                   {"DECDS_ENC_NT_MIN_N", DECDS_ENC_NT_MIN_N},
+                                   {"DECDS_PLAN_DECODE_MAX_N", DECDS_PLAN_DECODE_MAX_N}};
+constexpr int TUNE_DEC_SWEEP_MIN_N = 0, TUNE_ENC_SMALL_MAX_N = 1, TUNE_ENC_NT_MIN_N = 2, TUNE_PLAN_DECODE_MAX_N = 3,
+              N_TUNABLES = 4;
 static uint64_t tune_default(int k) {
-    static const uint64_t d[N_TUNABLES] = {TUNABLES[0].initial(), TUNABLES[1].initial(), TUNABLES[2].initial()};
+    static const uint64_t d[N_TUNABLES] = {TUNABLES[0].initial(), TUNABLES[1].initial(), TUNABLES[2].initial(),
+                                           TUNABLES[3].initial()};
     return d[k];
 }
 static std::atomic<uint64_t> &tune(int k) {
-    static std::atomic<uint64_t> v[N_TUNABLES] = {{tune_default(0)}, {tune_default(1)}, {tune_default(2)}};
+    static std::atomic<uint64_t> v[N_TUNABLES] = {{tune_default(0)}, {tune_default(1)}, {tune_default(2)}, {tune_default(3)}};
     return v[k];
 }
 uint64_t set_tuning(const char *name, uint64_t value, bool set) {
@@ -1570,6 +1693,9 @@ uint64_t set_tuning(const char *name, uint64_t value, bool set) {
 static bool decode_sweeps(size_t n) { return n >= tune(TUNE_DEC_SWEEP_MIN_N).load(std::memory_order_relaxed); }
 static bool encode_small(size_t n) { return n <= tune(TUNE_ENC_SMALL_MAX_N).load(std::memory_order_relaxed); }
 static bool encode_nt(size_t n) { return n >= tune(TUNE_ENC_NT_MIN_N).load(std::memory_order_relaxed); }
+static bool plan_decode_fused(size_t n) {
+    return n <= tune(TUNE_PLAN_DECODE_MAX_N).load(std::memory_order_relaxed) && !decode_sweeps(n);
+}
 
 // resident workgroups of a persistent kernel on this device (occupancy x CUs)
 static uint32_t resident_grid(const void *fn, uint32_t lds, int fallback_per_cu, int num_cus) {
@@ -1648,10 +1774,8 @@ hipError_t launch_encode_commit(const uint8_t *src, size_t n, const uint8_t *coe
     return hipGetLastError();
 }
 
-hipError_t launch_repair_plan(const uint8_t *coded, size_t pitch, size_t n, const uint8_t *cand, uint8_t *plan,
-                              int8_t *verdicts, int32_t *status, uint32_t poly, uint32_t gen, hipStream_t stream) {
-    if (n == 0) return hipSuccess;
-    // exp table of gen, kept for the last (poly, gen) asked for
+// exp table of gen under poly (the plan's log/exp tables), kept for the last (poly, gen) asked for
+static const GfExpTable &exp_table(uint32_t poly, uint32_t gen) {
     static thread_local uint32_t last_poly = 0, last_gen = 0;
     static thread_local GfExpTable tab;
     if (poly != last_poly || gen != last_gen) {
@@ -1669,6 +1793,13 @@ hipError_t launch_repair_plan(const uint8_t *coded, size_t pitch, size_t n, cons
         last_poly = poly;
         last_gen = gen;
     }
+    return tab;
+}
+
+hipError_t launch_repair_plan(const uint8_t *coded, size_t pitch, size_t n, const uint8_t *cand, uint8_t *plan,
+                              int8_t *verdicts, int32_t *status, uint32_t poly, uint32_t gen, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    const GfExpTable &tab = exp_table(poly, gen);
     if (hipError_t p_ = hip_launch_begin("rlnc_plan_kernel")) return p_;
     hipLaunchKernelGGL(rlnc_plan_kernel, dim3((uint32_t)n), dim3(64), 0, stream, coded, pitch, n, cand,
                        reinterpret_cast<RepairPlan *>(plan), verdicts, status, tab);
@@ -1715,6 +1846,30 @@ hipError_t launch_decode(const LaunchGeom &geom, const uint8_t *coded, size_t pi
     // (tail_scan_decoded for the chunksets whose tail bytes hold no marker): one launch
     return launch_decode_kernel(geom, coded, pitch, n, plan, dst, status, in_bases, out_bases, poly, marker, inf, stream);
 }
+
+hipError_t launch_repair(const LaunchGeom &geom, const uint8_t *coded, size_t pitch, size_t n, const uint8_t *cand,
+                         uint8_t *plan, int8_t *verdicts, uint8_t *dst, int32_t *status, uint32_t poly, uint32_t gen,
+                         uint32_t marker, uint8_t *info, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    if (!plan_decode_fused(n)) {
+        if (hipError_t e = launch_repair_plan(coded, pitch, n, cand, plan, verdicts, status, poly, gen, stream)) return e;
+        return launch_decode(geom, coded, pitch, n, plan, dst, status, nullptr, nullptr, poly, marker, info, stream);
+    }
+    const GfExpTable &tab = exp_table(poly, gen);
+    RepairPlan *pl = reinterpret_cast<RepairPlan *>(plan);
+    uint32_t *inf = reinterpret_cast<uint32_t *>(info);
+    const dim3 grid((uint32_t)(n * TILES<DECDS_DEC_DW>));
+    if (hipError_t p_ = hip_launch_begin("rlnc_plan_decode_kernel")) return p_;
+    if (n <= DEC_WT_MAX_N)
+        hipLaunchKernelGGL((rlnc_plan_decode_kernel<STORE_SC1>), grid, dim3(WG), PLAN_DEC_LDS, stream, coded, pitch, n, cand, pl,
+                           verdicts, dst, status, poly, marker, inf, tab);
+    else
+        hipLaunchKernelGGL((rlnc_plan_decode_kernel<0>), grid, dim3(WG), PLAN_DEC_LDS, stream, coded, pitch, n, cand, pl,
+                           verdicts, dst, status, poly, marker, inf, tab);
+    return hipGetLastError();
+}
+
+const char *repair_kernel_name(size_t n) { return plan_decode_fused(n) ? "rlnc_plan_decode_kernel" : "rlnc_plan_kernel"; }
 
 hipError_t launch_fill_random(uint64_t seed, uint64_t byte_offset, uint8_t *dst, size_t nbytes,
                               hipStream_t stream) {

@@ -142,19 +142,27 @@ int decds_decode_batch(decds_ctx *ctx, const uint8_t *coded, size_t coded_pitch,
  * rlnc_decode_sweep_kernel from DECDS_DEC_SWEEP_MIN_N chunksets on, rlnc_decode_kernel below */
 const char *decds_decode_kernel_name(size_t n_chunksets);
 /* Launch-shape thresholds, process-wide (every form gives identical bytes; these only pick the faster
- * kernel form per batch size): "DECDS_DEC_SWEEP_MIN_N" (default 256: persistent decode sweep from
+ * kernel form per batch size): "DECDS_DEC_SWEEP_MIN_N" (default 1536: persistent decode sweep from
  * that many chunksets on), "DECDS_ENC_SMALL_MAX_N" (default 2: encode batches up to that many
- * chunksets run 8-column tiles, twice as many workgroups) and "DECDS_ENC_NT_MIN_N" (default 256: from
- * that many chunksets on the encode stores its coded rows non-temporal, below write-through). Each starts from the environment variable
+ * chunksets run 8-column tiles, twice as many workgroups), "DECDS_ENC_NT_MIN_N" (default 256: from
+ * that many chunksets on the encode stores its coded rows non-temporal, below write-through) and
+ * "DECDS_PLAN_DECODE_MAX_N" (default 16: decds_repair_batch runs plan + decode as one kernel,
+ * rlnc_plan_decode_kernel, up to that many chunksets). Each starts from the environment variable
  * of its name (read once, at first use) or the default. set != 0 sets it (value UINT64_MAX: back to
  * that start value). Returns the value in force, UINT64_MAX for an unknown name. */
 uint64_t decds_tuning(const char *name, uint64_t value, int set);
 
 /* plan + decode in one call (the RepairingBlob::add_chunk loop + get_repaired_chunkset,
- * blob.rs:373-394, 451-473, for candidates already resident on the device) */
+ * blob.rs:373-394, 451-473, for candidates already resident on the device); the same outputs as
+ * decds_repair_plan_batch followed by decds_decode_batch — up to DECDS_PLAN_DECODE_MAX_N chunksets
+ * in one kernel launch (each decode workgroup runs its chunkset's plan first) */
 int decds_repair_batch(decds_ctx *ctx, const uint8_t *coded, size_t coded_pitch,
                        size_t n_chunksets, const uint8_t *cand, uint8_t *plan, int8_t *verdicts,
                        uint8_t *dst, int32_t *status, decds_repair_info *info, void *stream);
+/* name of the first gfx950 kernel decds_repair_batch launches for n chunksets: rlnc_plan_decode_kernel
+ * (plan and decode in one launch) up to DECDS_PLAN_DECODE_MAX_N, else rlnc_plan_kernel (then the
+ * decds_decode_kernel_name kernel) */
+const char *decds_repair_kernel_name(size_t n_chunksets);
 
 /* Counter-based SplitMix64 byte stream (seeded, reproducible on host and device) for synthetic
  * blobs and coding vectors; byte p = byte (p%8) of mix64(seed + (p/8 + 1) * 0x9E3779B97F4A7C15). */

@@ -245,12 +245,9 @@ def test_repair_batch_nothing_ready_leaves_every_output(ctx):
     assert list(host(status)) == [5] * n
     assert (host(out) == 0x5A).all()
 
-def test_repair_plan_fuzz_low_rank_and_repeats(ctx):
-    """The plan kernel alone (chunkset.rs:173-184 replayed per candidate) on 96 chunksets of
-    rank-deficient coding vectors: rows drawn from random subspaces of rank 1..10, zero and repeated
-    rows, candidate lists of every length with repeated ids. Verdicts, rank and status must equal the
-    oracle decoder's; at rank 10 sel must be the accepted rows in order and inv their inverse."""
-    n = 96
+def _fuzz_plan_inputs(n=96):
+    """coding vectors of rank-deficient chunksets (rows from random subspaces of rank 1..10, zero and
+    repeated rows) and candidate lists of every length with repeated ids"""
     rng = np.random.default_rng(0x91A7)
     coded = torch.zeros(n * N * F, dtype=torch.uint8, device="cuda")
     vecs = np.zeros((n, N, K), np.uint8)
@@ -272,11 +269,10 @@ def test_repair_plan_fuzz_low_rank_and_repeats(ctx):
     host_rows = np.zeros((n * N, 16), np.uint8)
     host_rows[:, :K] = vecs.reshape(n * N, K)
     coded.view(n * N, F)[:, :16].copy_(dev(host_rows))
-    plan = torch.empty(n * 128, dtype=torch.uint8, device="cuda")
-    verd = torch.empty(n * N, dtype=torch.int8, device="cuda")
-    status = torch.full((n,), -7, dtype=torch.int32, device="cuda")
-    codec.repair_plan_batch(ctx, coded, n, dev(cand), plan, verd, status)
-    st, v, pl = host(status), host(verd).reshape(n, N), host(plan).reshape(n, 128)
+    return coded, vecs, cand
+
+
+def _check_plans_against_oracle(n, vecs, cand, st, v, pl):
     ranks = set()
     for c in range(n):
         ov, rank = _oracle_verdicts(vecs[c], cand[c])
@@ -298,6 +294,106 @@ def test_repair_plan_fuzz_low_rank_and_repeats(ctx):
                     s ^= o.gf_mul(int(inv[i, k]), int(m[k, j]))
                 assert s == (1 if i == j else 0), (c, i, j)
     assert len(ranks) >= 8  # the draws cover most ranks
+
+
+def test_repair_plan_fuzz_low_rank_and_repeats(ctx):
+    """The plan kernel alone (chunkset.rs:173-184 replayed per candidate) on 96 chunksets of
+    rank-deficient coding vectors: rows drawn from random subspaces of rank 1..10, zero and repeated
+    rows, candidate lists of every length with repeated ids. Verdicts, rank and status must equal the
+    oracle decoder's; at rank 10 sel must be the accepted rows in order and inv their inverse."""
+    n = 96
+    coded, vecs, cand = _fuzz_plan_inputs(n)
+    plan = torch.empty(n * 128, dtype=torch.uint8, device="cuda")
+    verd = torch.empty(n * N, dtype=torch.int8, device="cuda")
+    status = torch.full((n,), -7, dtype=torch.int32, device="cuda")
+    codec.repair_plan_batch(ctx, coded, n, dev(cand), plan, verd, status)
+    _check_plans_against_oracle(n, vecs, cand, host(status), host(verd).reshape(n, N), host(plan).reshape(n, 128))
+
+
+@pytest.fixture
+def plan_decode_fused():
+    """decds_repair_batch with plan + decode as one launch (rlnc_plan_decode_kernel) at any batch size"""
+    from decds_amd._capi import lib
+    lib().decds_tuning(b"DECDS_PLAN_DECODE_MAX_N", 1 << 62, 1)
+    yield
+    lib().decds_tuning(b"DECDS_PLAN_DECODE_MAX_N", (1 << 64) - 1, 1)
+
+
+def test_fused_repair_plans_match_oracle_on_the_fuzz(ctx, plan_decode_fused):
+    """The fused kernel's plans (each decode workgroup runs its chunkset's plan on one wave; the tile-0
+    workgroup writes plan, verdicts and status) on the same 96 rank-deficient chunksets: identical to
+    the oracle decoder's, as the plan kernel's. (Payloads are zero: every ready chunkset decodes to
+    zeros, has no boundary marker anywhere, and ends ChunksetRepairingFailed.)"""
+    from decds_amd._capi import lib
+    assert lib().decds_repair_kernel_name(96) == b"rlnc_plan_decode_kernel"
+    n = 96
+    coded, vecs, cand = _fuzz_plan_inputs(n)
+    plan = torch.empty(n * 128, dtype=torch.uint8, device="cuda")
+    verd = torch.empty(n * N, dtype=torch.int8, device="cuda")
+    status = torch.full((n,), -7, dtype=torch.int32, device="cuda")
+    out = torch.empty(n * CS, dtype=torch.uint8, device="cuda")
+    codec.repair_batch(ctx, coded, n, dev(cand), plan, verd, out, status)
+    st = host(status)
+    ready = st != 5
+    assert set(np.unique(st[ready]).tolist()) == {6}  # zero payloads: no marker anywhere
+    st = np.where(ready, 0, st)
+    _check_plans_against_oracle(n, vecs, cand, st, host(verd).reshape(n, N), host(plan).reshape(n, 128))
+
+
+@pytest.mark.parametrize("n", [1, 2, 5, 16])
+def test_fused_repair_equals_plan_then_decode(ctx, n):
+    """decds_repair_batch at n <= 16 (one launch, rlnc_plan_decode_kernel) against the plan kernel then
+    the decode (the form above the threshold): plan bytes, verdicts, statuses, repair infos and every
+    repaired byte identical, and the repaired chunksets equal their sources. Candidates: shuffled full
+    lists, exactly 10, 9 (not ready), a repeated id, and a dependent row among the first 10."""
+    from decds_amd._capi import lib
+    rng = np.random.default_rng(0xF05E + n)
+    data = o.fill_random(0xF05E0 + n, n * CS)
+    coeffs = o.fill_random(0xF05E1 + n, n * N * K).reshape(n, N, K)
+    if n >= 5:
+        coeffs[4, 3] = coeffs[4, 1]           # chunkset 4: row 3 repeats row 1 (not useful when it arrives)
+    cand = np.full((n, N), 0xFF, np.uint8)
+    for c in range(n):
+        kind = c % 5
+        if kind == 0:
+            cand[c] = rng.permutation(N)
+        elif kind == 1:
+            cand[c, :K] = rng.permutation(N)[:K]
+        elif kind == 2:
+            cand[c, :K - 1] = rng.permutation(N)[:K - 1]     # rank 9: not ready
+        elif kind == 3:
+            p = rng.permutation(N)
+            cand[c, :12] = np.concatenate([p[:3], p[:1], p[3:11]])  # a repeated id
+        else:
+            cand[c, :13] = np.concatenate([[1, 3], rng.permutation([x for x in range(N) if x not in (1, 3)])[:11]])
+    coded = torch.empty(n * N * F, dtype=torch.uint8, device="cuda")
+    codec.encode_batch(ctx, dev(data), n, dev(coeffs.reshape(-1)), coded)
+    res = {}
+    for form, limit in (("fused", 1 << 62), ("split", 0)):
+        lib().decds_tuning(b"DECDS_PLAN_DECODE_MAX_N", limit, 1)
+        try:
+            assert lib().decds_repair_kernel_name(n) == (b"rlnc_plan_decode_kernel" if form == "fused" else b"rlnc_plan_kernel")
+            plan = torch.full((n * 128,), 0xEE, dtype=torch.uint8, device="cuda")
+            verd = torch.full((n * N,), 99, dtype=torch.int8, device="cuda")
+            status = torch.full((n,), -7, dtype=torch.int32, device="cuda")
+            out = torch.zeros(n * CS, dtype=torch.uint8, device="cuda")
+            info = torch.zeros(n * 16, dtype=torch.uint8, device="cuda")
+            codec.repair_batch(ctx, coded, n, dev(cand), plan, verd, out, status, info=info)
+            res[form] = [host(t) for t in (plan, verd, status, out, info)]
+        finally:
+            lib().decds_tuning(b"DECDS_PLAN_DECODE_MAX_N", (1 << 64) - 1, 1)
+    f, sp = res["fused"], res["split"]
+    st = sp[2]
+    assert np.array_equal(f[2], st) and np.array_equal(f[1], sp[1])
+    pf, ps = f[0].reshape(n, 128), sp[0].reshape(n, 128)
+    for c in range(n):
+        assert pf[c, 10] == ps[c, 10], c                       # rank
+        if st[c] == 0:
+            assert np.array_equal(pf[c, :K], ps[c, :K]) and np.array_equal(pf[c, 16:116], ps[c, 16:116]), c
+            assert np.array_equal(f[3][c * CS:(c + 1) * CS], data[c * CS:(c + 1) * CS]), c
+            assert np.array_equal(sp[3][c * CS:(c + 1) * CS], data[c * CS:(c + 1) * CS]), c
+            assert np.array_equal(f[4][c * 16:c * 16 + 14], sp[4][c * 16:c * 16 + 14]), c
+    assert set(st.tolist()) <= {0, 5} and (st == 5).sum() == sum(1 for c in range(n) if c % 5 == 2)
 
 
 MARKER = 0x81

@@ -193,7 +193,7 @@ def test_table_kernels_have_no_static_lds(tmp_path, which):
         pytest.skip("llvm-objdump not in this image")
     notes = _kernel_notes(tmp_path, which)
     table = {k: v for k, v in notes.items()
-             if any(s in k for s in ("encode_sweep_kernel", "decode_sweep_kernel", "rlnc_decode_kernel",
+             if any(s in k for s in ("encode_sweep_kernel", "decode_sweep_kernel", "rlnc_decode_kernel", "plan_decode_kernel",
                                      "encode_hash_kernel"))}
     assert len(table) >= 5, sorted(notes)
     for name, md in table.items():
@@ -224,7 +224,7 @@ def test_table_kernels_guard_their_lds_base(tmp_path, which):
         pytest.skip("llvm-objdump not in this image")
     funcs = _functions(_device_code(tmp_path, which))
     table = {k: v for k, v in funcs.items() if any(s in k for s in ("encode_sweep_kernel", "decode_sweep_kernel",
-                                                                    "rlnc_decode_kernel", "encode_hash_kernel"))}
+                                                                    "rlnc_decode_kernel", "encode_hash_kernel", "plan_decode_kernel"))}
     assert len(table) >= 5, sorted(funcs)[:20]
     for name, ins in table.items():
         assert any(x.startswith("s_trap 2") for _, x in ins), name
