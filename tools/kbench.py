@@ -19,6 +19,9 @@ def main():
     ap.add_argument("--dst-off", type=int, default=0, help="byte offset of the coded buffer (alignment study)")
     ap.add_argument("--check", action="store_true")
     ap.add_argument("--commit", action="store_true", help="also time decds_commit_batch (BLAKE3 + Merkle)")
+    ap.add_argument("--repair", action="store_true",
+                    help="also time decds_repair_batch (plan + decode in one call; one launch up to "
+                         "DECDS_PLAN_DECODE_MAX_N chunksets, rlnc_plan_decode_kernel)")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -47,7 +50,7 @@ def main():
         roots = torch.empty(n * 32, dtype=torch.uint8, device="cuda")
         proofs = torch.empty(n * N * 128, dtype=torch.uint8, device="cuda")
     torch.cuda.synchronize()
-    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(5)] for _ in range(a.reps + 3)]
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(6)] for _ in range(a.reps + 3)]
     for r in range(a.reps + 3):
         e = ev[r]
         e[0].record(st)
@@ -60,6 +63,11 @@ def main():
         if a.commit:
             codec.commit_batch(ctx, coded, n, dig, roots, proofs, pitch=pitch, stream=st)
             e[4].record(st)
+        if a.repair:
+            if not a.commit:  # (with --commit, e[4] already marks the commit's end)
+                e[4].record(st)
+            codec.repair_batch(ctx, coded, n, cand, plan, verd, out, status, pitch, stream=st)
+            e[5].record(st)
     torch.cuda.synchronize()
     t = np.array([[e[0].elapsed_time(e[1]), e[1].elapsed_time(e[2]), e[2].elapsed_time(e[3])] for e in ev[3:]])
     med = np.median(t, axis=0)
@@ -74,6 +82,11 @@ def main():
         tc = np.array([e[3].elapsed_time(e[4]) for e in ev[3:]])
         res["commit_ms"] = round(float(np.median(tc)), 4)
         res["commit_GBps"] = round(n * N * F / res["commit_ms"] / 1e6, 1)
+    if a.repair:
+        from decds_amd._capi import lib
+        tr = np.array([e[4].elapsed_time(e[5]) for e in ev[3:]])
+        res["repair_ms"] = round(float(np.median(tr)), 4)
+        res["repair_kernel"] = lib().decds_repair_kernel_name(n).decode()
     if a.check:
         good = True
         for c in np.nonzero(s == 0)[0].tolist():
