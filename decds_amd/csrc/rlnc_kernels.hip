@@ -12,7 +12,7 @@
 // (identical addresses broadcast) or rows on disjoint banks: the data-dependent lookups are
 // bank-conflict-free by construction (MI355X_MICROARCH.md §LDS) with no replicas — 5 KiB of tables
 // per workgroup, built with 16 ds_write_b32 by 80 threads (round 1 replicated every row 16x:
-// 80 KiB and ~3 µs of CU time per build, which made workgroups of fewer tiles lose).
+// 80 KiB and ~3 µs of CU time per build, which made workgroups of fewer tiles lose, profiles/HISTORY.md §8).
 // Per 16-column lane block: 10 unaligned 16-B loads, 320 conflict-free ds_read_b128, v_bitop3 XOR3
 // accumulation into a 16x16 byte block (columns x outputs), a v_perm byte transpose, 16 (or 10)
 // 16-B stores. No MFMA: this is byte-wise finite-field work, bounded by HBM bandwidth.
@@ -26,7 +26,7 @@
 // misalignment costs). The round-1 study variants
 // (persistent walks, XCD bands, per-half work shares, per-tile barriers, the warp-specialised kernel)
 // are in git history (tools/study/rlnc_kernels_r01_study.hip at a5d9101) with their measurements in
-// DESIGN.md §8.
+// profiles/HISTORY.md §8.
 #include <hip/hip_runtime.h>
 #include <cstdlib>
 #include <cstring>
@@ -551,7 +551,7 @@ __device__ __forceinline__ void stream_range(uint32_t ta, uint32_t tb, uint32_t 
 #pragma unroll
     for (int j = 0; j < NOUT; j++) strow<DW>(obase, ooff[j], OOB_COL, Vec<DW>{});
     // ta < tb (callers): a do-while, so no zero-trip guard lets hipcc sink the prologue loads
-    // below the dropped stores (it did: vmcnt(9) again)
+    // below the dropped stores (it did: vmcnt(9) again, profiles/HISTORY.md §8)
     uint32_t t = ta;
 #pragma unroll 1
     do {
@@ -754,7 +754,7 @@ constexpr uint32_t EDGE_WGS = 64;
 // value read before its atomic has landed breaks that — in the 3-wave encode build of round 4 (r06z14)
 // hipcc spilled the pending return register straight after the atomic, so the spill slot held the
 // atomic's data operand (1) and every workgroup took tile G + 1 again and again: a silent hang, not a
-// fault. Here a violated order ends the kernel with a trap (a named kernel fault on the
+// fault (profiles/HISTORY.md §8). Here a violated order ends the kernel with a trap (a named kernel fault on the
 // host side) instead of spinning. next and cur are wave-uniform (SGPRs): one compare per tile.
 // Both sweeps take their second tile statically (tile b + G of workgroup b) and only the third one on
 // from the counter (2G + the counter's value), so a workgroup's first grab goes out at its first loop
@@ -775,7 +775,7 @@ __device__ __forceinline__ void sweep_guard(uint32_t next, uint32_t cur) {
 // DECDS_ENC_NT_MIN_N chunksets, `nt` (2) from there on. A plain store leaves its line dirty in the
 // XCD's L2, so a small batch's coded rows were written back by the end-of-kernel release, after its
 // last wave: write-through moves that into the launch (-12...-16 % at 1-2 chunksets, -3 % at 16,
-// r06p / r06q). From 256 chunksets on `sc1` costs +0.5 % and `nt` gains 0.5-1.5 %.
+// r06p / r06q). From 256 chunksets on `sc1` costs +0.5 % and `nt` gains 0.5-1.5 % (profiles/HISTORY.md §8).
 constexpr int STORE_SC1 = 16, STORE_NT = 2;
 // Study builds only (DECDS_PHASE_TRACE, tools/phasetrace.py): wave 0 of each workgroup stamps the
 // 100 MHz real-time counter at its phases — entry, edge pass done, first tables ready, last lookups
@@ -1056,12 +1056,12 @@ void rlnc_decode_kernel(const uint8_t *__restrict__ coded, size_t pitch, size_t 
     constexpr int DW = DECDS_DEC_DW;
     constexpr uint32_t T = TILES<DW>;
     static_assert(T % UNIT == 0, "a workgroup's tiles stay in one chunkset");
-    constexpr uint32_t phase = 0;  // aligned decode loads measured slower (+3…+5 %)
+    constexpr uint32_t phase = 0;  // aligned decode loads measured slower (+3…+5 %, profiles/HISTORY.md §8)
     // Workgroups are dealt round-robin over the 8 XCDs. Piece i's stores start i bytes past a line
     // boundary, so the line at every tile edge is written partly by each of two workgroups; when those
     // sit on different XCDs both L2s write back a partial line. Runs of R consecutive tiles go to one
     // XCD instead (block 8R·g + 8j + x -> tile 8R·g + R·x + j), global order otherwise: only every R-th
-    // tile edge crosses an L2 (-3 % decode time).
+    // tile edge crosses an L2 (-3 % decode time, profiles/HISTORY.md §8).
     uint32_t u = blockIdx.x;
     if constexpr (DEC_XCD_RUN > 1) {
         constexpr uint32_t R = DEC_XCD_RUN;
@@ -1611,7 +1611,7 @@ constexpr bool MSG_OK = DECDS_ENC_DW == 4;
 #define ENC_SWEEP(MSG, SAUX) rlnc_encode_sweep_kernel<DECDS_ENC_DW, DECDS_ENC_WAVES, MSG, (DECDS_ENC_QUEUE != 0), false, SAUX>
 // small batches (DECDS_ENC_SMALL_MAX_N): 8-column lane blocks, 512 tiles per chunkset, 4 waves per SIMD
 // (118 VGPRs) — one chunkset fills 512 workgroups (16-column tiles give 256 at n = 1); slower per byte
-// from 4 chunksets on, where the 16-column form fills the grid too (r06c / r06j): threshold 2
+// from 4 chunksets on, where the 16-column form fills the grid too (r06c / r06j, profiles/HISTORY.md §8): threshold 2
 #ifndef DECDS_ENC_SMALL_WAVES
 #define DECDS_ENC_SMALL_WAVES 4
 #endif

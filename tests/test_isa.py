@@ -204,8 +204,8 @@ def test_table_kernels_have_no_static_lds(tmp_path, which):
 @pytest.mark.parametrize("which", LIBS)
 def test_sweeps_trap_instead_of_spinning(tmp_path, which):
     # every persistent sweep carries the guard (rlnc_kernels.hip sweep_guard): a next tile not past the
-    # current one — a counter value read before its atomic landed, the round-4 3-wave hang (DESIGN.md
-    # §8) — ends the kernel with s_trap instead of an endless loop over one tile
+    # current one — a counter value read before its atomic landed, the round-4 3-wave hang (profiles/
+    # HISTORY.md §8) — ends the kernel with s_trap instead of an endless loop over one tile
     if not os.path.exists(OBJDUMP):
         pytest.skip("llvm-objdump not in this image")
     funcs = _functions(_device_code(tmp_path, which))

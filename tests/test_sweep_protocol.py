@@ -5,7 +5,7 @@ next tile is past the end; each bumps an exit count on the way out and the last 
 for the next launch that takes the slot. Random interleavings of G workgroups check what the kernels rely
 on: every tile handed out exactly once, every next tile strictly past the current one (sweep_guard traps
 otherwise), and both counter words zero after the launch. A variant of the protocol (the counter zeroed by
-the last grab) was checked with this model before it ran on a device; its first form,
+the last grab, profiles/HISTORY.md §8 round 5) was checked with this model before it ran on a device; its first form,
 which broke the guard on the decode's exit step, fails `test_broken_exit_step_is_caught`."""
 import random
 

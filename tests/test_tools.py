@@ -29,7 +29,7 @@ def test_tool_microbenchmarks_compile():
 
 
 def test_study_builds_of_the_kernels_compile():
-    # the timing-study forms DESIGN.md §8 cites (per-workgroup phase trace, no edge pass, the pattern
+    # the timing-study forms profiles/HISTORY.md §8 cites (per-workgroup phase trace, no edge pass, the pattern
     # ceiling, the aligned-piece layouts) stay buildable
     if not os.path.exists(HIPCC) and not shutil.which("hipcc"):
         pytest.skip("hipcc not in this image")
