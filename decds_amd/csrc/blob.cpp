@@ -66,7 +66,7 @@ struct Pipe {
                    (e = hipStreamCreateWithPriority(&comp, hipStreamNonBlocking, mode == 2 ? greatest : least)) ||
                    (e = hipStreamCreateWithPriority(&d2h, hipStreamNonBlocking, least)))
             return e;
-        for (int i = 0; i < SLOTS; i++)
+        for (int i = 0; i < MAX_SLOTS; i++)
             for (hipEvent_t *ev : {&in_done[i], &k_done[i], &out_done[i]}) {
                 if ((e = hipEventCreateWithFlags(ev, hipEventDisableTiming))) return e;
                 if ((e = hipEventRecord(*ev, comp))) return e;  // every slot starts free
@@ -81,7 +81,7 @@ struct Pipe {
     }
     ~Pipe() {
         hip_tolerate(drain(), "hipStreamSynchronize (pipe teardown)");
-        for (int i = 0; i < SLOTS; i++)
+        for (int i = 0; i < MAX_SLOTS; i++)
             for (hipEvent_t ev : {in_done[i], k_done[i], out_done[i]})
                 if (ev) hip_tolerate(hipEventDestroy(ev), "hipEventDestroy");
         for (hipStream_t st : {h2d, comp, d2h})
