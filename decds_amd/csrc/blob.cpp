@@ -48,14 +48,17 @@ struct Pipe {
         // a pool is full, puts a new stream on the pool's least-used queue: with three equal-priority
         // streams created per call, whether H2D and D2H landed on one queue (copies then run one after
         // the other: blob encode 49-50 ms instead of 38 at 1 GiB, r07r) depended on how many streams the
-        // process already held. H2D and the kernels go on the high-priority pool (empty in most
-        // processes, so the two get queues of their own), D2H on the normal one: the copy directions can
-        // never share a queue, and encode/repair held 38 / 30 ms with 0-4 caller streams alive (r07u).
-        // The range is [0, -1] here: two levels. DECDS_PIPE_STREAMS=plain (all normal) | h2d (only H2D
-        // high) are study switches.
+        // process already held. The H2D stream goes on the high-priority pool (empty in most processes,
+        // so it gets a queue of its own), the kernel and D2H streams on the normal one: the two copy
+        // directions can never share a queue (encode/repair held 38 / 30 ms with 0-4 caller streams
+        // alive, r07u). The range is [0, -1] here: two levels. Round 5 raised the kernel stream as well
+        // ("h2d+comp"); that measured the same (encode 36.4-36.8 ms, repair 28.5-29.7 either way, r09e)
+        // and gave the library's kernels precedence over the caller's own work on the device, so round 6
+        // raises the H2D stream only. DECDS_PIPE_STREAMS=plain (all normal) | h2d+comp are
+        // study switches.
         static const int mode = [] {
             const char *v = std::getenv("DECDS_PIPE_STREAMS");
-            return !v ? 2 : !std::strcmp(v, "plain") ? 0 : !std::strcmp(v, "h2d") ? 1 : 2;
+            return !v ? 1 : !std::strcmp(v, "plain") ? 0 : !std::strcmp(v, "h2d+comp") ? 2 : 1;
         }();
         int least = 0, greatest = 0;
         if (mode == 0) {
@@ -265,19 +268,21 @@ void accept_rows(decds_ctx *ctx, const uint8_t *coded_host, size_t n, const uint
 // (rows 0..9 in order + the inverse of the accepted coding vectors, host_gf_invert — RepairingBlob's
 // decode_ready) go over beside them and the decode runs in its gather form. The gather of batch b+1
 // overlaps batch b's copy. The run form below (repair_range_runs) sent each run of consecutive
-// accepted rows as its own hipMemcpyAsync — about 500 per GiB, 30.9 ms at 1 GiB (r08zf) against a
-// duplex link bound of about 22 ms. DECDS_REPAIR_GATHER=0 selects the run form (A/B switch).
+// accepted rows as its own hipMemcpyAsync — about 500 per GiB, 29.6-31 ms at 1 GiB against 27.1-27.5
+// gathered (r09b / r09e), a duplex link bound of about 22 ms. DECDS_REPAIR_GATHER=0 selects the run form
+// (A/B switch).
 int repair_range_gather(decds_ctx *ctx, const uint8_t *coded_host, size_t n, const uint8_t *cand_host, size_t blob_len,
                         uint8_t *out, int32_t *status_host, size_t batch) {
     int s = decds_ctx_bind(ctx);
     if (s) return s;
     if (batch == 0) batch = 16;
     batch = std::min(batch, n);
-    // four slots: the gather of batch b needs slot b mod S free, i.e. batch b-S's D2H done; with three
-    // the host gathered while the link's H2D side sat idle behind the previous batch (DECDS_REPAIR_SLOTS)
+    // three slots (DECDS_REPAIR_SLOTS: 2-6): four or five, which let the gather of batch b start a batch
+    // earlier, measured slower at 1 GiB (29.5-30.7 ms at batch 16, 36-41 at batch 8, against 27.1-27.5
+    // with three, r09e)
     static const int S = [] {
         const char *v = std::getenv("DECDS_REPAIR_SLOTS");
-        return v ? std::max(2, std::min(MAX_SLOTS, std::atoi(v))) : 4;
+        return v ? std::max(2, std::min(MAX_SLOTS, std::atoi(v))) : 3;
     }();
     std::vector<uint8_t> sel(n * K, 0);
     accept_rows(ctx, coded_host, n, cand_host, sel.data(), status_host);

@@ -174,6 +174,7 @@ namespace {
 constexpr size_t CACHE_MIN = (size_t)64 << 20;
 std::mutex g_cache_mu;
 std::multimap<size_t, void *> g_cache;  // free blocks by size
+std::deque<void *> g_order;             // the same blocks, longest cached first
 std::map<void *, size_t> g_block;       // every block >= CACHE_MIN, live or cached -> its size
 size_t g_cached = 0;
 size_t cache_cap() {
@@ -194,6 +195,7 @@ hipError_t host_pinned_alloc(size_t n, void **out) {
             *out = it->second;
             g_cached -= it->first;
             g_cache.erase(it);
+            g_order.erase(std::find(g_order.begin(), g_order.end(), *out));
             return hipSuccess;
         }
     }
@@ -211,19 +213,39 @@ hipError_t host_pinned_alloc(size_t n, void **out) {
 
 void host_pinned_free(void *p, size_t) {
     if (!p) return;
+    std::vector<void *> evicted;
     {
         std::lock_guard<std::mutex> g(g_cache_mu);
         auto b = g_block.find(p);
         if (b != g_block.end()) {
-            if (g_cached + b->second <= cache_cap()) {
+            if (b->second <= cache_cap()) {
+                // the block just freed is the likeliest to be asked for again (the next Blob of the same
+                // size): blocks cached longest are released to make room for it (a 4 GiB Blob's 6.4 GiB
+                // store behind a 1 GiB one's 1.6 GiB was refused by the cap and page-locked anew per call:
+                // Blob::new at 4 GiB 0.66 s, r09e)
+                while (g_cached + b->second > cache_cap() && !g_order.empty()) {
+                    void *old = g_order.front();
+                    g_order.pop_front();
+                    for (auto it = g_cache.begin(); it != g_cache.end(); ++it)
+                        if (it->second == old) {
+                            g_cached -= it->first;
+                            g_cache.erase(it);
+                            break;
+                        }
+                    g_block.erase(old);
+                    evicted.push_back(old);
+                }
                 g_cache.emplace(b->second, p);
+                g_order.push_back(p);
                 g_cached += b->second;
-                return;
+                p = nullptr;
+            } else {
+                g_block.erase(b);
             }
-            g_block.erase(b);
         }
     }
-    hip_tolerate(hipHostFree(p), "hipHostFree");
+    for (void *q : evicted) hip_tolerate(hipHostFree(q), "hipHostFree");
+    if (p) hip_tolerate(hipHostFree(p), "hipHostFree");
 }
 
 size_t host_cache_trim() {
@@ -234,6 +256,7 @@ size_t host_cache_trim() {
         hip_tolerate(hipHostFree(kv.second), "hipHostFree");
     }
     g_cache.clear();
+    g_order.clear();
     g_cached = 0;
     return freed;
 }

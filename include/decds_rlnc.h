@@ -415,8 +415,10 @@ int decds_host_register(const void *ptr, size_t len);
 int decds_host_unregister(const void *ptr);
 /* page-locked host memory the host paths DMA directly (hipHostMalloc + the same registry). Blocks
  * of 64 MiB and more (the library's own, e.g. a Blob's coded store, and these) go to a cache when
- * freed — up to DECDS_PINNED_CACHE_MB (default 8192; all of them freed when the last context is destroyed) — and serve later requests of 80-100 % of
- * their size without page-locking again (~0.25 s per GiB); decds_host_cache_trim releases them and
+ * freed — up to DECDS_PINNED_CACHE_MB (default 8192; the blocks cached longest are released to make
+ * room for a newly freed one; all of them are freed when the last context is destroyed) — and serve
+ * later requests of 80-100 % of their size without page-locking again (~0.25 s per GiB);
+ * decds_host_cache_trim releases them and
  * returns the bytes released. Memory from the cache is not zeroed. */
 int decds_host_alloc(size_t len, void **out);
 int decds_host_free(void *ptr);

@@ -2,6 +2,7 @@
 an unready and a repair-failed chunkset in reused slots), registered vs staged caller memory, the
 multi-context (multi-device) shard forms, the host registry's rules, and concurrent chunkset-mirror
 callers (ChunkSet::new from rayon workers, blob.rs:256-264). Bit-exact against oracle/."""
+import os
 import threading
 
 import numpy as np
@@ -206,6 +207,35 @@ def test_pinned_block_cache_reuse_and_trim(ctx):
         assert hb.free() is True
     assert ptrs[0] == ptrs[1]
     L.decds_host_cache_trim()
+
+
+def test_pinned_block_cache_evicts_the_longest_cached_for_a_new_block():
+    # a freed block that does not fit beside the cached ones releases the longest-cached blocks instead
+    # of being refused (a 4 GiB Blob's 6.4 GiB store behind smaller ones, r09e): a process with a
+    # 256 MiB cap frees 96 MiB, then 200 MiB — the 200 MiB block is the one kept
+    import subprocess
+    import sys
+    code = """
+import ctypes, sys
+sys.path.insert(0, %r)
+from decds_amd._capi import lib, check
+import decds_amd
+ctx = decds_amd.Context(0)
+L = lib()
+a, b, c, d = (ctypes.c_void_p() for _ in range(4))
+check(L.decds_host_alloc(96 << 20, ctypes.byref(a))); check(L.decds_host_free(a))
+check(L.decds_host_alloc(200 << 20, ctypes.byref(b))); check(L.decds_host_free(b))
+check(L.decds_host_alloc(200 << 20, ctypes.byref(c)))
+assert c.value == b.value, "the newest block was not kept"
+check(L.decds_host_alloc(96 << 20, ctypes.byref(d)))  # a fresh block: a was released to make room for b
+check(L.decds_host_free(c)); check(L.decds_host_free(d))  # d does not fit beside c: c (cached first) goes
+freed = L.decds_host_cache_trim()
+assert freed == 96 << 20, freed
+print("ok")
+""" % os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120,
+                       env=dict(os.environ, DECDS_PINNED_CACHE_MB="256"))
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stderr[-2000:]
 
 
 @pytest.mark.parametrize("coalesce", ["0", "1"])
