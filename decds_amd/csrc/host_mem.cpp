@@ -369,6 +369,11 @@ void BounceRing::abandon() {
     }
 }
 
+void BounceRing::retire() {
+    for (int i = 0; i < R; i++)
+        if (!pend_dst[i]) used[i] = false;
+}
+
 BounceRing::~BounceRing() {
     abandon();
     for (int i = 0; i < R; i++) {

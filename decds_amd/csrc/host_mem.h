@@ -68,6 +68,11 @@ struct BounceRing {
     hipError_t d2h(uint8_t *hdst, const uint8_t *dsrc, size_t n, hipStream_t s);
     hipError_t flush();
     void abandon();  // after a failed call: wait for the pieces' copies, drop pending copy-outs
+    // after the streams this call's copies were queued on have been drained, before they are destroyed:
+    // every piece is free. (A piece left "used" had its event waited for by the NEXT call, after the
+    // stream the event was recorded on had been destroyed; that wait failed now and then with
+    // hipErrorCapturedEvent (907), r09f.) Pending copy-outs must have been flushed.
+    void retire();
     // h2d in two steps, so the host fill of a piece can overlap other host work: stage() settles the
     // next piece and returns it (*idx), commit() queues its copy to the device; an uncommitted piece is
     // simply reused later
