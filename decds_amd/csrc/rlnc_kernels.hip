@@ -1335,10 +1335,14 @@ __device__ __forceinline__ void wave_lds_sync() {
 // The plan of chunkset cs on one wave (lane = threadIdx.x & 63): writes *pl (rank always; sel and the
 // input-major inverse when ready) and, when status is given, status[cs]; returns lane a's verdict for
 // candidate a (< 16). WAVE_SYNC: the caller's other waves do not take part (wave-level LDS syncs).
-template <bool WAVE_SYNC>
+struct NoHook {
+    __device__ __forceinline__ void operator()() const {}
+};
+template <bool WAVE_SYNC, class AfterLoads = NoHook>
 __device__ __forceinline__ int32_t plan_wave(const uint8_t *__restrict__ coded, size_t pitch, size_t cs,
                                              const uint8_t *__restrict__ cand, PlanLds &sl, const GfExpTable &tab,
-                                             RepairPlan *pl, int32_t *__restrict__ status) {
+                                             RepairPlan *pl, int32_t *__restrict__ status,
+                                             AfterLoads after_loads = AfterLoads()) {
     const uint32_t lane = threadIdx.x & 63u;
     const bool col = lane < K;
     // the arrival order and the coding vector of every coded row of the chunkset (lane c < 10
@@ -1347,6 +1351,7 @@ __device__ __forceinline__ int32_t plan_wave(const uint8_t *__restrict__ coded, 
     uint32_t rowcv[N];
 #pragma unroll
     for (int r = 0; r < (int)N; r++) rowcv[r] = col ? coded[(cs * N + r) * pitch + lane] : 0u;
+    after_loads();  // (the fused kernel issues its speculative tile loads here, behind the plan's own)
     uint8_t *s_exp = sl.exp;
     uint16_t *s_log = sl.log, *s_lcv = sl.lcv;
     {
@@ -1492,8 +1497,7 @@ void rlnc_plan_decode_kernel(const uint8_t *__restrict__ coded, size_t pitch, si
     TailLds &s_tail = *reinterpret_cast<TailLds *>(lds + LDS_BYTES);
     PlanLds &s_plan = *reinterpret_cast<PlanLds *>(lds + LDS_BYTES + TAIL_LDS);
     RepairPlan &s_rp = *reinterpret_cast<RepairPlan *>(lds + LDS_BYTES + TAIL_LDS + sizeof(PlanLds));
-    constexpr int DW = DECDS_DEC_DW;
-    constexpr uint32_t T = TILES<DW>;
+    constexpr uint32_t T = TILES<DECDS_DEC_DW>;
     constexpr uint32_t phase = 0;
     uint32_t u = blockIdx.x;
     if constexpr (DEC_XCD_RUN > 1) {  // runs of consecutive tiles per XCD, as rlnc_decode_kernel
@@ -1503,9 +1507,34 @@ void rlnc_plan_decode_kernel(const uint8_t *__restrict__ coded, size_t pitch, si
     const uint32_t cs = u / T, tile0 = u % T;
     if (cs >= n) return;
     const bool first = tile0 == 0;
+    const uint8_t *ibase = coded + (size_t)cs * N * pitch;
+    // Speculative first loads: the first ten candidates in arrival order are the accepted rows in the
+    // common case (exactly ten survivors, or the first ten of more: independent with probability 0.996),
+    // so every wave issues its tile's loads from those rows before (wave 0: behind the plan's own loads)
+    // the plan is known; a plan that accepted other rows reloads below.
+    const uint32_t *cw = reinterpret_cast<const uint32_t *>(cand + (size_t)cs * N);
+    const uint32_t c0 = __builtin_amdgcn_readfirstlane(cw[0]), c1 = __builtin_amdgcn_readfirstlane(cw[1]),
+                   c2 = __builtin_amdgcn_readfirstlane(cw[2]) & 0xFFFFu;
+    const uint32_t spec_sel[K] = {c0 & 0xFFu, (c0 >> 8) & 0xFFu, (c0 >> 16) & 0xFFu, c0 >> 24,
+                                  c1 & 0xFFu, (c1 >> 8) & 0xFFu, (c1 >> 16) & 0xFFu, c1 >> 24,
+                                  c2 & 0xFFu, c2 >> 8};
+    bool spec_ok = true;
+#pragma unroll
+    for (int k = 0; k < (int)K; k++) spec_ok &= spec_sel[k] < N;
+    uint32_t soff[K];
+#pragma unroll
+    for (int k = 0; k < (int)K; k++) soff[k] = (uint32_t)((spec_sel[k] & 15u) * pitch + K);
+    constexpr int DW = DECDS_DEC_DW;
+    Vec<DW> x[K];
+    const uint32_t col0 = tile_col<DW, false>(tile0, tile0 + 1, 0);
+    auto speculate = [&]() {
+        if (spec_ok) load_block<K, DW>(x, ibase, soff, col0);
+    };
     if (threadIdx.x < 64) {
-        const int32_t v = plan_wave<true>(coded, pitch, cs, cand, s_plan, tab, &s_rp, first ? status : nullptr);
+        const int32_t v = plan_wave<true>(coded, pitch, cs, cand, s_plan, tab, &s_rp, first ? status : nullptr, speculate);
         if (first && threadIdx.x < N) verdicts[(size_t)cs * N + threadIdx.x] = (int8_t)v;
+    } else {
+        speculate();
     }
     if (first) tail_reset(s_tail);
     lds_barrier();
@@ -1524,14 +1553,12 @@ void rlnc_plan_decode_kernel(const uint8_t *__restrict__ coded, size_t pitch, si
     for (int k = 0; k < (int)K; k++) ioff[k] = (uint32_t)(sel[k] * pitch + K);
 #pragma unroll
     for (int i = 0; i < (int)K; i++) ooff[i] = piece_off(i);
-    const uint8_t *ibase = coded + (size_t)cs * N * pitch;
     uint8_t *obase = dst + (size_t)cs * CS;
-    const uint32_t cw = table_coeffs_imaj_lds<K, K>(s_rp.inv);
-    Vec<DW> x[K];
-    if constexpr (DECDS_PREFETCH_FIRST) load_block<K, DW>(x, ibase, ioff, tile_col<DW, false>(tile0, tile0 + 1, phase));
-    build_tables<K, K>(lds, cw, poly);
+    const uint32_t tcw = table_coeffs_imaj_lds<K, K>(s_rp.inv);
+    if (!spec_ok || w0 != c0 || w1 != c1 || (w2 & 0xFFFFu) != c2) load_block<K, DW>(x, ibase, ioff, col0);  // misspeculated
+    build_tables<K, K>(lds, tcw, poly);
     lds_barrier();
-    stream_range<K, K, DW, DECDS_PREFETCH_FIRST, false, DECDS_DEC_HB, SAUX>(tile0, tile0 + 1, phase, ibase, ioff, obase, ooff, x);
+    stream_range<K, K, DW, true, false, DECDS_DEC_HB, SAUX>(tile0, tile0 + 1, phase, ibase, ioff, obase, ooff, x);
     if (first) {
         // the edge columns and get_decoded_data's cut, as rlnc_decode_kernel's edge pass
         for (uint32_t idx = threadIdx.x; idx < edge_cols<DW, false>(phase) * K; idx += WG) {
@@ -1851,7 +1878,8 @@ hipError_t launch_repair(const LaunchGeom &geom, const uint8_t *coded, size_t pi
                          uint8_t *plan, int8_t *verdicts, uint8_t *dst, int32_t *status, uint32_t poly, uint32_t gen,
                          uint32_t marker, uint8_t *info, hipStream_t stream) {
     if (n == 0) return hipSuccess;
-    if (!plan_decode_fused(n)) {
+    // the fused kernel reads each chunkset's first ten candidates as three dwords: 4-byte aligned lists only
+    if (!plan_decode_fused(n) || (reinterpret_cast<uintptr_t>(cand) & 3u)) {
         if (hipError_t e = launch_repair_plan(coded, pitch, n, cand, plan, verdicts, status, poly, gen, stream)) return e;
         return launch_decode(geom, coded, pitch, n, plan, dst, status, nullptr, nullptr, poly, marker, info, stream);
     }
