@@ -356,12 +356,20 @@ int repair_range_gather(decds_ctx *ctx, const uint8_t *coded_host, size_t n, con
         pending_b0[k] = (size_t)-1;
         return DECDS_OK;
     };
+    // Per batch b in slot k = b mod S, the host waits for as little as it can, as late as it can:
+    // before gathering into the staging buffer only for batch b-S's H2D (long done), and only after
+    // batch b's H2D and decode are queued for batch b-S's D2H (to post-process its statuses) — so the
+    // link's H2D side always has the next batch queued. Device buffers are ordered on the device:
+    // batch b's H2D after batch b-S's decode (k_done), its decode after batch b-S's D2H (out_done).
     const std::vector<size_t> sizes = batch_sizes(n, batch, true);
+    std::vector<size_t> rl;
     for (size_t b0 = 0, it = 0; it < sizes.size() && rc == DECDS_OK; b0 += sizes[it], it++) {
         const int k = (int)(it % S);
-        if ((rc = finish(k))) break;  // slot k's previous batch fully done: all its buffers are free
         const size_t nb = sizes[it];
-        std::vector<size_t> &rl = ready[k];
+        if ((e = hipEventSynchronize(pp.in_done[k]))) {  // the staging buffer and plans of batch b-S sent
+            rc = decds_hip_error(e, "hipEventSynchronize");
+            break;
+        }
         rl.clear();
         for (size_t c = 0; c < nb; c++)
             if (status_host[b0 + c] == DECDS_OK) rl.push_back(c);
@@ -385,15 +393,17 @@ int repair_range_gather(decds_ctx *ctx, const uint8_t *coded_host, size_t n, con
             outb[i] = reinterpret_cast<uint64_t>(ddst[k] + rl[i] * CS);
         }
         if (rc) break;
-        // the gather: one 1 MiB row per job on the host pool, overlapping the previous batch's copies
+        // the gather: one 1 MiB row per job on the host pool, overlapping the previous batches' copies
         host_parallel(m * K, [&](size_t j) {
             const size_t i = j / K, a = j % K, c = b0 + rl[i];
             std::memcpy(hstage[k] + (i * K + a) * F, coded_host + (c * N + sel[c * K + a]) * F, F);
         });
-        if ((m && (e = hipMemcpyAsync(dstage[k], hstage[k], m * K * F, hipMemcpyHostToDevice, pp.h2d))) ||
+        if ((e = hipStreamWaitEvent(pp.h2d, pp.k_done[k], 0)) ||  // batch b-S's decode has read dstage[k]
+            (m && (e = hipMemcpyAsync(dstage[k], hstage[k], m * K * F, hipMemcpyHostToDevice, pp.h2d))) ||
             (e = hipMemcpyAsync(dsmall[k], hsmall[k], sm_h2d, hipMemcpyHostToDevice, pp.h2d)) ||
-            (e = hipMemsetAsync(dsmall[k] + sm_stat, 0, align256(batch * 4), pp.h2d)) ||
-            (e = hipEventRecord(pp.in_done[k], pp.h2d)) || (e = hipStreamWaitEvent(pp.comp, pp.in_done[k], 0))) {
+            (e = hipEventRecord(pp.in_done[k], pp.h2d)) || (e = hipStreamWaitEvent(pp.comp, pp.in_done[k], 0)) ||
+            (e = hipStreamWaitEvent(pp.comp, pp.out_done[k], 0)) ||  // batch b-S's D2H has read ddst[k], its statuses
+            (e = hipMemsetAsync(dsmall[k] + sm_stat, 0, align256(batch * 4), pp.comp))) {
             rc = decds_hip_error(e, "H2D");
             break;
         }
@@ -405,7 +415,14 @@ int repair_range_gather(decds_ctx *ctx, const uint8_t *coded_host, size_t n, con
             rc = decds_hip_error(e, "rlnc decode launch");
             break;
         }
-        if ((e = hipEventRecord(pp.k_done[k], pp.comp)) || (e = hipStreamWaitEvent(pp.d2h, pp.k_done[k], 0)) ||
+        if ((e = hipEventRecord(pp.k_done[k], pp.comp))) {
+            rc = decds_hip_error(e, "hipEventRecord");
+            break;
+        }
+        // batch b-S's statuses are read before batch b's D2H overwrites them
+        if ((rc = finish(k))) break;
+        ready[k] = rl;
+        if ((e = hipStreamWaitEvent(pp.d2h, pp.k_done[k], 0)) ||
             (m && (e = hipMemcpyAsync(hsmall[k] + sm_stat, dsmall[k] + sm_stat, sm_bytes - sm_stat, hipMemcpyDeviceToHost,
                                       pp.d2h)))) {
             rc = decds_hip_error(e, "D2H");
