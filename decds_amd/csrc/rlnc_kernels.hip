@@ -1681,7 +1681,11 @@ hipError_t configure_kernels() {
 #define DECDS_ENC_NT_MIN_N 256
 #endif
 #ifndef DECDS_PLAN_DECODE_MAX_N
-#define DECDS_PLAN_DECODE_MAX_N 16  // decds_repair_batch: plan + decode as one launch up to this many chunksets
+// decds_repair_batch: plan + decode as one launch up to this many chunksets. Every workgroup of the fused
+// kernel runs its chunkset's plan first (+6 us of one wave): a win while the grid is one round of resident
+// workgroups (256 per chunkset, 4 per CU: 4 chunksets) — 19.7 against 25.6 us at 1 chunkset between
+// events — and a loss past it (111 against 95 us at 16, r09f)
+#define DECDS_PLAN_DECODE_MAX_N 4
 #endif
 // Launch-shape thresholds (process-wide): the environment variable of the same name read once (at
 // first use), else the build's default; decds_set_tuning changes one for the process (tests force

@@ -342,7 +342,7 @@ def test_fused_repair_plans_match_oracle_on_the_fuzz(ctx, plan_decode_fused):
 
 @pytest.mark.parametrize("n", [1, 2, 5, 16])
 def test_fused_repair_equals_plan_then_decode(ctx, n):
-    """decds_repair_batch at n <= 16 (one launch, rlnc_plan_decode_kernel) against the plan kernel then
+    """decds_repair_batch in one launch (rlnc_plan_decode_kernel, forced at every n) against the plan kernel then
     the decode (the form above the threshold): plan bytes, verdicts, statuses, repair infos and every
     repaired byte identical, and the repaired chunksets equal their sources. Candidates: shuffled full
     lists, exactly 10, 9 (not ready), a repeated id, and a dependent row among the first 10."""
