@@ -82,7 +82,7 @@ def decode_batch(ctx, coded, n, plan, dst, status, pitch=CODED_PIECE_BYTES, stre
 
 def repair_batch(ctx, coded, n, cand, plan, verdicts, dst, status, pitch=CODED_PIECE_BYTES, stream=None, info=None):
     """decds_repair_batch: repair_plan_batch + decode_batch in one call — up to DECDS_PLAN_DECODE_MAX_N
-    chunksets (default 4) one kernel launch (rlnc_plan_decode_kernel), the same outputs either way"""
+    chunksets (default 2) one kernel launch (rlnc_plan_decode_kernel), the same outputs either way"""
     _need(coded, (n * N - 1) * pitch + CODED_PIECE_BYTES, "coded")
     _need(cand, n * N, "cand")
     _need(plan, n * REPAIR_PLAN_BYTES, "plan")

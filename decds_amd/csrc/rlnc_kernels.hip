@@ -1682,10 +1682,11 @@ hipError_t configure_kernels() {
 #endif
 #ifndef DECDS_PLAN_DECODE_MAX_N
 // decds_repair_batch: plan + decode as one launch up to this many chunksets. Every workgroup of the fused
-// kernel runs its chunkset's plan first (+6 us of one wave): a win while the grid is one round of resident
-// workgroups (256 per chunkset, 4 per CU: 4 chunksets) — 19.7 against 25.6 us at 1 chunkset between
-// events — and a loss past it (111 against 95 us at 16, r09f)
-#define DECDS_PLAN_DECODE_MAX_N 4
+// kernel runs its chunkset's plan first (~6 us of one wave). Against the plan kernel and the decode back
+// to back on one stream (no event between them, as decds_repair_batch launches them) it saves the second
+// launch: 17.6 / 20.2 against 18.2 / 21.0 us at 1 / 2 chunksets; from 4 on the redundant plans cost more
+// than that (30.9 against 29.7 us at 4, 54.9 against 44.7 at 8; r09h, tools/kbench.py --repair)
+#define DECDS_PLAN_DECODE_MAX_N 2
 #endif
 // Launch-shape thresholds (process-wide): the environment variable of the same name read once (at
 // first use), else the build's default; decds_set_tuning changes one for the process (tests force
