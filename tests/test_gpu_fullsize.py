@@ -1,7 +1,8 @@
 """BASELINE config 3/4 at full size on one GPU: a 16 GiB blob (1639 chunksets, the last one holding
 4 MiB of data) encoded in one batch, repaired from exactly 10 random survivors per chunkset, and
 committed (separately and fused into the encode) + validated (rows f1, f2). Every coded row of the
-1639-chunkset launches is compared byte for byte with the oracle's (tests/fullcheck.py); the other
+1639-chunkset launches is compared byte for byte with the oracle's, and every chunk digest with the
+BLAKE3 restatement's digest of the oracle's row (tests/fullcheck.py); the other
 checks are size-independent properties (decode∘encode = id, rank-deficient sets reported
 not-ready exactly where the oracle's rank test says so, every row's proof verifies, a flipped byte
 does not)."""
@@ -13,7 +14,7 @@ torch = pytest.importorskip("torch")
 from decds_amd import codec  # noqa: E402
 from decds_amd._capi import CHUNKSET_BYTES as CS, CODED_PIECE_BYTES as F, K, N  # noqa: E402
 import oracle as o  # noqa: E402
-from fullcheck import compare_device_rows  # noqa: E402
+from fullcheck import compare_device_rows, shard_oracle_digests  # noqa: E402
 
 pytestmark = pytest.mark.gpu
 
@@ -87,6 +88,11 @@ def test_cfg3_16gib_encode_repair_commit_validate(ctx):
     for row in (0, 1, 13107, n * N - 1):
         piece = coded[row * F:(row + 1) * F].cpu().numpy()
         assert d[row * 32:(row + 1) * 32].tobytes() == o.chunk_digest(row // N, row, piece), row
+    # every row's digest (chunk.rs:40-46; the fused and unfused paths gave the same, above) against the
+    # BLAKE3 restatement's digest of the oracle's own coded row
+    ref = shard_oracle_digests(0, n, 0xDEC05003, 0xC0EF0003, blob_len)
+    bad = np.nonzero((d.reshape(n * N, 32) != ref).any(axis=1))[0]
+    assert bad.size == 0, "digests differ from the oracle's: rows %s" % bad[:16].tolist()
     leaves = [d[((n - 1) * N + j) * 32:((n - 1) * N + j + 1) * 32].tobytes() for j in range(N)]
     r = roots.cpu().numpy()
     assert r[(n - 1) * 32:n * 32].tobytes() == o.merkle(leaves)[0]
