@@ -392,11 +392,13 @@ hipError_t copy_h2d(uint8_t *d, const uint8_t *h, size_t n, bool pinned, BounceR
 // host memory (hipHostMalloc coherent or not, hipHostRegister'd), one of 16 MiB at 54 GB/s, and a
 // kernel storing straight into the host buffer at 55 GB/s (tools/d2hbench.hip, r07j); a trace of the
 // blob encode showed the large copy executed as 8 MiB blit kernels with gaps as long as the kernels
-// between them (r07b). DECDS_D2H_PIECE_MB overrides the piece (0: one copy, round 4's behaviour).
+// between them (r07b). Pieces of 64 MiB (round 6): blob encode −1 % at 1 GiB and −3 % at 2 GiB against
+// 16 MiB, repair unchanged (three interleaved pairs each, r09k). DECDS_D2H_PIECE_MB overrides the piece
+// (0: one copy, round 4's behaviour).
 static size_t d2h_piece() {
     static const size_t piece = [] {
         const char *v = std::getenv("DECDS_D2H_PIECE_MB");
-        return v && *v ? (size_t)std::strtoull(v, nullptr, 10) << 20 : (size_t)16 << 20;
+        return v && *v ? (size_t)std::strtoull(v, nullptr, 10) << 20 : (size_t)64 << 20;
     }();
     return piece;
 }

@@ -1335,9 +1335,6 @@ __device__ __forceinline__ void wave_lds_sync() {
 // The plan of chunkset cs on one wave (lane = threadIdx.x & 63): writes *pl (rank always; sel and the
 // input-major inverse when ready) and, when status is given, status[cs]; returns lane a's verdict for
 // candidate a (< 16). WAVE_SYNC: the caller's other waves do not take part (wave-level LDS syncs).
-#ifndef DECDS_PLAN_BCAST
-#define DECDS_PLAN_BCAST 1  // plan reduction factors by broadcast LDS reads (0: v_readlane, round 5's form)
-#endif
 struct NoHook {
     __device__ __forceinline__ void operator()() const {}
 };
@@ -1402,15 +1399,8 @@ __device__ __forceinline__ int32_t plan_wave(const uint8_t *__restrict__ coded, 
             // augmented row [cv | unit(k)] minus its projection on the basis: the factor of basis row
             // e is the row's entry at pivot e
             uint32_t row = col ? (uint32_t)s_exp[lcv] : (lane == K + k ? 1u : 0u);
-#if DECDS_PLAN_BCAST
-            // the factors' logs straight from LDS at a wave-uniform address (a broadcast read, issued
-            // with the row's own read) instead of v_readlane of the row's logs after that read landed
-#pragma unroll
-            for (int e = 0; e < k; e++) row ^= s_exp[lgb[e] + (uint32_t)s_lcv[r * 16 + piv[e]]];
-#else
 #pragma unroll
             for (int e = 0; e < k; e++) row ^= s_exp[lgb[e] + __builtin_amdgcn_readlane(lcv, piv[e])];
-#endif
             const uint64_t nz = __ballot(col && row != 0);
             if (!nz) {
                 if (lane == a) my_verdict = 4;  // DECDS_ERR_CHUNK_DECODING_FAILED: piece not useful
