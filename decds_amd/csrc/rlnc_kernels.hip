@@ -1335,6 +1335,9 @@ __device__ __forceinline__ void wave_lds_sync() {
 // The plan of chunkset cs on one wave (lane = threadIdx.x & 63): writes *pl (rank always; sel and the
 // input-major inverse when ready) and, when status is given, status[cs]; returns lane a's verdict for
 // candidate a (< 16). WAVE_SYNC: the caller's other waves do not take part (wave-level LDS syncs).
+#ifndef DECDS_STUDY_PLAN
+#define DECDS_STUDY_PLAN 0  // timing studies of the plan (1: no elimination, 2: no coding-vector loads)
+#endif
 struct NoHook {
     __device__ __forceinline__ void operator()() const {}
 };
@@ -1350,7 +1353,11 @@ __device__ __forceinline__ int32_t plan_wave(const uint8_t *__restrict__ coded, 
     const uint32_t my_cand = lane < N ? cand[cs * N + lane] : (uint32_t)DECDS_NO_CANDIDATE_U8;
     uint32_t rowcv[N];
 #pragma unroll
+#if DECDS_STUDY_PLAN == 2  // timing study: no coding-vector loads (a fixed full-rank pattern instead)
+    for (int r = 0; r < (int)N; r++) rowcv[r] = col ? ((uint32_t)(r * 37 + lane * 11 + cs) & 0xFFu) | 1u : 0u;
+#else
     for (int r = 0; r < (int)N; r++) rowcv[r] = col ? coded[(cs * N + r) * pitch + lane] : 0u;
+#endif
     after_loads();  // (the fused kernel issues its speculative tile loads here, behind the plan's own)
     uint8_t *s_exp = sl.exp;
     uint16_t *s_log = sl.log, *s_lcv = sl.lcv;
@@ -1376,6 +1383,11 @@ __device__ __forceinline__ int32_t plan_wave(const uint8_t *__restrict__ coded, 
         for (int r = 0; r < (int)N; r++) s_lcv[r * 16 + lane] = s_log[rowcv[r]];
     }
     if constexpr (WAVE_SYNC) wave_lds_sync(); else __syncthreads();
+#if DECDS_STUDY_PLAN == 1  // timing study: loads and tables only, no elimination
+    if (lane == 0) pl->rank = (uint8_t)(s_lcv[lane] & 1u);
+    if (lane == 0 && status) status[cs] = 5;
+    return -1;
+#endif
     // Basis slot k is filled by the k-th accepted candidate, so the slot loop is unrolled with k a
     // constant: step k reduces against k basis rows only, and the pivots stay in SGPRs. Candidates
     // are taken in arrival order by a uniform inner loop until one raises the rank.
