@@ -33,11 +33,17 @@
 using namespace decds;
 
 namespace {
-
 constexpr int SLOTS = 3;      // buffer slots of the encode pipeline and of the repair run form
 constexpr int MAX_SLOTS = 6;  // events a Pipe holds (the gather form's slot count is tunable)
 inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+}  // namespace
 
+namespace decds {
+// The host paths' three streams and per-slot events, one set per context (ctx->pipe): created by the
+// context's first host-path call and kept (creating three streams and 18 events per call cost every
+// call their set-up, and an event of a ring piece could outlive the stream it was recorded on).
+// Calls on one context are serialised by ctx->host_mu; each ends with every stream drained, so the
+// next call finds every slot event complete (every slot free).
 struct Pipe {
     hipStream_t h2d = nullptr, comp = nullptr, d2h = nullptr;
     hipEvent_t in_done[MAX_SLOTS] = {}, k_done[MAX_SLOTS] = {}, out_done[MAX_SLOTS] = {};
@@ -91,6 +97,24 @@ struct Pipe {
             if (st) hip_tolerate(hipStreamDestroy(st), "hipStreamDestroy");
     }
 };
+
+void pipe_destroy(Pipe *p) { delete p; }
+}  // namespace decds
+
+namespace {
+// the context's pipe, created on first use (caller holds ctx->host_mu)
+hipError_t ctx_pipe(decds_ctx *ctx, Pipe **out) {
+    if (!ctx->pipe) {
+        auto *p = new Pipe;
+        if (hipError_t e = p->init()) {
+            delete p;
+            return e;
+        }
+        ctx->pipe = p;
+    }
+    *out = ctx->pipe;
+    return hipSuccess;
+}
 
 // commitment outputs of the encode pipeline (Blob::new: chunkset.rs:54-63 per chunkset)
 struct CommitOut {
@@ -193,8 +217,9 @@ int encode_range(decds_ctx *ctx, const uint8_t *blob, size_t blob_len, const uin
         uint8_t **dst[5] = {&din[i], &dout[i], &ddig[i], &drt[i], &dprf[i]};
         for (int j = 0; j < 5; j++) *dst[j] = base, base += sz[j];
     }
-    Pipe pp;
-    if ((e = pp.init())) return decds_hip_error(e, "stream/event setup");
+    Pipe *ppp;
+    if ((e = ctx_pipe(ctx, &ppp))) return decds_hip_error(e, "stream/event setup");
+    Pipe &pp = *ppp;
     if ((e = copy_h2d(dcv, coeffs, n * N * K, ucv.pinned(), ctx->in_ring, pp.h2d)))
         return finish_call(ctx, pp, decds_hip_error(e, "H2D"));
     auto issue_d2h = [&](int k, size_t b0, size_t nb) -> int {
@@ -328,8 +353,9 @@ int repair_range_gather(decds_ctx *ctx, const uint8_t *coded_host, size_t n, con
         dsmall[i] = base + stage;
         ddst[i] = base + stage + sm_bytes;
     }
-    Pipe pp;
-    if ((e = pp.init())) return decds_hip_error(e, "stream/event setup");
+    Pipe *ppp;
+    if ((e = ctx_pipe(ctx, &ppp))) return decds_hip_error(e, "stream/event setup");
+    Pipe &pp = *ppp;
     int rc = DECDS_OK;
     size_t pending_b0[MAX_SLOTS];
     std::vector<size_t> ready[MAX_SLOTS];  // batch positions of the slot's decoded chunksets
@@ -503,8 +529,9 @@ int repair_range_runs(decds_ctx *ctx, const uint8_t *coded_host, size_t n, const
         uint8_t **dst[7] = {&dcoded[i], &dcand[i], &dplan[i], &dverd[i], &dstat[i], &ddst[i], &dinfo[i]};
         for (int j = 0; j < 7; j++) *dst[j] = base, base += sz[j];
     }
-    Pipe pp;
-    if ((e = pp.init())) return decds_hip_error(e, "stream/event setup");
+    Pipe *ppp;
+    if ((e = ctx_pipe(ctx, &ppp))) return decds_hip_error(e, "stream/event setup");
+    Pipe &pp = *ppp;
     int rc = DECDS_OK;
     size_t pending_b0[SLOTS], pending_nb[SLOTS] = {};
     for (int i = 0; i < SLOTS; i++) pending_b0[i] = (size_t)-1;

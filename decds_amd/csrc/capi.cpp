@@ -169,6 +169,7 @@ int decds_ctx_destroy(decds_ctx *ctx) {
     if (!ctx) return DECDS_OK;
     hip_tolerate(hipSetDevice(ctx->device), "hipSetDevice");
     decds_lanes_destroy(ctx);
+    if (ctx->pipe) decds::pipe_destroy(ctx->pipe);  // drains its streams first
     if (ctx->host_scratch) hip_tolerate(hipFree(ctx->host_scratch), "hipFree");
     // the last context out returns the cached page-locked blocks (no idle pinned memory)
     if (g_live_ctx.fetch_sub(1) == 1) (void)host_cache_trim();

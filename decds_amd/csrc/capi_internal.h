@@ -14,6 +14,8 @@
 namespace decds {
 struct Lane;       // chunkset.cpp: the buffers and stream of one in-flight chunkset-mirror call
 struct Coalescer;  // chunkset.cpp: concurrent ChunkSet::new calls gathered into shared launches
+struct Pipe;       // blob.cpp: the host paths' H2D / kernel / D2H streams and slot events
+void pipe_destroy(Pipe *p);
 }
 
 struct decds_ctx {
@@ -29,6 +31,7 @@ struct decds_ctx {
     uint8_t *host_scratch = nullptr;
     size_t host_scratch_cap = 0;
     decds::BounceRing in_ring, out_ring;
+    decds::Pipe *pipe = nullptr;  // created by the first host-path call, kept for the context's life
     // chunkset mirror (decds_chunkset_new, decds_repairing_chunkset_repair): a pool of lanes, one
     // per concurrent caller (the reference calls ChunkSet::new from rayon workers, blob.rs:256-264)
     std::mutex lane_mu;
