@@ -183,25 +183,18 @@ int encode_range(decds_ctx *ctx, const uint8_t *blob, size_t blob_len, const uin
     batch = std::min(batch, n);
     const size_t PRF = N * PROOF_SIZE * 32;
     HostUse uin(blob, blob_len), ucv(coeffs, n * N * K), uout(coded, n * N * F);
-    // the commitment outputs (roots, proofs: 2,080 bytes per chunkset) land in one page-locked area
-    // of the call and are copied to the caller's memory at the end: staged through the out ring, two
-    // small copies per batch held ring pieces, and the host thread waited on them while the direct
+    std::lock_guard<std::mutex> lock(ctx->host_mu);
+    // the commitment outputs (roots, proofs: 2,080 bytes per chunkset) land in the context's small
+    // page-locked area and are copied to the caller's memory at the end: staged through the out ring,
+    // two small copies per batch held ring pieces, and the host thread waited on them while the direct
     // input copies of a page-locked blob could have run ahead (Blob::new of a page-locked 1 GiB blob
     // 69 ms against 41 from pageable memory, r09c)
-    struct PinnedCm {
-        void *p = nullptr;
-        ~PinnedCm() {
-            if (p) hip_tolerate(hipHostFree(p), "hipHostFree");
-        }
-    } cmh;
     uint8_t *h_roots = nullptr, *h_prf = nullptr;
     if (cm) {
-        hipError_t pe = hipHostMalloc(&cmh.p, n * (32 + PRF), DECDS_HOST_MALLOC_FLAGS);
+        hipError_t pe = decds_ctx_host_small(ctx, n * (32 + PRF), &h_roots);
         if (pe) return decds_hip_error(pe, "hipHostMalloc (commitment outputs)");
-        h_roots = static_cast<uint8_t *>(cmh.p);
         h_prf = h_roots + n * 32;
     }
-    std::lock_guard<std::mutex> lock(ctx->host_mu);
     // the coding vectors of the whole range go over in one copy ahead of the first batch (160 bytes
     // per chunkset): staged per batch from pageable memory, each small copy held a ring piece and
     // stalled the host's run-ahead (blob encode 15-17 GiB/s against 29 with them registered, r02zd)
@@ -328,23 +321,18 @@ int repair_range_gather(decds_ctx *ctx, const uint8_t *coded_host, size_t n, con
             if (p) host_pinned_free(p, n);
         }
     } hst;
-    struct PinnedSmall {
-        void *p = nullptr;
-        ~PinnedSmall() {
-            if (p) hip_tolerate(hipHostFree(p), "hipHostFree");
-        }
-    } hsm;
     hipError_t e;
     if ((e = host_pinned_alloc(S * stage, &hst.p))) return decds_hip_error(e, "page-locked staging for accepted rows");
     hst.n = S * stage;
-    if ((e = hipHostMalloc(&hsm.p, S * sm_bytes, DECDS_HOST_MALLOC_FLAGS))) return decds_hip_error(e, "hipHostMalloc");
+    HostUse uout(out, blob_len);
+    std::lock_guard<std::mutex> lock(ctx->host_mu);
+    uint8_t *hsm;
+    if ((e = decds_ctx_host_small(ctx, S * sm_bytes, &hsm))) return decds_hip_error(e, "hipHostMalloc");
     uint8_t *hstage[MAX_SLOTS], *hsmall[MAX_SLOTS];
     for (int i = 0; i < S; i++) {
         hstage[i] = static_cast<uint8_t *>(hst.p) + i * stage;
-        hsmall[i] = static_cast<uint8_t *>(hsm.p) + i * sm_bytes;
+        hsmall[i] = hsm + i * sm_bytes;
     }
-    HostUse uout(out, blob_len);
-    std::lock_guard<std::mutex> lock(ctx->host_mu);
     const size_t dsz = stage + sm_bytes + align256(batch * CS);
     uint8_t *base, *dstage[MAX_SLOTS], *dsmall[MAX_SLOTS], *ddst[MAX_SLOTS];
     if ((e = decds_ctx_scratch(ctx, S * dsz, &base))) return decds_hip_error(e, "hipMalloc");

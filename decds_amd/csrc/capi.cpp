@@ -82,6 +82,22 @@ hipError_t decds_ctx_scratch(decds_ctx *ctx, size_t bytes, uint8_t **out) {
     return hipSuccess;
 }
 
+hipError_t decds_ctx_host_small(decds_ctx *ctx, size_t bytes, uint8_t **out) {
+    if (ctx->host_small_cap < bytes) {
+        if (ctx->host_small) hip_tolerate(hipHostFree(ctx->host_small), "hipHostFree");
+        ctx->host_small = nullptr;
+        ctx->host_small_cap = 0;
+        hipError_t e = hipHostMalloc(reinterpret_cast<void **>(&ctx->host_small), bytes, DECDS_HOST_MALLOC_FLAGS);
+        if (e) {
+            (void)hipGetLastError();  // this call's own error, returned
+            return e;
+        }
+        ctx->host_small_cap = bytes;
+    }
+    *out = ctx->host_small;
+    return hipSuccess;
+}
+
 extern "C" {
 
 const char *decds_last_error(void) { return g_last_error.c_str(); }
@@ -171,6 +187,7 @@ int decds_ctx_destroy(decds_ctx *ctx) {
     decds_lanes_destroy(ctx);
     if (ctx->pipe) decds::pipe_destroy(ctx->pipe);  // drains its streams first
     if (ctx->host_scratch) hip_tolerate(hipFree(ctx->host_scratch), "hipFree");
+    if (ctx->host_small) hip_tolerate(hipHostFree(ctx->host_small), "hipHostFree");
     // the last context out returns the cached page-locked blocks (no idle pinned memory)
     if (g_live_ctx.fetch_sub(1) == 1) (void)host_cache_trim();
     if (ctx->geom.counters) {

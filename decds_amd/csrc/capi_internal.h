@@ -30,6 +30,8 @@ struct decds_ctx {
     std::mutex host_mu;
     uint8_t *host_scratch = nullptr;
     size_t host_scratch_cap = 0;
+    uint8_t *host_small = nullptr;  // page-locked, grow-only: plans, statuses, commitment outputs of a call
+    size_t host_small_cap = 0;
     decds::BounceRing in_ring, out_ring;
     decds::Pipe *pipe = nullptr;  // created by the first host-path call, kept for the context's life
     // chunkset mirror (decds_chunkset_new, decds_repairing_chunkset_repair): a pool of lanes, one
@@ -42,6 +44,8 @@ struct decds_ctx {
 
 // at least `bytes` of the context's host-path scratch (caller holds ctx->host_mu)
 hipError_t decds_ctx_scratch(decds_ctx *ctx, size_t bytes, uint8_t **out);
+// at least `bytes` of the context's small page-locked host area (caller holds ctx->host_mu)
+hipError_t decds_ctx_host_small(decds_ctx *ctx, size_t bytes, uint8_t **out);
 void decds_lanes_destroy(decds_ctx *ctx);  // chunkset.cpp
 
 int decds_set_error(int code, const char *fmt, ...);
