@@ -166,8 +166,8 @@ int finish_call(decds_ctx *ctx, Pipe &pp, int rc) {
         ctx->out_ring.abandon();
         ctx->in_ring.abandon();
     }
-    // the pipe's streams are drained and are destroyed when the call returns: no ring piece may keep
-    // an event recorded on them for the next call to wait on
+    // the pipe's streams are drained: no ring piece keeps an event of this call for the next call (on
+    // this context or, through the library's shared rings, another) to wait on
     ctx->in_ring.retire();
     ctx->out_ring.retire();
     return rc;
