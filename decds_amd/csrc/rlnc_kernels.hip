@@ -1044,7 +1044,10 @@ constexpr size_t DEC_WT_MAX_N = 2;
 #ifndef DECDS_DEC_DW
 #define DECDS_DEC_DW 4  // decode lane-block width in dwords (4: 16 columns per lane)
 #endif
-template <uint32_t UNIT, int SAUX = 0>
+// DW: lane-block width of the one-tile form — DECDS_DEC_DW (16 columns), or 2 (8 columns: 512 tiles per
+// chunkset) for batches up to DECDS_DEC_NARROW_MAX_N, where a chunkset's 256 wide tiles leave one workgroup
+// per CU and its lookups run at half the CU's LDS rate (phase trace r09r: 4.7-5 us of a 1-chunkset repair)
+template <uint32_t UNIT, int SAUX = 0, int DW = DECDS_DEC_DW>
 __global__ __launch_bounds__(WG, DECDS_DEC_WAVES) __attribute__((amdgpu_waves_per_eu(DECDS_DEC_WAVES, DECDS_DEC_WAVES)))
 void rlnc_decode_kernel(const uint8_t *__restrict__ coded, size_t pitch, size_t n, const RepairPlan *__restrict__ plan,
                         uint8_t *__restrict__ dst, int32_t *__restrict__ status, const uint64_t *__restrict__ in_bases,
@@ -1053,7 +1056,6 @@ void rlnc_decode_kernel(const uint8_t *__restrict__ coded, size_t pitch, size_t 
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     tables_at_lds_zero();
     TailLds &s_tail = *reinterpret_cast<TailLds *>(lds + LDS_BYTES);
-    constexpr int DW = DECDS_DEC_DW;
     constexpr uint32_t T = TILES<DW>;
     static_assert(T % UNIT == 0, "a workgroup's tiles stay in one chunkset");
     constexpr uint32_t phase = 0;  // aligned decode loads measured slower (+3…+5 %, profiles/HISTORY.md §8)
@@ -1068,6 +1070,7 @@ void rlnc_decode_kernel(const uint8_t *__restrict__ coded, size_t pitch, size_t 
         if (gridDim.x % (8 * R) == 0) u = (u / (8 * R)) * 8 * R + (u % 8) * R + (u / 8) % R;
     }
     const uint32_t t0 = u * UNIT, cs = t0 / T, tile0 = t0 % T;
+    PT_STAMP(0);
     if (cs >= n) return;
     const uint32_t *pw = reinterpret_cast<const uint32_t *>(plan + cs);
     const uint32_t w0 = __builtin_amdgcn_readfirstlane(pw[0]);
@@ -1101,6 +1104,7 @@ void rlnc_decode_kernel(const uint8_t *__restrict__ coded, size_t pitch, size_t 
     if (tile0 == 0) tail_reset(s_tail);
     build_tables<K, K>(lds, cw, poly);
     lds_barrier();
+    PT_STAMP(4);
     auto edge_pass = [&]() {
         // the workgroup of tile 0 makes one pass over the edge columns — after its tile, so that no
         // branch ahead of the tile's stream merges memory-counter pictures (which had the lookups wait for
@@ -1128,7 +1132,12 @@ void rlnc_decode_kernel(const uint8_t *__restrict__ coded, size_t pitch, size_t 
     // (realigning the piece stores — pieces start i bytes past alignment — through LDS staging or a DPP
     // wave shift measured 4-5 % slower / spilled: r02v/w)
     stream_range<K, K, DW, DECDS_PREFETCH_FIRST, false, DECDS_DEC_HB, SAUX>(tile0, tile0 + UNIT, phase, ibase, ioff, obase, ooff, x);
+    PT_STAMP(5);
     edge_pass();
+#ifdef DECDS_PHASE_TRACE
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    PT_STAMP(6);
+#endif
 }
 
 // 3 waves/SIMD for the decode sweep: at 4 (128 VGPRs) its loop spills, the tile counter's pending
@@ -1309,20 +1318,25 @@ void rlnc_decode_sweep_kernel(const uint8_t *__restrict__ coded, size_t pitch, s
 // At rank 10 the coefficient parts are unit vectors e_piv, so B = E·R = P and R^-1 = Pᵀ·E: row i
 // of the inverse is the combination part of the basis row whose pivot is column i.
 // Products are log-domain: x * f = exp[log x + log f], with log 0 = PLAN_LOG0 and exp zero from
-// index 510 on, so a product with a zero factor reads a zero and no term needs a mask. The basis
+// index 765 on, so a product with a zero factor reads a zero and no term needs a mask. The basis
 // is kept with its logs and every candidate's log is read up front, so a step is four dependent
 // LDS reads (projection, log of the reduced row, normalised row + basis update, basis logs); the
-// exp table comes from the host as a kernel argument.
+// exp table comes from the host as a kernel argument. Most chunksets never get
+// here: plan_fast inverts the first ten candidates directly when they are valid and independent.
 struct GfExpTable {
     uint32_t w[64];  // byte i = gen^i (i < 255), byte 255 = 0
 };
-constexpr uint32_t PLAN_LOG0 = 512;
-constexpr uint32_t PLAN_EXP_BYTES = 2 * PLAN_LOG0 + 4;  // largest index: log0 + log0
+// exp[i] = gen^(i mod 255) for i < 765 (three periods: a sum of up to three logs needs no reduction), zero
+// from 765 to the largest index, log0 + 255 + log0 (plan_fast's unreduced pivot-row products)
+constexpr uint32_t PLAN_LOG0 = 1024;
+constexpr uint32_t PLAN_EXP_VALID = 3 * 255;
+constexpr uint32_t PLAN_EXP_BYTES = 2 * PLAN_LOG0 + 256;
 // the plan's LDS scratch: exp / log tables and the logs of every coded row's coding vector
 struct PlanLds {
-    uint8_t exp[(PLAN_EXP_BYTES + 15) & ~15u];
+    uint8_t exp[PLAN_EXP_BYTES];
     uint16_t log[256];
     uint16_t lcv[N * 16];  // log of byte c of row r's coding vector at r * 16 + c
+    uint8_t cv[N * 16];    // byte c of row r's coding vector at r * 16 + c
 };
 
 // LDS visibility among the lanes of one wave: its LDS operations complete in order, so waiting for
@@ -1338,6 +1352,80 @@ __device__ __forceinline__ void wave_lds_sync() {
 #ifndef DECDS_STUDY_PLAN
 #define DECDS_STUDY_PLAN 0  // timing studies of the plan (1: no elimination, 2: no coding-vector loads)
 #endif
+#ifndef DECDS_PLAN_FAST
+#define DECDS_PLAN_FAST 1  // 0: the incremental elimination for every chunkset (A/B builds)
+#endif
+// The plan's fast path, for the common case: the first ten candidates in arrival order are valid and
+// independent, so the rank test accepts exactly them (chunkset.rs:177-183) and every later candidate
+// is "ready to repair". Their inverse is then found by Gauss-Jordan elimination on the augmented
+// matrix [R | I] column by column — row s (after a swap when its entry is zero) is the pivot of column
+// s and column s is cleared from all nine other rows at once — so a column costs two dependent LDS
+// round trips (the products exp[log row + log factor], then the logs of the updated rows) where the
+// incremental form needs five per accepted row. A column without a pivot means the ten rows are
+// dependent: false, and the caller runs the incremental form, which decides which rows are accepted.
+// Lane c < 20 holds column c of every row; the factors are the rows' logs at lane s (readlane).
+__device__ __forceinline__ bool plan_fast(uint32_t lane, uint32_t my_cand, const PlanLds &sl, RepairPlan *pl,
+                                          int32_t *__restrict__ status, size_t cs, int32_t *verdict) {
+    const uint8_t *s_exp = sl.exp;
+    const uint16_t *s_log = sl.log;
+    const bool col = lane < K;
+    uint32_t M[K], LM[K];
+    const uint32_t c = col ? lane : 0u;
+#pragma unroll
+    for (int i = 0; i < (int)K; i++) {
+        const uint32_t r = __builtin_amdgcn_readlane(my_cand, i);  // < N (checked by the caller)
+        const uint32_t v = sl.cv[r * 16 + c];
+        M[i] = col ? v : (lane == K + i ? 1u : 0u);
+    }
+#pragma unroll
+    for (int i = 0; i < (int)K; i++) LM[i] = s_log[M[i]];
+#pragma unroll
+    for (int s = 0; s < (int)K; s++) {
+        uint32_t f[K];
+#pragma unroll
+        for (int i = 0; i < (int)K; i++) f[i] = __builtin_amdgcn_readlane(LM[i], s);
+        if (f[s] == PLAN_LOG0) {  // zero pivot: swap in the first later row with a nonzero entry
+            int q = -1;
+#pragma unroll
+            for (int j = s + 1; j < (int)K; j++)
+                if (q < 0 && f[j] != PLAN_LOG0) q = j;
+            if (q < 0) return false;  // no pivot: the ten rows are dependent
+#pragma unroll
+            for (int j = s + 1; j < (int)K; j++)
+                if (j == q) {
+                    const uint32_t m = M[s], lm = LM[s], ff = f[s];
+                    M[s] = M[j], LM[s] = LM[j], f[s] = f[j];
+                    M[j] = m, LM[j] = lm, f[j] = ff;
+                }
+        }
+        // row i -= (row i's entry / pivot) * pivot row, row s /= pivot: log row s + (255 - log pivot)
+        // [+ log of row i's entry], the uniform part summed on the scalar unit; unreduced, every index
+        // stays below PLAN_EXP_BYTES (a nonzero product below 765, one with a zero entry or factor at
+        // log0 or above, where the table reads zero), so no term needs a mask or a reduction
+        const uint32_t u = 255u - f[s];
+#pragma unroll
+        for (int i = 0; i < (int)K; i++) M[i] = i == s ? (uint32_t)s_exp[LM[s] + u] : M[i] ^ (uint32_t)s_exp[LM[s] + (u + f[i])];
+        if (s + 1 < (int)K) {
+#pragma unroll
+            for (int i = 0; i < (int)K; i++) LM[i] = s_log[M[i]];
+        }
+    }
+    // row s is now [e_s | row s of the inverse]: lane 10 + k writes inverse entry (s, k), input-major
+    if (lane >= K && lane < 2 * K) {
+#pragma unroll
+        for (int s = 0; s < (int)K; s++) pl->inv[(lane - K) * K + s] = (uint8_t)M[s];
+    }
+    if (lane < K) pl->sel[lane] = (uint8_t)my_cand;
+    if (lane == 0) {
+        pl->rank = (uint8_t)K;
+        if (status) status[cs] = 0;
+    }
+    // verdicts: accepted (0) for the ten, "ready to repair" (3) for the later ones up to the list's end
+    const uint64_t ends = __ballot(lane < N && my_cand >= N) | (1ull << N);
+    const uint32_t end = (uint32_t)__builtin_ctzll(ends & ~((1ull << K) - 1));
+    *verdict = lane < K ? 0 : (lane < end ? 3 : -1);
+    return true;
+}
 struct NoHook {
     __device__ __forceinline__ void operator()() const {}
 };
@@ -1362,7 +1450,7 @@ __device__ __forceinline__ int32_t plan_wave(const uint8_t *__restrict__ coded, 
     uint8_t *s_exp = sl.exp;
     uint16_t *s_log = sl.log, *s_lcv = sl.lcv;
     {
-        // exp[i] = gen^i for i < 510 (doubled: a sum of two logs needs no reduction), zeros after
+        // exp[i] = gen^(i mod 255) for i < 765, zeros after (PLAN_EXP_BYTES)
         const uint32_t e4 = tab.w[lane];  // exp[4 lane .. 4 lane + 3]
 #pragma unroll
         for (uint32_t q = 0; q < 4; q++) {
@@ -1370,14 +1458,30 @@ __device__ __forceinline__ int32_t plan_wave(const uint8_t *__restrict__ coded, 
             if (i < 255) {
                 s_exp[i] = (uint8_t)v;
                 s_exp[i + 255] = (uint8_t)v;
+                s_exp[i + 510] = (uint8_t)v;
                 s_log[v] = (uint16_t)i;
             }
         }
-        for (uint32_t w = 512 / 4 + lane; w < PLAN_EXP_BYTES / 4; w += 64) reinterpret_cast<uint32_t *>(s_exp)[w] = 0;
-        if (lane < 2) s_exp[510 + lane] = 0;
+        for (uint32_t w = 768 / 4 + lane; w < PLAN_EXP_BYTES / 4; w += 64) reinterpret_cast<uint32_t *>(s_exp)[w] = 0;
+        if (lane < 3) s_exp[PLAN_EXP_VALID + lane] = 0;
         if (lane == 0) s_log[0] = PLAN_LOG0;
+        if (col) {
+#pragma unroll
+            for (int r = 0; r < (int)N; r++) sl.cv[r * 16 + lane] = (uint8_t)rowcv[r];
+        }
     }
     if constexpr (WAVE_SYNC) wave_lds_sync(); else __syncthreads();
+    PT_STAMP(1);
+#if DECDS_PLAN_FAST && DECDS_STUDY_PLAN == 0
+    if (!__ballot(lane < K && my_cand >= N)) {  // the first ten candidates exist
+        int32_t v = -1;
+        if (plan_fast(lane, my_cand, sl, pl, status, cs, &v)) {
+            PT_STAMP(2);
+            return v;
+        }
+    }
+#endif
+    // the incremental form: every coded row's logs
     if (col) {
 #pragma unroll
         for (int r = 0; r < (int)N; r++) s_lcv[r * 16 + lane] = s_log[rowcv[r]];
@@ -1496,9 +1600,10 @@ __device__ __forceinline__ uint32_t table_coeffs_imaj_lds(const uint8_t *M) {
 // wave 0 replays the rank test and inverts the accepted coding vectors (plan_wave, into LDS) while
 // the other waves wait at the barrier; the workgroup of tile 0 also writes the plan, the verdicts and
 // the status to memory, as rlnc_plan_kernel would. Every workgroup of a chunkset computes the same
-// plan (about 256 per chunkset: the plan's few microseconds of one wave, in parallel, against a
-// second launch and its plan round trip through memory). Same bytes as plan + decode.
-template <int SAUX = 0>
+// plan (256 per chunkset, 512 with 8-column tiles: the plan's few microseconds of one wave, in
+// parallel, against a second launch and its plan round trip through memory). Same bytes as plan +
+// decode.
+template <int SAUX = 0, int DW = DECDS_DEC_DW>
 __global__ __launch_bounds__(WG, DECDS_DEC_WAVES) __attribute__((amdgpu_waves_per_eu(DECDS_DEC_WAVES, DECDS_DEC_WAVES)))
 void rlnc_plan_decode_kernel(const uint8_t *__restrict__ coded, size_t pitch, size_t n, const uint8_t *__restrict__ cand,
                              RepairPlan *__restrict__ plan, int8_t *__restrict__ verdicts, uint8_t *__restrict__ dst,
@@ -1509,7 +1614,7 @@ void rlnc_plan_decode_kernel(const uint8_t *__restrict__ coded, size_t pitch, si
     TailLds &s_tail = *reinterpret_cast<TailLds *>(lds + LDS_BYTES);
     PlanLds &s_plan = *reinterpret_cast<PlanLds *>(lds + LDS_BYTES + TAIL_LDS);
     RepairPlan &s_rp = *reinterpret_cast<RepairPlan *>(lds + LDS_BYTES + TAIL_LDS + sizeof(PlanLds));
-    constexpr uint32_t T = TILES<DECDS_DEC_DW>;
+    constexpr uint32_t T = TILES<DW>;
     constexpr uint32_t phase = 0;
     uint32_t u = blockIdx.x;
     if constexpr (DEC_XCD_RUN > 1) {  // runs of consecutive tiles per XCD, as rlnc_decode_kernel
@@ -1517,6 +1622,7 @@ void rlnc_plan_decode_kernel(const uint8_t *__restrict__ coded, size_t pitch, si
         if (gridDim.x % (8 * R) == 0) u = (u / (8 * R)) * 8 * R + (u % 8) * R + (u / 8) % R;
     }
     const uint32_t cs = u / T, tile0 = u % T;
+    PT_STAMP(0);
     if (cs >= n) return;
     const bool first = tile0 == 0;
     const uint8_t *ibase = coded + (size_t)cs * N * pitch;
@@ -1536,7 +1642,6 @@ void rlnc_plan_decode_kernel(const uint8_t *__restrict__ coded, size_t pitch, si
     uint32_t soff[K];
 #pragma unroll
     for (int k = 0; k < (int)K; k++) soff[k] = (uint32_t)((spec_sel[k] & 15u) * pitch + K);
-    constexpr int DW = DECDS_DEC_DW;
     Vec<DW> x[K];
     const uint32_t col0 = tile_col<DW, false>(tile0, tile0 + 1, 0);
     auto speculate = [&]() {
@@ -1550,6 +1655,7 @@ void rlnc_plan_decode_kernel(const uint8_t *__restrict__ coded, size_t pitch, si
     }
     if (first) tail_reset(s_tail);
     lds_barrier();
+    PT_STAMP(3);
     const uint32_t *pw = reinterpret_cast<const uint32_t *>(&s_rp);
     if (first && threadIdx.x < sizeof(RepairPlan) / 4)  // the plan, as rlnc_plan_kernel leaves it
         reinterpret_cast<uint32_t *>(plan + cs)[threadIdx.x] = pw[threadIdx.x];
@@ -1570,7 +1676,9 @@ void rlnc_plan_decode_kernel(const uint8_t *__restrict__ coded, size_t pitch, si
     if (!spec_ok || w0 != c0 || w1 != c1 || (w2 & 0xFFFFu) != c2) load_block<K, DW>(x, ibase, ioff, col0);  // misspeculated
     build_tables<K, K>(lds, tcw, poly);
     lds_barrier();
+    PT_STAMP(4);
     stream_range<K, K, DW, true, false, DECDS_DEC_HB, SAUX>(tile0, tile0 + 1, phase, ibase, ioff, obase, ooff, x);
+    PT_STAMP(5);
     if (first) {
         // the edge columns and get_decoded_data's cut, as rlnc_decode_kernel's edge pass
         for (uint32_t idx = threadIdx.x; idx < edge_cols<DW, false>(phase) * K; idx += WG) {
@@ -1588,6 +1696,10 @@ void rlnc_plan_decode_kernel(const uint8_t *__restrict__ coded, size_t pitch, si
         tail_scan_decoded(s_tail, lds, ibase, ioff, marker);
         tail_finish(s_tail, cs, status, info);
     }
+#ifdef DECDS_PHASE_TRACE
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    PT_STAMP(6);
+#endif
 }
 constexpr uint32_t PLAN_DEC_LDS = DEC_LDS + sizeof(PlanLds) + sizeof(RepairPlan);
 
@@ -1673,6 +1785,10 @@ hipError_t configure_kernels() {
     // launch — which may come from several caller threads at once (the coalesced ChunkSet::new)
     const void *rest[] = {reinterpret_cast<const void *>(rlnc_plan_kernel), reinterpret_cast<const void *>(rlnc_plan_decode_kernel<0>),
                           reinterpret_cast<const void *>(rlnc_plan_decode_kernel<STORE_SC1>),
+                          reinterpret_cast<const void *>(rlnc_plan_decode_kernel<0, 2>),
+                          reinterpret_cast<const void *>(rlnc_plan_decode_kernel<STORE_SC1, 2>),
+                          reinterpret_cast<const void *>(rlnc_decode_kernel<DEC_UNIT, 0, 2>),
+                          reinterpret_cast<const void *>(rlnc_decode_kernel<DEC_UNIT, STORE_SC1, 2>),
                           reinterpret_cast<const void *>(fill_random_words_kernel),
                           reinterpret_cast<const void *>(fill_random_bytes_kernel)};
     for (const void *f : rest) {
@@ -1691,6 +1807,10 @@ hipError_t configure_kernels() {
 #endif
 #ifndef DECDS_ENC_NT_MIN_N
 #define DECDS_ENC_NT_MIN_N 256
+#endif
+#ifndef DECDS_DEC_NARROW_MAX_N
+// the one-tile decode (and the fused plan + decode) with 8-column lane blocks up to this many chunksets
+#define DECDS_DEC_NARROW_MAX_N 2
 #endif
 #ifndef DECDS_PLAN_DECODE_MAX_N
 // decds_repair_batch: plan + decode as one launch up to this many chunksets. Every workgroup of the fused
@@ -1714,16 +1834,18 @@ struct Tunable {
 static const Tunable TUNABLES[] = {{"DECDS_DEC_SWEEP_MIN_N", DECDS_DEC_SWEEP_MIN_N},
                                    {"DECDS_ENC_SMALL_MAX_N", DECDS_ENC_SMALL_MAX_N},
                                    {"DECDS_ENC_NT_MIN_N", DECDS_ENC_NT_MIN_N},
-                                   {"DECDS_PLAN_DECODE_MAX_N", DECDS_PLAN_DECODE_MAX_N}};
+                                   {"DECDS_PLAN_DECODE_MAX_N", DECDS_PLAN_DECODE_MAX_N},
+                                   {"DECDS_DEC_NARROW_MAX_N", DECDS_DEC_NARROW_MAX_N}};
 constexpr int TUNE_DEC_SWEEP_MIN_N = 0, TUNE_ENC_SMALL_MAX_N = 1, TUNE_ENC_NT_MIN_N = 2, TUNE_PLAN_DECODE_MAX_N = 3,
-              N_TUNABLES = 4;
+              TUNE_DEC_NARROW_MAX_N = 4, N_TUNABLES = 5;
 static uint64_t tune_default(int k) {
     static const uint64_t d[N_TUNABLES] = {TUNABLES[0].initial(), TUNABLES[1].initial(), TUNABLES[2].initial(),
-                                           TUNABLES[3].initial()};
+                                           TUNABLES[3].initial(), TUNABLES[4].initial()};
     return d[k];
 }
 static std::atomic<uint64_t> &tune(int k) {
-    static std::atomic<uint64_t> v[N_TUNABLES] = {{tune_default(0)}, {tune_default(1)}, {tune_default(2)}, {tune_default(3)}};
+    static std::atomic<uint64_t> v[N_TUNABLES] = {{tune_default(0)}, {tune_default(1)}, {tune_default(2)}, {tune_default(3)},
+                                                  {tune_default(4)}};
     return v[k];
 }
 uint64_t set_tuning(const char *name, uint64_t value, bool set) {
@@ -1737,6 +1859,7 @@ uint64_t set_tuning(const char *name, uint64_t value, bool set) {
 static bool decode_sweeps(size_t n) { return n >= tune(TUNE_DEC_SWEEP_MIN_N).load(std::memory_order_relaxed); }
 static bool encode_small(size_t n) { return n <= tune(TUNE_ENC_SMALL_MAX_N).load(std::memory_order_relaxed); }
 static bool encode_nt(size_t n) { return n >= tune(TUNE_ENC_NT_MIN_N).load(std::memory_order_relaxed); }
+static bool decode_narrow(size_t n) { return n <= tune(TUNE_DEC_NARROW_MAX_N).load(std::memory_order_relaxed); }
 static bool plan_decode_fused(size_t n) {
     return n <= tune(TUNE_PLAN_DECODE_MAX_N).load(std::memory_order_relaxed) && !decode_sweeps(n);
 }
@@ -1871,14 +1994,14 @@ static hipError_t launch_decode_kernel(const LaunchGeom &geom, const uint8_t *co
     }
     constexpr uint32_t U = DEC_UNIT;
     if (hipError_t p_ = hip_launch_begin("rlnc_decode_kernel")) return p_;
-    const dim3 grid((uint32_t)(n * (TILES<DECDS_DEC_DW> / U)));
-    if (n <= DEC_WT_MAX_N)
-        hipLaunchKernelGGL((rlnc_decode_kernel<U, STORE_SC1>), grid, dim3(WG), DEC_LDS, stream, coded, pitch, n, pl, dst,
-                           status, in_bases, out_bases, poly, marker, info);
-    else
-        hipLaunchKernelGGL(rlnc_decode_kernel<U>, grid, dim3(WG), DEC_LDS, stream, coded, pitch, n, pl, dst, status,
-                           in_bases, out_bases, poly, marker, info);
-    return hipGetLastError();
+    const bool narrow = decode_narrow(n), wt = n <= DEC_WT_MAX_N;
+    const dim3 grid((uint32_t)(n * ((narrow ? TILES<2> : TILES<DECDS_DEC_DW>) / U)));
+    const void *fn = narrow ? (wt ? reinterpret_cast<const void *>(rlnc_decode_kernel<U, STORE_SC1, 2>)
+                                  : reinterpret_cast<const void *>(rlnc_decode_kernel<U, 0, 2>))
+                            : (wt ? reinterpret_cast<const void *>(rlnc_decode_kernel<U, STORE_SC1>)
+                                  : reinterpret_cast<const void *>(rlnc_decode_kernel<U>));
+    void *args[] = {&coded, &pitch, &n, &pl, &dst, &status, &in_bases, &out_bases, &poly, &marker, &info};
+    return hipLaunchKernel(fn, grid, dim3(WG), args, DEC_LDS, stream);
 }
 
 hipError_t launch_decode(const LaunchGeom &geom, const uint8_t *coded, size_t pitch, size_t n, const uint8_t *plan,
@@ -1903,15 +2026,16 @@ hipError_t launch_repair(const LaunchGeom &geom, const uint8_t *coded, size_t pi
     const GfExpTable &tab = exp_table(poly, gen);
     RepairPlan *pl = reinterpret_cast<RepairPlan *>(plan);
     uint32_t *inf = reinterpret_cast<uint32_t *>(info);
-    const dim3 grid((uint32_t)(n * TILES<DECDS_DEC_DW>));
     if (hipError_t p_ = hip_launch_begin("rlnc_plan_decode_kernel")) return p_;
-    if (n <= DEC_WT_MAX_N)
-        hipLaunchKernelGGL((rlnc_plan_decode_kernel<STORE_SC1>), grid, dim3(WG), PLAN_DEC_LDS, stream, coded, pitch, n, cand, pl,
-                           verdicts, dst, status, poly, marker, inf, tab);
-    else
-        hipLaunchKernelGGL((rlnc_plan_decode_kernel<0>), grid, dim3(WG), PLAN_DEC_LDS, stream, coded, pitch, n, cand, pl,
-                           verdicts, dst, status, poly, marker, inf, tab);
-    return hipGetLastError();
+    const bool narrow = decode_narrow(n), wt = n <= DEC_WT_MAX_N;
+    const dim3 grid((uint32_t)(n * (narrow ? TILES<2> : TILES<DECDS_DEC_DW>)));
+    const void *fn = narrow ? (wt ? reinterpret_cast<const void *>(rlnc_plan_decode_kernel<STORE_SC1, 2>)
+                                  : reinterpret_cast<const void *>(rlnc_plan_decode_kernel<0, 2>))
+                            : (wt ? reinterpret_cast<const void *>(rlnc_plan_decode_kernel<STORE_SC1>)
+                                  : reinterpret_cast<const void *>(rlnc_plan_decode_kernel<0>));
+    GfExpTable targ = tab;
+    void *args[] = {&coded, &pitch, &n, &cand, &pl, &verdicts, &dst, &status, &poly, &marker, &inf, &targ};
+    return hipLaunchKernel(fn, grid, dim3(WG), args, PLAN_DEC_LDS, stream);
 }
 
 const char *repair_kernel_name(size_t n) { return plan_decode_fused(n) ? "rlnc_plan_decode_kernel" : "rlnc_plan_kernel"; }

@@ -147,7 +147,8 @@ const char *decds_decode_kernel_name(size_t n_chunksets);
  * chunksets run 8-column tiles, twice as many workgroups), "DECDS_ENC_NT_MIN_N" (default 256: from
  * that many chunksets on the encode stores its coded rows non-temporal, below write-through) and
  * "DECDS_PLAN_DECODE_MAX_N" (default 2: decds_repair_batch runs plan + decode as one kernel,
- * rlnc_plan_decode_kernel, up to that many chunksets). Each starts from the environment variable
+ * rlnc_plan_decode_kernel, up to that many chunksets) and "DECDS_DEC_NARROW_MAX_N" (default 2: the
+ * one-tile decode, fused or not, runs 8-column tiles up to that many chunksets). Each starts from the environment variable
  * of its name (read once, at first use) or the default. set != 0 sets it (value UINT64_MAX: back to
  * that start value). Returns the value in force, UINT64_MAX for an unknown name. */
 uint64_t decds_tuning(const char *name, uint64_t value, int set);

@@ -45,14 +45,17 @@ def _tuning(name, value):
     return lib().decds_tuning(name.encode(), value, 1)
 
 
-@pytest.fixture(params=["tiles", "sweep"])
+@pytest.fixture(params=["tiles", "tiles8", "sweep"])
 def decode_form(request):
-    """Run a decoding test through both decode kernels whatever its batch size: one-tile workgroups
-    (rlnc_decode_kernel) and the persistent sweep (rlnc_decode_sweep_kernel), by the process-wide
-    threshold DECDS_DEC_SWEEP_MIN_N (decds_tuning; back to its start value afterwards)."""
+    """Run a decoding test through every decode kernel form whatever its batch size: one-tile workgroups
+    (rlnc_decode_kernel) with 16-column or 8-column lane blocks, and the persistent sweep
+    (rlnc_decode_sweep_kernel), by the process-wide thresholds DECDS_DEC_SWEEP_MIN_N and
+    DECDS_DEC_NARROW_MAX_N (decds_tuning; back to their start values afterwards)."""
     _tuning("DECDS_DEC_SWEEP_MIN_N", 1 if request.param == "sweep" else 1 << 62)
+    _tuning("DECDS_DEC_NARROW_MAX_N", 1 << 62 if request.param == "tiles8" else 0)
     yield request.param
     _tuning("DECDS_DEC_SWEEP_MIN_N", (1 << 64) - 1)
+    _tuning("DECDS_DEC_NARROW_MAX_N", (1 << 64) - 1)
 
 
 @pytest.fixture(params=["cols16", "cols16_nt", "cols8"])

@@ -293,7 +293,7 @@ def _check_plans_against_oracle(n, vecs, cand, st, v, pl):
                 for k in range(K):
                     s ^= o.gf_mul(int(inv[i, k]), int(m[k, j]))
                 assert s == (1 if i == j else 0), (c, i, j)
-    assert len(ranks) >= 8  # the draws cover most ranks
+    return ranks
 
 
 def test_repair_plan_fuzz_low_rank_and_repeats(ctx):
@@ -307,7 +307,79 @@ def test_repair_plan_fuzz_low_rank_and_repeats(ctx):
     verd = torch.empty(n * N, dtype=torch.int8, device="cuda")
     status = torch.full((n,), -7, dtype=torch.int32, device="cuda")
     codec.repair_plan_batch(ctx, coded, n, dev(cand), plan, verd, status)
-    _check_plans_against_oracle(n, vecs, cand, host(status), host(verd).reshape(n, N), host(plan).reshape(n, 128))
+    ranks = _check_plans_against_oracle(n, vecs, cand, host(status), host(verd).reshape(n, N), host(plan).reshape(n, 128))
+    assert len(ranks) >= 8  # the draws cover most ranks
+
+
+def _fast_path_inputs(n=128):
+    """chunksets whose first ten candidates are valid (the plan's Gauss-Jordan fast path, plan_fast):
+    permuted scaled unit vectors and sparse rows (zero pivots: row swaps at most columns), dense random
+    rows, rows over {0..3}, and a dependent or repeated row among the ten (the fast path gives up and
+    the incremental form decides); candidate lists of 10..16 ids whose tail ends at every position"""
+    rng = np.random.default_rng(0xFA57)
+    coded = torch.zeros(n * N * F, dtype=torch.uint8, device="cuda")
+    vecs = np.zeros((n, N, K), np.uint8)
+    cand = np.full((n, N), 0xFF, np.uint8)
+    for c in range(n):
+        kind = c % 6
+        if kind == 0:
+            v = np.zeros((N, K), np.uint8)
+            perm = rng.permutation(K)
+            v[np.arange(K), perm] = rng.integers(1, 256, K)
+            v[K:] = rng.integers(0, 256, (N - K, K))
+        elif kind == 1:
+            v = (rng.integers(1, 256, (N, K)) * (rng.random((N, K)) < 0.3)).astype(np.uint8)
+        elif kind == 2:
+            v = rng.integers(0, 256, (N, K), dtype=np.uint8)
+        elif kind == 3:
+            v = rng.integers(0, 4, (N, K), dtype=np.uint8)
+        else:
+            v = rng.integers(0, 256, (N, K), dtype=np.uint8)
+        order = rng.permutation(N)
+        if kind == 4:  # a row among the first ten = a combination of two earlier ones
+            i, j, t = sorted(rng.choice(K, 3, replace=False))
+            a, b = int(rng.integers(1, 256)), int(rng.integers(1, 256))
+            v[order[t]] = [o.gf_mul(a, int(x)) ^ o.gf_mul(b, int(y)) for x, y in zip(v[order[i]], v[order[j]])]
+        if kind == 5 and c % 12 == 5:  # a repeated id among the first ten
+            order[int(rng.integers(1, K))] = order[0]
+        vecs[c] = v
+        length = K + (c // 6) % (N - K + 1)
+        cand[c, :length] = order[:length]
+    host_rows = np.zeros((n * N, 16), np.uint8)
+    host_rows[:, :K] = vecs.reshape(n * N, K)
+    coded.view(n * N, F)[:, :16].copy_(dev(host_rows))
+    return coded, vecs, cand
+
+
+@pytest.mark.parametrize("form", ["plan_kernel", "fused"])
+def test_repair_plan_fast_path_matches_oracle(ctx, form):
+    """The plan's Gauss-Jordan fast path (first ten candidates valid; rlnc_kernels.hip plan_fast) in the plan
+    kernel and in the fused plan + decode: verdicts, rank, sel and the inverse equal the oracle decoder's on
+    row swaps, sparse and small-valued rows, lists of every length from 10, and first tens that are
+    dependent (handed to the incremental form)."""
+    from decds_amd._capi import lib
+    n = 128
+    coded, vecs, cand = _fast_path_inputs(n)
+    plan = torch.empty(n * 128, dtype=torch.uint8, device="cuda")
+    verd = torch.empty(n * N, dtype=torch.int8, device="cuda")
+    status = torch.full((n,), -7, dtype=torch.int32, device="cuda")
+    if form == "plan_kernel":
+        codec.repair_plan_batch(ctx, coded, n, dev(cand), plan, verd, status)
+        st = host(status)
+    else:
+        lib().decds_tuning(b"DECDS_PLAN_DECODE_MAX_N", 1 << 62, 1)
+        try:
+            assert lib().decds_repair_kernel_name(n) == b"rlnc_plan_decode_kernel"
+            out = torch.empty(n * CS, dtype=torch.uint8, device="cuda")
+            codec.repair_batch(ctx, coded, n, dev(cand), plan, verd, out, status)
+        finally:
+            lib().decds_tuning(b"DECDS_PLAN_DECODE_MAX_N", (1 << 64) - 1, 1)
+        st = host(status)
+        ready = st != 5
+        assert set(np.unique(st[ready]).tolist()) <= {6}  # zero payloads: no marker anywhere
+        st = np.where(ready, 0, st)
+    ranks = _check_plans_against_oracle(n, vecs, cand, st, host(verd).reshape(n, N), host(plan).reshape(n, 128))
+    assert K in ranks and len(ranks) >= 2  # ready chunksets, and dependent tens that stay below rank 10
 
 
 @pytest.fixture
@@ -337,14 +409,15 @@ def test_fused_repair_plans_match_oracle_on_the_fuzz(ctx, plan_decode_fused):
     ready = st != 5
     assert set(np.unique(st[ready]).tolist()) == {6}  # zero payloads: no marker anywhere
     st = np.where(ready, 0, st)
-    _check_plans_against_oracle(n, vecs, cand, st, host(verd).reshape(n, N), host(plan).reshape(n, 128))
+    ranks = _check_plans_against_oracle(n, vecs, cand, st, host(verd).reshape(n, N), host(plan).reshape(n, 128))
+    assert len(ranks) >= 8
 
 
 @pytest.mark.parametrize("n", [1, 2, 5, 16])
 def test_fused_repair_equals_plan_then_decode(ctx, n):
     """decds_repair_batch in one launch (rlnc_plan_decode_kernel, forced at every n) against the plan kernel then
-    the decode (the form above the threshold): plan bytes, verdicts, statuses, repair infos and every
-    repaired byte identical, and the repaired chunksets equal their sources. Candidates: shuffled full
+    the decode (the form above the threshold), each with 16- and 8-column lane blocks: plan bytes, verdicts,
+    statuses, repair infos and every repaired byte identical, and the repaired chunksets equal their sources. Candidates: shuffled full
     lists, exactly 10, 9 (not ready), a repeated id, and a dependent row among the first 10."""
     from decds_amd._capi import lib
     rng = np.random.default_rng(0xF05E + n)
@@ -369,30 +442,39 @@ def test_fused_repair_equals_plan_then_decode(ctx, n):
     coded = torch.empty(n * N * F, dtype=torch.uint8, device="cuda")
     codec.encode_batch(ctx, dev(data), n, dev(coeffs.reshape(-1)), coded)
     res = {}
+    # every form: fused / split, each with 16- and 8-column lane blocks (DECDS_DEC_NARROW_MAX_N)
     for form, limit in (("fused", 1 << 62), ("split", 0)):
-        lib().decds_tuning(b"DECDS_PLAN_DECODE_MAX_N", limit, 1)
-        try:
-            assert lib().decds_repair_kernel_name(n) == (b"rlnc_plan_decode_kernel" if form == "fused" else b"rlnc_plan_kernel")
-            plan = torch.full((n * 128,), 0xEE, dtype=torch.uint8, device="cuda")
-            verd = torch.full((n * N,), 99, dtype=torch.int8, device="cuda")
-            status = torch.full((n,), -7, dtype=torch.int32, device="cuda")
-            out = torch.zeros(n * CS, dtype=torch.uint8, device="cuda")
-            info = torch.zeros(n * 16, dtype=torch.uint8, device="cuda")
-            codec.repair_batch(ctx, coded, n, dev(cand), plan, verd, out, status, info=info)
-            res[form] = [host(t) for t in (plan, verd, status, out, info)]
-        finally:
-            lib().decds_tuning(b"DECDS_PLAN_DECODE_MAX_N", (1 << 64) - 1, 1)
-    f, sp = res["fused"], res["split"]
+        for cols, narrow in ((16, 0), (8, 1 << 62)):
+            lib().decds_tuning(b"DECDS_PLAN_DECODE_MAX_N", limit, 1)
+            lib().decds_tuning(b"DECDS_DEC_NARROW_MAX_N", narrow, 1)
+            try:
+                assert lib().decds_repair_kernel_name(n) == (b"rlnc_plan_decode_kernel" if form == "fused" else b"rlnc_plan_kernel")
+                plan = torch.full((n * 128,), 0xEE, dtype=torch.uint8, device="cuda")
+                verd = torch.full((n * N,), 99, dtype=torch.int8, device="cuda")
+                status = torch.full((n,), -7, dtype=torch.int32, device="cuda")
+                out = torch.zeros(n * CS, dtype=torch.uint8, device="cuda")
+                info = torch.zeros(n * 16, dtype=torch.uint8, device="cuda")
+                codec.repair_batch(ctx, coded, n, dev(cand), plan, verd, out, status, info=info)
+                res[form, cols] = [host(t) for t in (plan, verd, status, out, info)]
+            finally:
+                lib().decds_tuning(b"DECDS_PLAN_DECODE_MAX_N", (1 << 64) - 1, 1)
+                lib().decds_tuning(b"DECDS_DEC_NARROW_MAX_N", (1 << 64) - 1, 1)
+    sp = res["split", 16]
     st = sp[2]
-    assert np.array_equal(f[2], st) and np.array_equal(f[1], sp[1])
-    pf, ps = f[0].reshape(n, 128), sp[0].reshape(n, 128)
+    ps = sp[0].reshape(n, 128)
+    for key in (("fused", 16), ("fused", 8), ("split", 8)):
+        f = res[key]
+        assert np.array_equal(f[2], st) and np.array_equal(f[1], sp[1]), key
+        pf = f[0].reshape(n, 128)
+        for c in range(n):
+            assert pf[c, 10] == ps[c, 10], (key, c)                       # rank
+            if st[c] == 0:
+                assert np.array_equal(pf[c, :K], ps[c, :K]) and np.array_equal(pf[c, 16:116], ps[c, 16:116]), (key, c)
+                assert np.array_equal(f[3][c * CS:(c + 1) * CS], data[c * CS:(c + 1) * CS]), (key, c)
+                assert np.array_equal(f[4][c * 16:c * 16 + 14], sp[4][c * 16:c * 16 + 14]), (key, c)
     for c in range(n):
-        assert pf[c, 10] == ps[c, 10], c                       # rank
         if st[c] == 0:
-            assert np.array_equal(pf[c, :K], ps[c, :K]) and np.array_equal(pf[c, 16:116], ps[c, 16:116]), c
-            assert np.array_equal(f[3][c * CS:(c + 1) * CS], data[c * CS:(c + 1) * CS]), c
             assert np.array_equal(sp[3][c * CS:(c + 1) * CS], data[c * CS:(c + 1) * CS]), c
-            assert np.array_equal(f[4][c * 16:c * 16 + 14], sp[4][c * 16:c * 16 + 14]), c
     assert set(st.tolist()) <= {0, 5} and (st == 5).sum() == sum(1 for c in range(n) if c % 5 == 2)
 
 
