@@ -118,10 +118,12 @@ hipError_t ctx_pipe(decds_ctx *ctx, Pipe **out) {
 
 // commitment outputs of the encode pipeline (Blob::new: chunkset.rs:54-63 per chunkset)
 struct CommitOut {
-    uint8_t *roots;   // n x 32
-    uint8_t *proofs;  // n x 16 x PROOF_SIZE x 32
+    uint8_t *roots;      // n x 32
+    uint8_t *proofs;     // n x 16 x PROOF_SIZE x 32
     uint64_t first_id;
+    uint8_t *group_cvs;  // whole-blob digest: the range's full 1 MiB groups' subtree values (32 B each), or null
 };
+constexpr size_t BLOB_GROUP = (size_t)1 << 20;  // blob_group_kernel's unit: 1024 BLAKE3 chunks
 
 // Batch sizes of a host-path call over n chunksets. A pipeline over the three engines only overlaps
 // once its first batch is in and until its last one is out: the first H2D and the last D2H run with
@@ -189,23 +191,28 @@ int encode_range(decds_ctx *ctx, const uint8_t *blob, size_t blob_len, const uin
     // two small copies per batch held ring pieces, and the host thread waited on them while the direct
     // input copies of a page-locked blob could have run ahead (Blob::new of a page-locked 1 GiB blob
     // 69 ms against 41 from pageable memory, r09c)
-    uint8_t *h_roots = nullptr, *h_prf = nullptr;
+    // with group_cvs, the whole-blob digest's full 1 MiB groups are hashed on the device from each
+    // batch's uploaded inputs (blob_group_kernel) and come back with the commitment outputs
+    const size_t n_groups = cm && cm->group_cvs ? blob_len / BLOB_GROUP : 0;
+    uint8_t *h_roots = nullptr, *h_prf = nullptr, *h_gcv = nullptr;
     if (cm) {
-        hipError_t pe = decds_ctx_host_small(ctx, n * (32 + PRF), &h_roots);
+        hipError_t pe = decds_ctx_host_small(ctx, n * (32 + PRF) + n_groups * 32, &h_roots);
         if (pe) return decds_hip_error(pe, "hipHostMalloc (commitment outputs)");
         h_prf = h_roots + n * 32;
+        h_gcv = h_prf + n * PRF;
     }
     // the coding vectors of the whole range go over in one copy ahead of the first batch (160 bytes
     // per chunkset): staged per batch from pageable memory, each small copy held a ring piece and
     // stalled the host's run-ahead (blob encode 15-17 GiB/s against 29 with them registered, r02zd)
-    const size_t cv_all = align256(n * N * K);
+    const size_t cv_all = align256(n * N * K), gcv_all = align256(n_groups * 32);
     const size_t sz[5] = {align256(batch * CS), align256(batch * N * F), cm ? align256(batch * N * 32) : 0,
                           cm ? align256(batch * 32) : 0, cm ? align256(batch * PRF) : 0};
     const size_t per = sz[0] + sz[1] + sz[2] + sz[3] + sz[4];
-    uint8_t *base, *dcv, *din[SLOTS], *dout[SLOTS], *ddig[SLOTS], *drt[SLOTS], *dprf[SLOTS];
+    uint8_t *base, *dcv, *dgcv, *din[SLOTS], *dout[SLOTS], *ddig[SLOTS], *drt[SLOTS], *dprf[SLOTS];
     hipError_t e;
-    if ((e = decds_ctx_scratch(ctx, cv_all + SLOTS * per, &base))) return decds_hip_error(e, "hipMalloc");
+    if ((e = decds_ctx_scratch(ctx, cv_all + gcv_all + SLOTS * per, &base))) return decds_hip_error(e, "hipMalloc");
     dcv = base, base += cv_all;
+    dgcv = base, base += gcv_all;
     for (int i = 0; i < SLOTS; i++) {
         uint8_t **dst[5] = {&din[i], &dout[i], &ddig[i], &drt[i], &dprf[i]};
         for (int j = 0; j < 5; j++) *dst[j] = base, base += sz[j];
@@ -247,6 +254,11 @@ int encode_range(decds_ctx *ctx, const uint8_t *blob, size_t blob_len, const uin
         if ((rc = decds_encode_batch(ctx, din[k], nb, dcv + b0 * N * K, dout[k], F, pp.comp))) break;
         if (cm && (rc = decds_commit_batch(ctx, dout[k], F, nb, cm->first_id + b0, ddig[k], drt[k], dprf[k], pp.comp)))
             break;
+        if (n_groups && (e = launch_blob_groups(din[k], have / BLOB_GROUP, (cm->first_id * CS + off) / 1024,
+                                                dgcv + off / BLOB_GROUP * 32, pp.comp))) {
+            rc = decds_hip_error(e, "blob_group_kernel launch");
+            break;
+        }
         if ((e = hipEventRecord(pp.k_done[k], pp.comp))) {
             rc = decds_hip_error(e, "hipEventRecord");
             break;
@@ -257,10 +269,16 @@ int encode_range(decds_ctx *ctx, const uint8_t *blob, size_t blob_len, const uin
         pend = k, pend_b0 = b0, pend_nb = nb;
     }
     if (rc == DECDS_OK && pend >= 0) rc = issue_d2h(pend, pend_b0, pend_nb);
+    // the group values after the last batch's kernels (one stream: every earlier batch's too)
+    if (rc == DECDS_OK && n_groups &&
+        ((e = hipStreamWaitEvent(pp.d2h, pp.k_done[pend], 0)) ||
+         (e = hipMemcpyAsync(h_gcv, dgcv, n_groups * 32, hipMemcpyDeviceToHost, pp.d2h))))
+        rc = decds_hip_error(e, "D2H (blob digest groups)");
     rc = finish_call(ctx, pp, rc);
     if (rc == DECDS_OK && cm) {
         std::memcpy(cm->roots, h_roots, n * 32);
         std::memcpy(cm->proofs, h_prf, n * PRF);
+        if (n_groups) std::memcpy(cm->group_cvs, h_gcv, n_groups * 32);
     }
     return rc;
 }
@@ -1048,14 +1066,31 @@ int decds_blob_new(decds_ctx *const *ctxs, size_t n_ctx, const uint8_t *data, si
     }
     b->roots.resize(n * 32);
     b->cs_proofs.resize(n * N * PROOF_SIZE * 32);
-    // blob.rs:249 whole-blob BLAKE3 on host threads, beside the device work
+    // blob.rs:249 whole-blob BLAKE3. Above 1 MiB: the full 1 MiB groups' subtree values on the device,
+    // from the inputs each batch uploads anyway (blob_group_kernel, 1024 chunks per workgroup), the last
+    // partial group's on the host, and the host folds them (round 6; until then 16 host threads hashed
+    // the whole blob beside the device pipeline, competing with its staging copies for the CPUs). Up to
+    // 1 MiB: on the host.
+    static const bool host_digest = [] {  // DECDS_BLOB_DIGEST=host: the whole digest on host threads (A/B)
+        const char *v = std::getenv("DECDS_BLOB_DIGEST");
+        return v && !std::strcmp(v, "host");
+    }();
+    const size_t full_groups = len > BLOB_GROUP && !host_digest ? len / BLOB_GROUP : 0;
+    const bool part = full_groups && len % BLOB_GROUP;
+    std::vector<uint32_t> gcv((full_groups + part) * 8);
     std::thread dig([&] {
         const unsigned hw = std::thread::hardware_concurrency();
-        decds_blake3_parallel(data, len, b->digest, (int)std::min(16u, hw ? hw : 4u));
+        const int th = (int)std::min(16u, hw ? hw : 4u);
+        if (!full_groups)
+            decds_blake3_parallel(data, len, b->digest, th);
+        else if (part)
+            blake3_subtree_cv(data + full_groups * BLOB_GROUP, len - full_groups * BLOB_GROUP, full_groups * (BLOB_GROUP / 1024),
+                              &gcv[full_groups * 8], th);
     });
     int s = run_shards(ctxs, n_ctx, n, [&](decds_ctx *ctx, size_t lo, size_t hi) {
         const size_t l = std::min<uint64_t>(len, hi * CS) - lo * CS;
-        const CommitOut cm{b->roots.data() + lo * 32, b->cs_proofs.data() + lo * N * PROOF_SIZE * 32, lo};
+        const CommitOut cm{b->roots.data() + lo * 32, b->cs_proofs.data() + lo * N * PROOF_SIZE * 32, lo,
+                           full_groups ? reinterpret_cast<uint8_t *>(&gcv[lo * (CS / BLOB_GROUP) * 8]) : nullptr};
         return encode_range(ctx, data + lo * CS, l, coeffs + lo * N * K, b->coded + lo * N * F, 0, &cm);
     });
     dig.join();
@@ -1063,6 +1098,8 @@ int decds_blob_new(decds_ctx *const *ctxs, size_t n_ctx, const uint8_t *data, si
         delete b;
         return s;
     }
+    if (full_groups)
+        blake3_fold_root(reinterpret_cast<const uint32_t(*)[8]>(gcv.data()), full_groups + part, b->digest);
     // blob.rs:266-273: Merkle tree over the chunkset roots; every chunk carries its chunkset's path
     int depth = 0;
     while (((size_t)1 << depth) < n) depth++;

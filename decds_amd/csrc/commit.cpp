@@ -142,6 +142,34 @@ void full_piece_digest(uint64_t chunkset_id, uint64_t chunk_id, const uint8_t *d
     b3::parent(q[0], last, b3::ROOT, root);
     to_bytes(root, out);
 }
+
+// the chaining value of the BLAKE3 subtree of [p, p + len) from chunk `first` (not finalised), on up to
+// `threads` host threads
+void blake3_subtree_cv(const uint8_t *p, size_t len, uint64_t first, uint32_t cv[8], int threads) {
+    subtree_cv_par(p, len, first, false, cv, threads);
+}
+
+// blake3::hash of a message given as the chaining values of its consecutive aligned subtrees of 2^k
+// chunks each (the last one possibly smaller): pairwise PARENT levels, an odd last node carried up
+// unchanged — BLAKE3's left-balanced tree — and ROOT on the final parent; n >= 2
+void blake3_fold_root(const uint32_t (*cvs)[8], size_t n, uint8_t out[32]) {
+    std::vector<std::array<uint32_t, 8>> lvl(n);
+    for (size_t i = 0; i < n; i++)
+        for (int w = 0; w < 8; w++) lvl[i][w] = cvs[i][w];
+    while (lvl.size() > 2) {
+        std::vector<std::array<uint32_t, 8>> up((lvl.size() + 1) / 2);
+        for (size_t i = 0; i < up.size(); i++) {
+            if (2 * i + 1 < lvl.size())
+                b3::parent(lvl[2 * i].data(), lvl[2 * i + 1].data(), 0, up[i].data());
+            else
+                up[i] = lvl[2 * i];
+        }
+        lvl.swap(up);
+    }
+    uint32_t root[8];
+    b3::parent(lvl[0].data(), lvl[1].data(), b3::ROOT, root);
+    to_bytes(root, out);
+}
 }  // namespace decds
 
 extern "C" {

@@ -22,6 +22,8 @@ constexpr uint32_t LAST_BYTES = MSG_BYTES - FULL_CHUNKS * b3::CHUNK;  // 27
 static_assert(FULL_CHUNKS == 1024 && LAST_BYTES == 27, "BLAKE3 tree shape of a coded chunk message");
 
 constexpr uint32_t DG_WG = FULL_CHUNKS / 4;  // 256 threads per row, 4 consecutive chunks each
+constexpr uint32_t BLOB_GROUP_BYTES = FULL_CHUNKS * b3::CHUNK;  // 1 MiB: blob_group_kernel's unit
+static_assert((uint64_t)CS % BLOB_GROUP_BYTES == 0, "a chunkset is whole blob-digest groups");
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 // Digest of one coded row per 256-thread workgroup: thread t hashes chunks 4t .. 4t+3 one after the
@@ -42,26 +44,23 @@ __device__ __forceinline__ uint32_t dg_slot(uint32_t t, uint32_t piece) {
     return t * DG_STEP + 16 * (piece ^ ((t >> 1) & 7u));
 }
 
-__global__ __launch_bounds__(DG_WG) void chunk_digest_kernel(const uint8_t *__restrict__ coded, size_t pitch,
-                                                             uint64_t first_chunkset_id,
-                                                             const uint64_t *__restrict__ ids,
-                                                             uint8_t *__restrict__ digests) {
-    __shared__ __attribute__((aligned(16))) uint8_t slots[DG_WG * DG_STEP];  // 32 KiB; the fold reuses it
-    const uint32_t row = blockIdx.x;
-    const uint64_t cs_id = ids ? ids[2 * (size_t)row] : first_chunkset_id + row / N;
-    const uint64_t chunk_id = ids ? ids[2 * (size_t)row + 1] : cs_id * N + row % N;
-    const uint8_t *piece = coded + (size_t)row * pitch;
+// The 1024-chunk BLAKE3 subtree (chaining value, not finalised) of the message at byte `bias` of rs's
+// buffer (message byte m = buffer byte m + bias; a negative bias reads zeros before the buffer), chunk
+// counters counter0 + 0 .. 1023: thread t hashes chunks 4t .. 4t+3 as described above and the 256 subtree
+// values fold in LDS; the result is in cvs[0][0..7] of the returned LDS array for every thread. IDS:
+// chunk 0's block 0 starts with the two ids (chunk.rs:40-46), patched over the zeros read at bias -16.
+template <bool IDS>
+__device__ __forceinline__ const uint32_t (*subtree_1024(__amdgpu_buffer_rsrc_t rs, int32_t bias, uint64_t counter0,
+                                                        uint64_t cs_id, uint64_t chunk_id,
+                                                        uint8_t *slots))[8] {
     const uint32_t t = threadIdx.x, l = t & 63u, wb = t & ~63u;
-    // load k of this lane: segment of thread lt = wb + 8k + l/8, its 16-byte piece l % 8; message byte m
-    // is piece byte m - 16 (block 0 of chunk 0 reads offset -16: out of range, zeros, ids patched in)
-    const __amdgpu_buffer_rsrc_t rs =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(piece), 0, (int)F, 0x00020000);
+    // load k of this lane: segment of thread lt = wb + 8k + l/8, its 16-byte piece l % 8
     const uint32_t lt0 = wb + (l >> 3), lp = l & 7u;
     auto load_step = [&](u32x4 (&v)[8], uint32_t g) {  // step g: chunk 4 lt + g / 8, bytes 128 (g % 8) ..
 #pragma unroll
         for (uint32_t k = 0; k < 8; k++) {
             const uint32_t lt = lt0 + 8 * k;
-            const uint32_t off = (4 * lt + (g >> 3)) * b3::CHUNK + (g & 7u) * DG_STEP + 16 * lp - 16;
+            const uint32_t off = (4 * lt + (g >> 3)) * b3::CHUNK + (g & 7u) * DG_STEP + 16 * lp + (uint32_t)bias;
             v[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
         }
     };
@@ -73,7 +72,8 @@ __global__ __launch_bounds__(DG_WG) void chunk_digest_kernel(const uint8_t *__re
 #pragma unroll
         for (uint32_t k = 0; k < 8; k++) *reinterpret_cast<u32x4 *>(slots + dg_slot(lt0 + 8 * k, lp)) = pf[k];
         if (g + 1 < DG_STEPS) load_step(pf, g + 1);  // in flight across this step's compressions
-        const uint32_t st = g & 7u, a = g >> 3, c = 4 * t + a;
+        const uint32_t st = g & 7u, a = g >> 3;
+        const uint64_t c = counter0 + 4 * t + a;
         if (st == 0)
 #pragma unroll
             for (int i = 0; i < 8; i++) cv[i] = b3::K3.iv[i];
@@ -86,7 +86,7 @@ __global__ __launch_bounds__(DG_WG) void chunk_digest_kernel(const uint8_t *__re
                 const u32x4 v = *reinterpret_cast<const u32x4 *>(slots + dg_slot(t, 4 * kb + w));
                 mw[4 * w] = v.x, mw[4 * w + 1] = v.y, mw[4 * w + 2] = v.z, mw[4 * w + 3] = v.w;
             }
-            if (kb == 0 && g == 0) {  // chunk 0's block 0 starts with the two ids (chunk.rs:40-46)
+            if (IDS && kb == 0 && g == 0) {  // chunk 0's block 0 starts with the two ids (chunk.rs:40-46)
                 const bool c0 = t == 0;
                 mw[0] = c0 ? (uint32_t)cs_id : mw[0];
                 mw[1] = c0 ? (uint32_t)(cs_id >> 32) : mw[1];
@@ -125,7 +125,24 @@ __global__ __launch_bounds__(DG_WG) void chunk_digest_kernel(const uint8_t *__re
             for (int i = 0; i < 8; i++) cvs[t][i] = out[i];
         __syncthreads();
     }
-    if (t == 0) {
+    return cvs;
+}
+
+__global__ __launch_bounds__(DG_WG) void chunk_digest_kernel(const uint8_t *__restrict__ coded, size_t pitch,
+                                                             uint64_t first_chunkset_id,
+                                                             const uint64_t *__restrict__ ids,
+                                                             uint8_t *__restrict__ digests) {
+    __shared__ __attribute__((aligned(16))) uint8_t slots[DG_WG * DG_STEP];  // 32 KiB; the fold reuses it
+    const uint32_t row = blockIdx.x;
+    const uint64_t cs_id = ids ? ids[2 * (size_t)row] : first_chunkset_id + row / N;
+    const uint64_t chunk_id = ids ? ids[2 * (size_t)row + 1] : cs_id * N + row % N;
+    const uint8_t *piece = coded + (size_t)row * pitch;
+    // message byte m is piece byte m - 16 (block 0 of chunk 0 reads offset -16: out of range, zeros,
+    // ids patched in)
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(piece), 0, (int)F, 0x00020000);
+    const uint32_t(*cvs)[8] = subtree_1024<true>(rs, -16, 0, cs_id, chunk_id, slots);
+    if (threadIdx.x == 0) {
         // last chunk: LAST_BYTES message bytes = the piece's final 27 bytes, one partial block
         uint32_t m[16], last[8], root[8], left[8];
 #pragma unroll
@@ -144,6 +161,21 @@ __global__ __launch_bounds__(DG_WG) void chunk_digest_kernel(const uint8_t *__re
 #pragma unroll
         for (int i = 0; i < 8; i++) d[i] = root[i];
     }
+}
+
+// Blob::new's whole-blob digest (blake3::hash(&data), blob.rs:249), group part: workgroup g hashes the
+// 1 MiB at data + g MiB — BLAKE3 chunks first_chunk + 1024 g .. + 1023, all full — into its 1024-chunk
+// subtree chaining value at cvs + 32 g. A chunkset is 10 such groups, so groups never straddle the
+// batches or shards of the blob paths; the host folds the groups' values (and the last partial group's,
+// hashed on the host) pairwise into the root (decds_blob_new).
+__global__ __launch_bounds__(DG_WG) void blob_group_kernel(const uint8_t *__restrict__ data, uint64_t first_chunk,
+                                                           uint8_t *__restrict__ cvs_out) {
+    __shared__ __attribute__((aligned(16))) uint8_t slots[DG_WG * DG_STEP];
+    const uint32_t g = blockIdx.x;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint8_t *>(data + (size_t)g * BLOB_GROUP_BYTES), 0, (int)BLOB_GROUP_BYTES, 0x00020000);
+    const uint32_t(*cvs)[8] = subtree_1024<false>(rs, 0, first_chunk + (uint64_t)g * FULL_CHUNKS, 0, 0, slots);
+    if (threadIdx.x < 8) reinterpret_cast<uint32_t *>(cvs_out + (size_t)g * 32)[threadIdx.x] = cvs[0][threadIdx.x];
 }
 
 // Digest of each coded row from the fused encode's 256 aligned 4-chunk subtree values
@@ -298,13 +330,22 @@ __global__ __launch_bounds__(64) void validate_kernel(const uint8_t *__restrict_
 
 hipError_t configure_commit_kernels() {
     const void *fns[] = {reinterpret_cast<const void *>(chunk_digest_kernel), reinterpret_cast<const void *>(chunkset_merkle_kernel),
-                         reinterpret_cast<const void *>(commit_fold_kernel), reinterpret_cast<const void *>(validate_kernel)};
+                         reinterpret_cast<const void *>(commit_fold_kernel), reinterpret_cast<const void *>(validate_kernel),
+                         reinterpret_cast<const void *>(blob_group_kernel)};
     for (const void *f : fns) {
         hipFuncAttributes a;
         hipError_t e = hipFuncGetAttributes(&a, f);
         if (e != hipSuccess) return e;
     }
     return hipSuccess;
+}
+
+hipError_t launch_blob_groups(const uint8_t *data, size_t n_groups, uint64_t first_chunk, uint8_t *cvs,
+                              hipStream_t stream) {
+    if (n_groups == 0) return hipSuccess;
+    if (hipError_t p_ = hip_launch_begin("blob_group_kernel")) return p_;
+    hipLaunchKernelGGL(blob_group_kernel, dim3((uint32_t)n_groups), dim3(DG_WG), 0, stream, data, first_chunk, cvs);
+    return hipGetLastError();
 }
 
 hipError_t launch_commit(const uint8_t *coded, size_t pitch, size_t n, uint64_t first_chunkset_id, uint8_t *digests,

@@ -75,6 +75,26 @@ def test_blob_new_matches_oracle(ctx):
     ctx2.close()
 
 
+@pytest.mark.parametrize("blob_len", [1, 1023, 1024, 1025, (1 << 20) - 1, 1 << 20, (1 << 20) + 1, 2 << 20,
+                                      (3 << 20) + 777, CS - 1, CS, CS + 1, 2 * CS + 12345, 4 * CS + (1 << 20) + 5])
+def test_blob_digest_every_group_shape(ctx, blob_len):
+    """Blob::new's whole-blob digest (blake3::hash(&data), blob.rs:249) at every shape of its split: up to
+    1 MiB on the host; above, full 1 MiB groups on the device (blob_group_kernel) plus the last partial
+    group on the host, folded on the host — against the oracle's BLAKE3, one and three contexts."""
+    data = o.fill_random(0xD16E57 + blob_len, blob_len)
+    n = -(-blob_len // CS)
+    coeffs = o.fill_random(0xC0DE + blob_len, n * N * K)
+    want = o.blake3(data)
+    assert decds_amd.Blob(ctx, data, coeffs).get_blob_header().get_blob_digest() == want
+    if n >= 3:
+        ctxs = [decds_amd.Context(0) for _ in range(2)]
+        try:
+            assert decds_amd.Blob([ctx] + ctxs, data, coeffs).get_blob_header().get_blob_digest() == want
+        finally:
+            for c in ctxs:
+                c.close()
+
+
 def test_repairing_blob_add_chunk_like_reference(ctx):
     # blob.rs:700-762
     _, _, blob = _blob(ctx, 2 * CS, 0x2B20)
