@@ -263,7 +263,8 @@ int decds_blob_repair_host_multi(decds_ctx *const *ctxs, size_t n_ctx, const uin
 /* ---- Blob (blob.rs:227-318) ------------------------------------------------------------------ */
 typedef struct decds_blob decds_blob;
 /* Blob::new(data) (blob.rs:244-285): empty -> DECDS_ERR_EMPTY_DATA_FOR_BLOB; whole-blob BLAKE3
- * digest (host threads); every chunkset RLNC-encoded with its commitment (digests, root, proofs) on
+ * digest (from the device: 1 MiB groups hashed from each batch's uploaded inputs, folded on the host;
+ * blobs up to 1 MiB on the host); every chunkset RLNC-encoded with its commitment (digests, root, proofs) on
  * the devices of ctxs (sharded as the _multi calls); blob-level Merkle tree over the chunkset roots
  * with each chunk's blob-level path appended to its proof. coeffs: n x 16 x 10 or NULL (drawn from
  * the library's RNG, as the reference draws from rand::rng()). */
