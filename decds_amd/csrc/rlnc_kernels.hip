@@ -804,6 +804,15 @@ void rlnc_encode_sweep_kernel(const uint8_t *__restrict__ src, size_t n, const u
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     tables_at_lds_zero();
     PT_STAMP(0);
+#ifdef DECDS_PHASE_TRACE
+    {  // where the workgroup runs: HW_ID (CU / SH / SE in bits 8-15) and the XCD
+        uint32_t hw, xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        PT_SET(6, hw);
+        PT_SET(7, xcc);
+    }
+#endif
     constexpr uint32_t T = TILES<DW>;
     uint32_t ioff[K], ooff[N];
 #pragma unroll

@@ -86,6 +86,26 @@ def main():
                    if (tile & (s[:, 1] - s[:, 0] > 200)).any() else None,
                    "span_us": round(float((s[:, 4].max() - t0) / 100.0), 2),
                    "algorithmic_frac_of_span": round(n * (CS + N * F) / ((s[:, 4].max() - t0) * 1e-8) / 8e12, 4)}
+            if (s[:, 6] != 0).any():  # placement (HW_ID / XCC_ID, trace builds that record them)
+                key = (s[:, 7] << 16) | ((s[:, 6] >> 8) & 0xFF)
+                fin = us(3)
+                tiles_wg = s[:, 5]
+                pair_dt, pair_dfin, lone = [], [], 0
+                for k in np.unique(key[tile]):
+                    m = np.nonzero(tile & (key == k))[0]
+                    if len(m) == 2:
+                        pair_dt.append(abs(int(tiles_wg[m[0]]) - int(tiles_wg[m[1]])))
+                        pair_dfin.append(abs(float(fin[m[0]] - fin[m[1]])))
+                    else:
+                        lone += 1
+                rec["placement"] = {
+                    "cus": int(len(np.unique(key[tile]))), "cus_not_two_wgs": lone,
+                    "pair_tile_diff_hist": {int(v): int(c) for v, c in zip(*np.unique(pair_dt, return_counts=True))},
+                    "pair_finish_diff_us_p50_90_max": pct(pair_dfin, (50, 90, 100)),
+                    "finish_us_by_xcd_p50": {int(x): round(float(np.median(fin[tile & (s[:, 7] == x)])), 2)
+                                             for x in np.unique(s[tile, 7])},
+                    "tiles_by_xcd_mean": {int(x): round(float(np.mean(tiles_wg[tile & (s[:, 7] == x)])), 2)
+                                          for x in np.unique(s[tile, 7])}}
             print(json.dumps(rec), flush=True)
 
 
