@@ -781,7 +781,7 @@ constexpr int STORE_SC1 = 16, STORE_NT = 2;
 // 100 MHz real-time counter at its phases — entry, edge pass done, first tables ready, last lookups
 // issued, stores drained — plus its tile count (vector stores; decds_debug_phase_trace copies them out).
 #ifdef DECDS_PHASE_TRACE
-constexpr uint32_t PT_WGS = 8192, PT_SLOTS = 24;  // slots 8 + k: tile k's tables ready (k < 16)
+constexpr uint32_t PT_WGS = 8192, PT_SLOTS = 32;  // slots 8 + k: tile k's tables ready (k < 16)
 __device__ uint64_t g_phase_trace[PT_WGS * PT_SLOTS];
 #define PT_SET(slot, v)                                                                   \
     do {                                                                                  \
@@ -900,7 +900,16 @@ void rlnc_encode_sweep_kernel(const uint8_t *__restrict__ src, size_t n, const u
     bool first = true;
 #pragma unroll 1
     do {
+#ifdef DECDS_PHASE_TRACE
+        if (first) {  // slot 24: the first tile's coefficient bytes are in; slot 25: its tables are built
+            asm volatile("s_waitcnt vmcnt(26)" ::: "memory");
+            PT_STAMP(24);
+        }
+#endif
         build_tables<K, N>(lds, cw, poly);
+#ifdef DECDS_PHASE_TRACE
+        if (first) PT_STAMP(25);
+#endif
         if constexpr (QUEUE) {
             // the counter's answer: at the first tile everything but its ten input loads and the 16
             // dropped stores, later everything but the previous tile's 16 stores (waited for whether

@@ -15,7 +15,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-PT_WGS, PT_SLOTS = 8192, 24
+PT_WGS, PT_SLOTS = 8192, 32
 
 
 def pct(v, qs=(0, 50, 90, 100)):
@@ -72,6 +72,8 @@ def main():
                    "tile_wgs": int(tile.sum()), "edge_or_idle_wgs": int(edge.sum()),
                    "entry_p0_50_90_100": pct(us(0)),
                    "edge_done": pct(us(1)[tile]),
+                   "coeffs_in": pct(us(24)[tile & (s[:, 24] > 0)]),
+                   "first_build_done": pct(us(25)[tile & (s[:, 25] > 0)]),
                    "tables_ready": pct(us(2)[tile]),
                    "lookups_done": pct(us(3)[tile]),
                    "drained": pct(us(4)[tile]),

@@ -15,7 +15,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-PT_WGS, PT_SLOTS = 8192, 24
+PT_WGS, PT_SLOTS = 8192, 32
 
 
 def main():
