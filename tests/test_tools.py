@@ -36,7 +36,7 @@ def test_study_builds_of_the_kernels_compile():
     src = os.path.join(ROOT, "decds_amd", "csrc", "rlnc_kernels.hip")
     for defs in (["-DDECDS_PHASE_TRACE=1"], ["-DDECDS_PHASE_TRACE=1", "-DDECDS_STUDY_NO_EDGE=1"],
                  ["-DDECDS_STUDY_PATTERN=1"], ["-DDECDS_STUDY_ALIGNED_PIECES=1"], ["-DDECDS_STUDY_ALIGNED_PIECES=3"],
-                 ["-DDECDS_STUDY_PLAN=1"], ["-DDECDS_STUDY_PLAN=2"]):
+                 ["-DDECDS_STUDY_PLAN=1"], ["-DDECDS_STUDY_PLAN=2"], ["-DDECDS_PLAN_FAST=0"]):
         r = subprocess.run([HIPCC, "--offload-arch=gfx950", "-std=c++17", "-I" + os.path.join(ROOT, "include"),
                             "-fsyntax-only"] + defs + [src], capture_output=True, text=True, timeout=300)
         assert r.returncode == 0, (defs, r.stderr[-1500:])
