@@ -115,6 +115,9 @@ def test_decode_kernel_by_batch_size():
             assert tune("DECDS_ENC_SMALL_MAX_N", 0, 0) == 2
         if "DECDS_ENC_NT_MIN_N" not in os.environ:
             assert tune("DECDS_ENC_NT_MIN_N", 0, 0) == 256
+        for knob, default in (("DECDS_PLAN_DECODE_MAX_N", 2), ("DECDS_DEC_NARROW_MAX_N", 2)):
+            if knob not in os.environ:
+                assert tune(knob, 0, 0) == default, knob
         assert tune("ENC_NT_MIN_N", 5) == 5 and tune("DECDS_ENC_NT_MIN_N", reset) != 5
         assert tune("NO_SUCH_KNOB", 5) == reset
     finally:
