@@ -351,12 +351,13 @@ def _fast_path_inputs(n=128):
     return coded, vecs, cand
 
 
-@pytest.mark.parametrize("form", ["plan_kernel", "fused"])
+@pytest.mark.parametrize("form", ["plan_kernel", "fused", "fused_pairs"])
 def test_repair_plan_fast_path_matches_oracle(ctx, form):
     """The plan's Gauss-Jordan fast path (first ten candidates valid; rlnc_kernels.hip plan_fast) in the plan
-    kernel and in the fused plan + decode: verdicts, rank, sel and the inverse equal the oracle decoder's on
-    row swaps, sparse and small-valued rows, lists of every length from 10, and first tens that are
-    dependent (handed to the incremental form)."""
+    kernel and in the fused plan + decode — one 128-chunkset launch (16-column tiles) or 64 launches of two
+    (the default repair of small batches, 8-column tiles): verdicts, rank, sel and the inverse equal the oracle
+    decoder's on row swaps, sparse and small-valued rows, lists of every length from 10, and first tens that
+    are dependent (handed to the incremental form)."""
     from decds_amd._capi import lib
     n = 128
     coded, vecs, cand = _fast_path_inputs(n)
@@ -366,6 +367,16 @@ def test_repair_plan_fast_path_matches_oracle(ctx, form):
     if form == "plan_kernel":
         codec.repair_plan_batch(ctx, coded, n, dev(cand), plan, verd, status)
         st = host(status)
+    elif form == "fused_pairs":
+        assert lib().decds_repair_kernel_name(2) == b"rlnc_plan_decode_kernel"
+        out = torch.empty(2 * CS, dtype=torch.uint8, device="cuda")
+        cand_d = dev(cand)
+        for c in range(0, n, 2):  # rows of chunksets c, c + 1: the coded buffer's view from row 16c
+            codec.repair_batch(ctx, coded[c * N * F:], 2, cand_d[c:c + 2], plan[c * 128:], verd[c * N:], out, status[c:])
+        st = host(status)
+        ready = st != 5
+        assert set(np.unique(st[ready]).tolist()) <= {6}
+        st = np.where(ready, 0, st)
     else:
         lib().decds_tuning(b"DECDS_PLAN_DECODE_MAX_N", 1 << 62, 1)
         try:
